@@ -1,0 +1,66 @@
+"""Frozen SD-1.5 UNet / VAE-encoder / DDIM scheduler (PyTorch-ROCm side of the path)."""
+from .unet import UNet2DConditionModel, CrossAttention, CaptureComplete
+from .vae import AutoencoderKL
+from .scheduler import DDIMScheduler
+
+
+class StableDiffusionParts:
+    """The three pipeline members the hot path touches: ``unet``, ``vae``, ``scheduler``.
+
+    Stands in for ``StableDiffusionPipeline`` (reference ``optimize_token.py:38-40``);
+    the text encoder/tokenizer are frozen and unused by the path, so they are absent.
+    """
+
+    def __init__(self, unet, vae, scheduler):
+        self.unet = unet
+        self.vae = vae
+        self.scheduler = scheduler
+
+    def to(self, device):
+        self.unet.to(device)
+        self.vae.to(device)
+        return self
+
+
+TINY_CONFIG = dict(unet=dict(block_out_channels=(32, 64, 64, 64), cross_attention_dim=32),
+                   vae=dict(block_out_channels=(32, 32, 64, 64)))
+
+
+def build_sd15(seed=0, device="cpu", weights=None, config=None):
+    """Random-init SD-1.5 parts (seeded), or load a local diffusers-0.8.0 state dict.
+
+    ``weights`` may be a directory holding ``unet.safetensors``/``vae.safetensors`` or
+    ``.pt`` files (loaded with ``weights_only=True``).  ``config`` shrinks the
+    architecture (``TINY_CONFIG`` keeps SD-1.5's block structure at toy widths for
+    golden vectors and CPU tests).
+    """
+    import os
+    import torch
+    g = torch.random.fork_rng(devices=[])
+    with g:
+        torch.manual_seed(seed)
+        cfg = config or {}
+        unet = UNet2DConditionModel(**cfg.get("unet", {}))
+        vae = AutoencoderKL(**cfg.get("vae", {}))
+    if weights:
+        for name, mod in (("unet", unet), ("vae", vae)):
+            for ext in (".safetensors", ".pt", ".bin"):
+                p = os.path.join(weights, name + ext)
+                if os.path.exists(p):
+                    if ext == ".safetensors":
+                        from safetensors.torch import load_file
+                        sd = load_file(p)
+                    else:
+                        sd = torch.load(p, map_location="cpu", weights_only=True)
+                    if name == "vae":
+                        sd = {k: v for k, v in sd.items() if k.startswith(("encoder.", "quant_conv."))}
+                    mod.load_state_dict(sd, strict=True)
+                    break
+    sched = DDIMScheduler(beta_start=0.00085, beta_end=0.012, beta_schedule="scaled_linear",
+                          clip_sample=False, set_alpha_to_one=False)
+    sched.set_timesteps(50)
+    for m in (unet, vae):
+        m.eval()
+        for p in m.parameters():
+            p.requires_grad = False
+    return StableDiffusionParts(unet, vae, sched).to(device)

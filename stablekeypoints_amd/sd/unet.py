@@ -1,0 +1,364 @@
+"""Self-contained Stable-Diffusion-1.5 UNet (diffusers-0.8.0 module names) in plain PyTorch.
+
+The reference loads ``UNet2DConditionModel`` from diffusers 0.8.0 through
+``StableDiffusionPipeline.from_pretrained`` (reference
+``unsupervised_keypoints/optimize_token.py:38-40``).  diffusers is not available
+here, so this file restates the SD-1.5 UNet architecture with the same
+sub-module names, so a diffusers-0.8.0 ``state_dict`` loads with
+``load_state_dict(strict=True)``.  The UNet is frozen on the hot path and stays
+in PyTorch-ROCm (fp32); only the attention-capture path is replaced by HIP
+kernels (see ``stablekeypoints_amd/ptp_utils.py``).
+
+The hot-path hook walks ``model.named_children()`` for names containing "up"
+and patches modules whose class name is exactly ``CrossAttention``
+(reference ``ptp_utils.py:555-573``), so that class name and its attribute
+interface (``heads``, ``scale``, ``to_q``/``to_k``/``to_v``/``to_out``,
+``reshape_heads_to_batch_dim``, ``reshape_batch_dim_to_heads``) are kept.
+"""
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class CaptureComplete(Exception):
+    """Raised by a patched attention when its controller has every map it needs.
+
+    The reference discards the UNet output of a capture pass
+    (``ptp_utils.py:246-252``), and nothing after the 4th captured layer feeds the
+    loss, so the forward may stop there (SURVEY.md §7 "UNet early exit").
+    """
+
+
+# --------------------------------------------------------------------------- attention
+class CrossAttention(nn.Module):
+    """diffusers-0.8.0 ``CrossAttention`` (bias-free q/k/v, ``to_out=[Linear, Dropout]``)."""
+
+    # "sdpa" routes the un-captured attention through torch SDPA; "math" is the
+    # literal einsum/softmax form of diffusers 0.8.0.
+    backend = "sdpa"
+
+    def __init__(self, query_dim, cross_attention_dim=None, heads=8, dim_head=64, dropout=0.0, bias=False):
+        super().__init__()
+        inner_dim = dim_head * heads
+        cross_attention_dim = cross_attention_dim if cross_attention_dim is not None else query_dim
+        self.scale = dim_head ** -0.5
+        self.heads = heads
+        self.to_q = nn.Linear(query_dim, inner_dim, bias=bias)
+        self.to_k = nn.Linear(cross_attention_dim, inner_dim, bias=bias)
+        self.to_v = nn.Linear(cross_attention_dim, inner_dim, bias=bias)
+        self.to_out = nn.ModuleList([nn.Linear(inner_dim, query_dim), nn.Dropout(dropout)])
+
+    def reshape_heads_to_batch_dim(self, tensor):
+        b, s, dim = tensor.shape
+        h = self.heads
+        return tensor.reshape(b, s, h, dim // h).permute(0, 2, 1, 3).reshape(b * h, s, dim // h)
+
+    def reshape_batch_dim_to_heads(self, tensor):
+        bh, s, d = tensor.shape
+        h = self.heads
+        return tensor.reshape(bh // h, h, s, d).permute(0, 2, 1, 3).reshape(bh // h, s, d * h)
+
+    def forward(self, x, context=None, mask=None):
+        context = x if context is None else context
+        q = self.reshape_heads_to_batch_dim(self.to_q(x))
+        k = self.reshape_heads_to_batch_dim(self.to_k(context))
+        v = self.reshape_heads_to_batch_dim(self.to_v(context))
+        out = attention_core(q, k, v, self.scale, mask, self.heads)
+        out = self.reshape_batch_dim_to_heads(out)
+        return self.to_out[1](self.to_out[0](out))
+
+
+def attention_core(q, k, v, scale, mask=None, heads=1):
+    """softmax(q kᵀ · scale) v over (B·H, S, D) tensors (diffusers-0.8.0 semantics)."""
+    if mask is None and CrossAttention.backend == "sdpa":
+        return F.scaled_dot_product_attention(q.unsqueeze(0), k.unsqueeze(0), v.unsqueeze(0), scale=scale)[0]
+    sim = torch.baddbmm(torch.empty(q.shape[0], q.shape[1], k.shape[1], dtype=q.dtype, device=q.device),
+                        q, k.transpose(1, 2), beta=0, alpha=scale)
+    if mask is not None:
+        b = mask.shape[0]
+        m = mask.reshape(b, -1)[:, None, :].repeat(heads, 1, 1)
+        sim = sim.masked_fill(~m, -torch.finfo(sim.dtype).max)
+    return torch.bmm(sim.softmax(dim=-1), v)
+
+
+class GEGLU(nn.Module):
+    def __init__(self, dim_in, dim_out):
+        super().__init__()
+        self.proj = nn.Linear(dim_in, dim_out * 2)
+
+    def forward(self, x):
+        x, gate = self.proj(x).chunk(2, dim=-1)
+        return x * F.gelu(gate)
+
+
+class FeedForward(nn.Module):
+    def __init__(self, dim, mult=4, dropout=0.0):
+        super().__init__()
+        inner = dim * mult
+        self.net = nn.ModuleList([GEGLU(dim, inner), nn.Dropout(dropout), nn.Linear(inner, dim)])
+
+    def forward(self, x):
+        for m in self.net:
+            x = m(x)
+        return x
+
+
+class BasicTransformerBlock(nn.Module):
+    def __init__(self, dim, n_heads, d_head, cross_attention_dim):
+        super().__init__()
+        self.attn1 = CrossAttention(dim, heads=n_heads, dim_head=d_head)
+        self.ff = FeedForward(dim)
+        self.attn2 = CrossAttention(dim, cross_attention_dim=cross_attention_dim, heads=n_heads, dim_head=d_head)
+        self.norm1 = nn.LayerNorm(dim)
+        self.norm2 = nn.LayerNorm(dim)
+        self.norm3 = nn.LayerNorm(dim)
+
+    def forward(self, h, context=None):
+        h = self.attn1(self.norm1(h)) + h
+        h = self.attn2(self.norm2(h), context=context) + h
+        h = self.ff(self.norm3(h)) + h
+        return h
+
+
+class Transformer2DModel(nn.Module):
+    """SD-1.x spatial transformer (conv proj_in/proj_out, one BasicTransformerBlock)."""
+
+    def __init__(self, num_attention_heads, attention_head_dim, in_channels, cross_attention_dim, norm_num_groups=32):
+        super().__init__()
+        inner = num_attention_heads * attention_head_dim
+        self.norm = nn.GroupNorm(norm_num_groups, in_channels, eps=1e-6, affine=True)
+        self.proj_in = nn.Conv2d(in_channels, inner, 1)
+        self.transformer_blocks = nn.ModuleList(
+            [BasicTransformerBlock(inner, num_attention_heads, attention_head_dim, cross_attention_dim)])
+        self.proj_out = nn.Conv2d(inner, in_channels, 1)
+
+    def forward(self, x, encoder_hidden_states=None):
+        b, c, hh, ww = x.shape
+        res = x
+        x = self.proj_in(self.norm(x))
+        inner = x.shape[1]
+        x = x.permute(0, 2, 3, 1).reshape(b, hh * ww, inner)
+        for blk in self.transformer_blocks:
+            x = blk(x, context=encoder_hidden_states)
+        x = x.reshape(b, hh, ww, inner).permute(0, 3, 1, 2)
+        return self.proj_out(x) + res
+
+
+# --------------------------------------------------------------------------- resnets
+class ResnetBlock2D(nn.Module):
+    def __init__(self, in_channels, out_channels=None, temb_channels=1280, groups=32, eps=1e-5):
+        super().__init__()
+        out_channels = in_channels if out_channels is None else out_channels
+        self.norm1 = nn.GroupNorm(groups, in_channels, eps=eps, affine=True)
+        self.conv1 = nn.Conv2d(in_channels, out_channels, 3, 1, 1)
+        self.time_emb_proj = nn.Linear(temb_channels, out_channels) if temb_channels is not None else None
+        self.norm2 = nn.GroupNorm(groups, out_channels, eps=eps, affine=True)
+        self.dropout = nn.Dropout(0.0)
+        self.conv2 = nn.Conv2d(out_channels, out_channels, 3, 1, 1)
+        self.conv_shortcut = nn.Conv2d(in_channels, out_channels, 1) if in_channels != out_channels else None
+
+    def forward(self, x, temb=None):
+        h = self.conv1(F.silu(self.norm1(x)))
+        if temb is not None and self.time_emb_proj is not None:
+            h = h + self.time_emb_proj(F.silu(temb))[:, :, None, None]
+        h = self.conv2(self.dropout(F.silu(self.norm2(h))))
+        if self.conv_shortcut is not None:
+            x = self.conv_shortcut(x)
+        return x + h
+
+
+class Downsample2D(nn.Module):
+    def __init__(self, channels, padding=1):
+        super().__init__()
+        self.padding = padding
+        self.conv = nn.Conv2d(channels, channels, 3, stride=2, padding=padding)
+
+    def forward(self, x):
+        if self.padding == 0:
+            x = F.pad(x, (0, 1, 0, 1), mode="constant", value=0)
+        return self.conv(x)
+
+
+class Upsample2D(nn.Module):
+    def __init__(self, channels):
+        super().__init__()
+        self.conv = nn.Conv2d(channels, channels, 3, padding=1)
+
+    def forward(self, x, output_size=None):
+        if output_size is None:
+            x = F.interpolate(x, scale_factor=2.0, mode="nearest")
+        else:
+            x = F.interpolate(x, size=output_size, mode="nearest")
+        return self.conv(x)
+
+
+# --------------------------------------------------------------------------- blocks
+class CrossAttnDownBlock2D(nn.Module):
+    def __init__(self, in_ch, out_ch, temb, heads, ctx_dim, add_downsample):
+        super().__init__()
+        self.resnets = nn.ModuleList([ResnetBlock2D(in_ch if i == 0 else out_ch, out_ch, temb) for i in range(2)])
+        self.attentions = nn.ModuleList([Transformer2DModel(heads, out_ch // heads, out_ch, ctx_dim) for _ in range(2)])
+        self.downsamplers = nn.ModuleList([Downsample2D(out_ch)]) if add_downsample else None
+
+    def forward(self, h, temb, context):
+        outs = ()
+        for resnet, attn in zip(self.resnets, self.attentions):
+            h = attn(resnet(h, temb), encoder_hidden_states=context)
+            outs += (h,)
+        if self.downsamplers is not None:
+            h = self.downsamplers[0](h)
+            outs += (h,)
+        return h, outs
+
+
+class DownBlock2D(nn.Module):
+    def __init__(self, in_ch, out_ch, temb, add_downsample):
+        super().__init__()
+        self.resnets = nn.ModuleList([ResnetBlock2D(in_ch if i == 0 else out_ch, out_ch, temb) for i in range(2)])
+        self.downsamplers = nn.ModuleList([Downsample2D(out_ch)]) if add_downsample else None
+
+    def forward(self, h, temb, context=None):
+        outs = ()
+        for resnet in self.resnets:
+            h = resnet(h, temb)
+            outs += (h,)
+        if self.downsamplers is not None:
+            h = self.downsamplers[0](h)
+            outs += (h,)
+        return h, outs
+
+
+class _UpBase(nn.Module):
+    def _make_resnets(self, in_ch, out_ch, prev_ch, temb):
+        res = []
+        for i in range(3):
+            skip = in_ch if i == 2 else out_ch
+            rin = prev_ch if i == 0 else out_ch
+            res.append(ResnetBlock2D(rin + skip, out_ch, temb))
+        return nn.ModuleList(res)
+
+
+class CrossAttnUpBlock2D(_UpBase):
+    def __init__(self, in_ch, out_ch, prev_ch, temb, heads, ctx_dim, add_upsample):
+        super().__init__()
+        self.resnets = self._make_resnets(in_ch, out_ch, prev_ch, temb)
+        self.attentions = nn.ModuleList([Transformer2DModel(heads, out_ch // heads, out_ch, ctx_dim) for _ in range(3)])
+        self.upsamplers = nn.ModuleList([Upsample2D(out_ch)]) if add_upsample else None
+
+    def forward(self, h, res_tuple, temb, context, upsample_size=None):
+        for resnet, attn in zip(self.resnets, self.attentions):
+            skip = res_tuple[-1]
+            res_tuple = res_tuple[:-1]
+            h = torch.cat([h, skip], dim=1)
+            h = attn(resnet(h, temb), encoder_hidden_states=context)
+        if self.upsamplers is not None:
+            h = self.upsamplers[0](h, upsample_size)
+        return h
+
+
+class UpBlock2D(_UpBase):
+    def __init__(self, in_ch, out_ch, prev_ch, temb, add_upsample):
+        super().__init__()
+        self.resnets = self._make_resnets(in_ch, out_ch, prev_ch, temb)
+        self.upsamplers = nn.ModuleList([Upsample2D(out_ch)]) if add_upsample else None
+
+    def forward(self, h, res_tuple, temb, context=None, upsample_size=None):
+        for resnet in self.resnets:
+            skip = res_tuple[-1]
+            res_tuple = res_tuple[:-1]
+            h = resnet(torch.cat([h, skip], dim=1), temb)
+        if self.upsamplers is not None:
+            h = self.upsamplers[0](h, upsample_size)
+        return h
+
+
+class UNetMidBlock2DCrossAttn(nn.Module):
+    def __init__(self, ch, temb, heads, ctx_dim):
+        super().__init__()
+        self.resnets = nn.ModuleList([ResnetBlock2D(ch, ch, temb) for _ in range(2)])
+        self.attentions = nn.ModuleList([Transformer2DModel(heads, ch // heads, ch, ctx_dim)])
+
+    def forward(self, h, temb, context):
+        h = self.resnets[0](h, temb)
+        h = self.attentions[0](h, encoder_hidden_states=context)
+        return self.resnets[1](h, temb)
+
+
+class TimestepEmbedding(nn.Module):
+    def __init__(self, ch, dim):
+        super().__init__()
+        self.linear_1 = nn.Linear(ch, dim)
+        self.linear_2 = nn.Linear(dim, dim)
+
+    def forward(self, x):
+        return self.linear_2(F.silu(self.linear_1(x)))
+
+
+def timestep_embedding(timesteps, dim, flip_sin_to_cos=True, downscale_freq_shift=0.0, max_period=10000):
+    half = dim // 2
+    exponent = -math.log(max_period) * torch.arange(half, dtype=torch.float32, device=timesteps.device)
+    exponent = exponent / (half - downscale_freq_shift)
+    emb = timesteps[:, None].float() * torch.exp(exponent)[None, :]
+    emb = torch.cat([torch.sin(emb), torch.cos(emb)], dim=-1)
+    if flip_sin_to_cos:
+        emb = torch.cat([emb[:, half:], emb[:, :half]], dim=-1)
+    return emb
+
+
+class UNet2DConditionModel(nn.Module):
+    """SD-1.5 UNet: blocks (320, 640, 1280, 1280), 8 heads, cross-attention dim 768."""
+
+    def __init__(self, in_channels=4, out_channels=4, block_out_channels=(320, 640, 1280, 1280),
+                 cross_attention_dim=768, attention_head_dim=8):
+        super().__init__()
+        ch0 = block_out_channels[0]
+        temb = ch0 * 4
+        heads = attention_head_dim
+        self.conv_in = nn.Conv2d(in_channels, ch0, 3, padding=1)
+        self.time_embedding = TimestepEmbedding(ch0, temb)
+        self.down_blocks = nn.ModuleList()
+        out_ch = ch0
+        for i in range(4):
+            in_ch, out_ch = out_ch, block_out_channels[i]
+            last = i == 3
+            if i < 3:
+                self.down_blocks.append(CrossAttnDownBlock2D(in_ch, out_ch, temb, heads, cross_attention_dim, not last))
+            else:
+                self.down_blocks.append(DownBlock2D(in_ch, out_ch, temb, not last))
+        self.mid_block = UNetMidBlock2DCrossAttn(block_out_channels[-1], temb, heads, cross_attention_dim)
+        self.up_blocks = nn.ModuleList()
+        rev = list(reversed(block_out_channels))
+        out_ch = rev[0]
+        for i in range(4):
+            prev_ch, out_ch = out_ch, rev[i]
+            in_ch = rev[min(i + 1, 3)]
+            last = i == 3
+            if i == 0:
+                self.up_blocks.append(UpBlock2D(in_ch, out_ch, prev_ch, temb, not last))
+            else:
+                self.up_blocks.append(CrossAttnUpBlock2D(in_ch, out_ch, prev_ch, temb, heads, cross_attention_dim, not last))
+        self.conv_norm_out = nn.GroupNorm(32, ch0, eps=1e-5)
+        self.conv_act = nn.SiLU()
+        self.conv_out = nn.Conv2d(ch0, out_channels, 3, padding=1)
+        self.time_proj_dim = ch0
+
+    def forward(self, sample, timestep, encoder_hidden_states, return_dict=True):
+        if not torch.is_tensor(timestep):
+            timestep = torch.tensor([timestep], dtype=torch.long, device=sample.device)
+        timesteps = timestep.reshape(-1).to(sample.device).expand(sample.shape[0])
+        emb = self.time_embedding(timestep_embedding(timesteps, self.time_proj_dim).to(sample.dtype))
+        h = self.conv_in(sample)
+        res = (h,)
+        for blk in self.down_blocks:
+            h, r = blk(h, emb, encoder_hidden_states)
+            res += r
+        h = self.mid_block(h, emb, encoder_hidden_states)
+        for i, blk in enumerate(self.up_blocks):
+            n = len(blk.resnets)
+            r, res = res[-n:], res[:-n]
+            size = res[-1].shape[2:] if (i < 3) else None
+            h = blk(h, r, emb, encoder_hidden_states, upsample_size=size)
+        h = self.conv_out(self.conv_act(self.conv_norm_out(h)))
+        return {"sample": h} if return_dict else (h,)

@@ -1,0 +1,312 @@
+"""Generate golden vectors by importing the REFERENCE implementation (build container only).
+
+Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py
+
+The reference (damaggu/StableKeypoints, read-only at /root/reference) is imported at
+function level with stubs for packages absent here (wandb, h5py, cv2, diffusers,
+torchvision) and a namespace package for its ``datasets/`` folder.
+Its hot-path functions run on torch-CPU; their outputs are written as small
+``.npz`` fixtures next to this script.  Large inputs are regenerated from the
+numpy recipes in ``recipes.py`` and pinned by SHA-256.  The reference itself never
+leaves this container: nothing under ``tests/`` imports it at test time.
+
+This script refuses to run when /root/reference is absent (e.g. on the GPU box).
+"""
+import os
+import sys
+import types
+from unittest.mock import MagicMock
+
+import numpy as np
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+
+
+def import_reference():
+    if not os.path.isdir(os.path.join(REF, "unsupervised_keypoints")):
+        raise SystemExit("make_goldens: /root/reference is absent; goldens are generated only in the build container")
+    sys.dont_write_bytecode = True
+    for m in ["wandb", "h5py", "cv2", "diffusers", "torchvision", "torchvision.transforms",
+              "torchvision.transforms.functional", "torchvision.datasets"]:
+        sys.modules[m] = MagicMock()
+    ds = types.ModuleType("datasets")
+    ds.__path__ = [os.path.join(REF, "datasets")]
+    sys.modules["datasets"] = ds
+    sys.path.insert(0, REF)
+    from unsupervised_keypoints import ptp_utils, optimize, eval as ref_eval, optimize_token, invertable_transform
+    return types.SimpleNamespace(ptp_utils=ptp_utils, optimize=optimize, eval=ref_eval,
+                                 optimize_token=optimize_token, invertable_transform=invertable_transform)
+
+
+sys.path.insert(0, HERE)
+sys.path.insert(0, REPO)
+import recipes  # noqa: E402
+import torch  # noqa: E402
+import torch.nn as nn  # noqa: E402
+
+LAYER_SHAPES_SMALL = [(4, 64), (4, 64), (4, 64), (8, 32)]      # (s, C) per captured layer
+LAYER_SHAPES_SD15 = [(16, 1280), (16, 1280), (16, 1280), (32, 640)]
+HEADS = 8
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+class _UpTree(nn.Module):
+    """Module tree with an ``up_blocks`` child holding CrossAttention modules.
+
+    The reference's ``register_attention_control`` only walks children whose name
+    contains "up" (ptp_utils.py:564-568) and patches class name "CrossAttention".
+    """
+
+    def __init__(self, shapes, ctx_dim, params):
+        super().__init__()
+        from stablekeypoints_amd.sd.unet import CrossAttention
+        self.up_blocks = nn.ModuleList()
+        for li, (s, c) in enumerate(shapes):
+            m = CrossAttention(c, cross_attention_dim=ctx_dim, heads=HEADS, dim_head=c // HEADS)
+            m.load_state_dict({k: torch.from_numpy(v) for k, v in params[li].items()})
+            self.up_blocks.append(m)
+
+
+def capture_case(R, shapes, n_tokens, ctx_dim, seed, want_grad, indices=None, upsample_res=-1, layers=(0, 1, 2, 3)):
+    ref = REFM
+    xs_np, ctx_np, params = recipes.capture_inputs(seed, shapes, n_tokens, ctx_dim)
+    tree = _UpTree(shapes, ctx_dim, params)
+    ctl = ref.ptp_utils.AttentionStore()
+    ref.ptp_utils.register_attention_control(tree, ctl, feature_upsample_res=R)
+    xs = [torch.from_numpy(x).requires_grad_(want_grad) for x in xs_np]
+    ctx = torch.from_numpy(ctx_np).requires_grad_(want_grad)
+    outs = [m(x, context=ctx) for m, x in zip(tree.up_blocks, xs)]
+    attn = [a for a in ctl.step_store["attn"]]
+    maps = ref.optimize.collect_maps(ctl, from_where=["up_cross"], upsample_res=upsample_res, layers=list(layers),
+                                     indices=indices)
+    return tree, xs, ctx, outs, attn, maps
+
+
+def gen_capture_small():
+    out = {}
+    R, N, D = 32, 16, 24
+    tree, xs, ctx, outs, attn, maps = capture_case(R, LAYER_SHAPES_SMALL, N, D, seed=1, want_grad=True)
+    wsel = torch.zeros_like(maps)
+    sel = [3, 7, 11]
+    wsel[sel] = torch.from_numpy(recipes.random_logits(5, (len(sel), R, R)))
+    loss = (maps * wsel).sum() + sum((o ** 2).mean() for o in outs) * 0.0
+    loss.backward()
+    out["R"] = R
+    out["N"] = N
+    out["ctx"] = _np(ctx)
+    for i, x in enumerate(xs):
+        out[f"x{i}"] = _np(x)
+        out[f"dx{i}"] = _np(x.grad)
+        out[f"attn{i}"] = _np(attn[i])
+        out[f"out{i}"] = _np(outs[i])
+        for name, p in tree.up_blocks[i].named_parameters():
+            out[f"w{i}.{name}"] = _np(p)
+    out["dctx"] = _np(ctx.grad)
+    out["map"] = _np(maps)
+    out["wsel"] = _np(wsel)
+    # index gather + bilinear up-res + layer subset (collect_maps optimize.py:44-75)
+    *_, maps_b = capture_case(R, LAYER_SHAPES_SMALL, N, D, seed=1, want_grad=False,
+                              indices=[5, 0, 9], upsample_res=48, layers=[0, 2, 3])
+    out["map_idx_up48_l023"] = _np(maps_b)
+    np.savez_compressed(os.path.join(HERE, "capture_small.npz"), **out)
+
+
+def gen_capture_sd15():
+    """Full-shape capture+aggregate (N=500, R=128): argmax, per-token sums, samples only."""
+    R, N, D = 128, 500, 768
+    with torch.no_grad():
+        *_, maps = capture_case(R, LAYER_SHAPES_SD15, N, D, seed=3, want_grad=False)
+    m = _np(maps)
+    out = {"R": R, "N": N,
+           "argmax_rc": _np(REFM.eval.find_max_pixel(maps)),
+           "token_sums": m.reshape(N, -1).sum(axis=1, dtype=np.float64),
+           "samples_idx": np.arange(0, m.size, 9973, dtype=np.int64)}
+    out["samples"] = m.reshape(-1)[out["samples_idx"]]
+    top2 = np.sort(m.reshape(N, -1), axis=1)[:, -2:]
+    out["argmax_margin"] = (top2[:, 1] - top2[:, 0]).astype(np.float32)
+    np.savez_compressed(os.path.join(HERE, "capture_sd15.npz"), **out)
+
+
+def gen_argmax():
+    ev = REFM.eval
+    out = {}
+    cases = torch.from_numpy(recipes.argmax_edge_cases())
+    out["edge"] = _np(cases)
+    out["edge_max"] = _np(ev.find_max_pixel(cases.clone()))
+    out["edge_k3"] = _np(ev.find_k_max_pixels(cases.clone(), num=3))
+    m = torch.from_numpy(recipes.attention_like_maps(11, 6, 32))
+    out["maps32"] = _np(m)
+    out["maps32_k3"] = _np(ev.find_k_max_pixels(m.clone(), num=3))
+    pt = ev.find_max_pixel(m)
+    out["maps32_mask"] = _np(ev.mask_radius(m.clone(), pt, 0.05 * 32 * 3))
+    wa = m.clone()
+    out["maps32_wavg"] = _np(ev.pixel_from_weighted_avg(wa, distance=5))
+    out["maps32_wavg_mutated"] = _np(wa)
+    out["maps32_wavg_nodist"] = _np(ev.pixel_from_weighted_avg(m.clone(), distance=-1))
+    big = torch.from_numpy(recipes.attention_like_maps(12, 10, 512))
+    out["maps512_sha"] = np.array(recipes.sha256(_np(big)))
+    out["maps512_max"] = _np(ev.find_max_pixel(big))
+    out["maps512_wavg"] = _np(ev.pixel_from_weighted_avg(big.clone()))
+    np.savez_compressed(os.path.join(HERE, "argmax.npz"), **out)
+
+
+def gen_gaussian():
+    ot = REFM.optimize_token
+    out = {}
+    pos = torch.from_numpy(recipes.uniform(21, (2, 5, 2)))
+    out["pos"] = _np(pos)
+    for size, sigma in ((32, 2.0), (128, 2.0), (20, 3.0)):
+        out[f"circles_{size}_{sigma}"] = _np(ot.gaussian_circles(pos, size=size, sigma=sigma, device="cpu"))
+    out["circle_32_2.0"] = _np(ot.gaussian_circle(pos[0], size=32, sigma=2.0, device="cpu"))
+    np.savez_compressed(os.path.join(HERE, "gaussian.npz"), **out)
+
+
+def gen_select():
+    pu = REFM.ptp_utils
+    out = {}
+    # full-shape selection (A8/A9/A10) from regenerated maps
+    maps = torch.from_numpy(recipes.attention_like_maps(31, 500, 128))
+    maps_t = torch.from_numpy(recipes.attention_like_maps(32, 500, 128))
+    out["maps_sha"] = np.array(recipes.sha256(_np(maps)))
+    out["maps_t_sha"] = np.array(recipes.sha256(_np(maps_t)))
+    cand = pu.find_top_k_gaussian(maps, 25, sigma=2.0)
+    out["topk_gauss25"] = _np(cand)
+    out["topk_gauss25_s2"] = _np(pu.find_top_k_gaussian(maps, 25, sigma=2.0, num_subjects=2))
+    out["entropy25"] = _np(pu.entropy_sort(maps, 25))
+    out["entropy25_sharp"] = _np(pu.entropy_sort(maps * 100.0, 25))
+    out["fps10"] = _np(pu.furthest_point_sampling(maps_t, 10, cand))
+    out["fps10_same"] = _np(pu.furthest_point_sampling(maps, 10, cand))
+    # small committed case
+    ms = torch.from_numpy(recipes.attention_like_maps(33, 64, 32))
+    out["maps_small"] = _np(ms)
+    c = pu.find_top_k_gaussian(ms, 12, sigma=2.0)
+    out["small_topk12"] = _np(c)
+    out["small_entropy12"] = _np(pu.entropy_sort(ms, 12))
+    out["small_fps5"] = _np(pu.furthest_point_sampling(ms, 5, c))
+    # FPS with tied positions: all candidates share one argmax
+    tie = torch.zeros(6, 8, 8)
+    tie[:, 3, 4] = 1.0
+    tie[4, 0, 0] = 2.0
+    out["tie_maps"] = _np(tie)
+    out["tie_fps4"] = _np(pu.furthest_point_sampling(tie, 4, torch.tensor([5, 2, 4, 0, 1])))
+    np.savez_compressed(os.path.join(HERE, "select.npz"), **out)
+
+
+def gen_losses():
+    opt = REFM.optimize
+    it = REFM.invertable_transform
+    out = {}
+    A = torch.from_numpy(recipes.attention_like_maps(41, 10, 32)).requires_grad_(True)
+    At = torch.from_numpy(recipes.attention_like_maps(42, 10, 32)).requires_grad_(True)
+    out["A"] = _np(A)
+    out["At"] = _np(At)
+    for ns in (1, 2):
+        A.grad = None
+        l = opt.sharpening_loss(A, sigma=2.0, device="cpu", num_subjects=ns)
+        l.backward()
+        out[f"sharp_ns{ns}"] = _np(l)
+        out[f"dA_sharp_ns{ns}"] = _np(A.grad)
+    # equivariance (optimize.py:157-163) with two replicas, picking index 1
+    T = it.RandomAffineWithInverse(degrees=15, scale=(0.8, 1.0), translate=(0.25, 0.25))
+    torch.manual_seed(7)
+    img = torch.from_numpy(recipes.uniform(43, (2, 3, 64, 64)))
+    warped = T(img)
+    theta = T.last_params["theta"]
+    out["img"] = _np(img)
+    out["theta"] = _np(theta)
+    out["warped"] = _np(warped)
+    A.grad = None
+    At.grad = None
+    l = opt.equivariance_loss(A, At[None].repeat(2, 1, 1, 1), T, 1)
+    l.backward()
+    out["equiv"] = _np(l)
+    out["dA_equiv"] = _np(A.grad)
+    out["dAt_equiv"] = _np(At.grad)
+    out["inv_At"] = _np(T.inverse(At.detach()[None].repeat(2, 1, 1, 1)))
+    # theta draw semantics (invertable_transform.py:42-57): seeded draws
+    T2 = it.RandomAffineWithInverse(degrees=30, scale=(0.9, 1.1), translate=(0.1, 0.1))
+    torch.manual_seed(123)
+    T2(torch.zeros(3, 1, 4, 4))
+    out["theta_seed123"] = _np(T2.last_params["theta"])
+    np.savez_compressed(os.path.join(HERE, "losses.npz"), **out)
+
+
+class _RecordingScheduler:
+    def __init__(self, inner):
+        self.inner = inner
+        self.timesteps = inner.timesteps
+        self.noises = []
+
+    def add_noise(self, x, noise, t):
+        self.noises.append(noise.clone())
+        return self.inner.add_noise(x, noise, t)
+
+
+def gen_step_tiny():
+    """One token-opt micro-iteration (optimize.py:362-445) on the tiny SD-1.5-shaped model, CPU."""
+    pu, opt = REFM.ptp_utils, REFM.optimize
+    it = REFM.invertable_transform
+    from stablekeypoints_amd.sd import build_sd15, TINY_CONFIG
+    parts = build_sd15(seed=0, config=TINY_CONFIG)
+    psum = float(sum(p.double().sum() for p in list(parts.unet.parameters()) + list(parts.vae.parameters())))
+    parts.scheduler = _RecordingScheduler(parts.scheduler)
+    R, N = 32, 16
+    controllers = {torch.device("cpu"): pu.AttentionStore()}
+
+    def hook_fn(module, inp):   # optimize_token.py:59-68
+        pu.register_attention_control(module, controllers[inp[0].device], feature_upsample_res=R)
+    parts.unet.register_forward_pre_hook(hook_fn)
+    img = torch.from_numpy(recipes.uniform(51, (1, 3, 64, 64)))
+    ctx = torch.from_numpy(recipes.random_logits(52, (1, N, 32))).requires_grad_(True)
+    T = it.RandomAffineWithInverse(degrees=15, scale=(0.8, 1.0), translate=(0.25, 0.25))
+    kw = dict(layers=[0, 1, 2, 3], noise_level=-1, from_where=["down_cross", "mid_cross", "up_cross"],
+              upsample_res=-1, device="cpu", controllers=controllers)
+    torch.manual_seed(100)
+    maps = pu.run_and_find_attn(parts, img, ctx, **kw)
+    torch.manual_seed(101)
+    timg = T(img)
+    torch.manual_seed(102)
+    maps_t = pu.run_and_find_attn(parts, timg, ctx, **kw)
+    sigma, top_k, fps_n, bs, num_gpus = 2.0, 4, 8, 4, 1
+    cand = pu.find_top_k_gaussian(maps[0], fps_n, sigma=sigma, num_subjects=1)
+    idx = pu.furthest_point_sampling(maps_t[0], top_k, cand)
+    sharp = opt.sharpening_loss(maps[0][idx], device="cpu", sigma=sigma, num_subjects=1)
+    eq = opt.equivariance_loss(maps[0][idx], maps_t[0][idx][None].repeat(num_gpus, 1, 1, 1), T, 0)
+    loss = (eq * 1000.0 + sharp * 100.0) / (bs // num_gpus)
+    loss.backward()
+    out = {"R": R, "N": N, "param_sum": psum, "img": _np(img), "ctx": _np(ctx), "timg": _np(timg),
+           "theta": _np(T.last_params["theta"]), "noise0": _np(parts.scheduler.noises[0]),
+           "noise1": _np(parts.scheduler.noises[1]), "map": _np(maps[0]), "map_t": _np(maps_t[0]),
+           "cand": _np(cand), "idx": _np(idx), "sharp": _np(sharp), "eq": _np(eq), "loss": _np(loss),
+           "dctx": _np(ctx.grad)}
+    np.savez_compressed(os.path.join(HERE, "step_tiny.npz"), **out)
+
+
+def gen_interp():
+    """Torch interpolation/warp numerics the kernels restate."""
+    import torch.nn.functional as F
+    out = {}
+    z = torch.from_numpy(recipes.random_logits(61, (3, 5, 6, 6)))
+    out["z"] = _np(z)
+    out["bicubic_6_to_32"] = _np(F.interpolate(z, size=(32, 32), mode="bicubic", align_corners=False))
+    out["bicubic_6_to_13"] = _np(F.interpolate(z, size=(13, 13), mode="bicubic", align_corners=False))
+    m = torch.from_numpy(recipes.random_logits(62, (1, 4, 16, 16)))
+    out["m"] = _np(m)
+    out["bilinear_16_to_40"] = _np(F.interpolate(m, size=(40, 40), mode="bilinear", align_corners=False))
+    out["bilinear_16_to_64"] = _np(F.interpolate(m, size=(64, 64), mode="bilinear", align_corners=False))
+    np.savez_compressed(os.path.join(HERE, "interp.npz"), **out)
+
+
+if __name__ == "__main__":
+    REFM = import_reference()
+    torch.set_num_threads(8)
+    which = sys.argv[1:] or ["capture_small", "capture_sd15", "argmax", "gaussian", "select", "losses",
+                             "step_tiny", "interp"]
+    for w in which:
+        print("generating", w, flush=True)
+        globals()["gen_" + w]()
