@@ -1,0 +1,147 @@
+/*
+ * skp.h — C ABI of libskp.so, the MI355X (gfx950) hot path of StableKeypoints.
+ *
+ * The reference (damaggu/StableKeypoints) has no FFI: its hot path is Python/torch
+ * (SURVEY.md §8b).  Each entry point below replaces one reference function or the
+ * torch-op sequence inside it; the reference file:line is cited per function.
+ * The Python mirror of the reference API (stablekeypoints_amd/) binds these with
+ * ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *   - All pointers are DEVICE pointers to row-major fp32 / int64 buffers that the
+ *     caller allocates (caller owns every buffer; the library keeps no global state
+ *     and is safe to call concurrently on different streams).
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream).
+ *   - Return 0 on success, SKP_EBADARG (-1) for invalid arguments, SKP_ELAUNCH (-2)
+ *     when a kernel launch fails.  skp_last_error() gives the thread-local message.
+ *   - "maps" are (T, h, w) fp32; "positions" are (row + 0.5, col + 0.5) fp32 pairs;
+ *     "attn" is one captured layer (BH, R*R, N) fp32 in the reference layout
+ *     (ptp_utils.py:534-536: (batch*heads, pixels, tokens)).
+ */
+#ifndef SKP_H
+#define SKP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SKP_OK 0
+#define SKP_EBADARG (-1)
+#define SKP_ELAUNCH (-2)
+#define SKP_MAX_LAYERS 16
+
+const char* skp_last_error(void);
+int skp_version(void);
+
+/* ---------------------------------------------------------------- A1 capture
+ * Replaces the capture branch of the patched CrossAttention.forward,
+ * ptp_utils.py:508-538 (bicubic(x) -> to_q -> q kᵀ·scale -> softmax).  With
+ * z_low = the layer's normal-path logits q kᵀ·scale at s×s (ptp_utils.py:493),
+ * attn[b,p,n] = softmax_n(bicubic_{s->R}(z_low[b,:,n])[p]).
+ *   z_low (BH, s*s, N) -> attn (BH, R*R, N).                                     */
+int skp_capture_fwd(const float* z_low, int BH, int s, int N, int R, float* attn, void* stream);
+
+/* Backward of skp_capture_fwd: dz_low = bicubicᵀ( a ⊙ (g − Σ_n a g) ).
+ * g = dattn is read with element strides (sb, sp, sn) so a broadcast gradient
+ * (e.g. sb = 0 from the layer mean of collect_maps) needs no materialisation.
+ * `workspace` holds BH*R*s*N floats (the row-adjoint partials).               */
+int skp_capture_bwd(const float* z_low, int BH, int s, int N, int R, const float* dattn, long long sb,
+                    long long sp, long long sn, float gscale, float* dz_low, float* workspace, void* stream);
+
+/* ---------------------------------------------------------------- A3 aggregate
+ * optimize.collect_maps (optimize.py:27-79), token-major output:
+ * out[m, p] = (1/(L·BH)) Σ_l Σ_b attn_l[b, p, idx(m)], idx = indices[m] or m.
+ * layers: host array of L device pointers, each (BH, RR, N).                  */
+int skp_aggregate(const float* const* layers, int L, int BH, int RR, int N, const long long* indices,
+                  int n_out, float* out, void* stream);
+
+/* Bilinear resize (F.interpolate mode="bilinear", align_corners=False; optimize.py:63-70)
+ * of C square planes R×R -> Ro×Ro, and its adjoint.                            */
+int skp_resize_bilinear(const float* in, int C, int R, int Ro, float* out, void* stream);
+int skp_resize_bilinear_bwd(const float* gout, int C, int R, int Ro, float* gin, void* stream);
+
+/* ---------------------------------------------------------------- A4-A6 argmax family
+ * eval.find_max_pixel (eval.py:39-60): first-occurrence argmax, NaN is max.
+ * rows: optional device list of n_rows row ids (NULL = rows 0..T-1).
+ * pos (n_rows, 2) = (idx / w + 0.5, idx % w + 0.5); idx (n_rows) optional.     */
+int skp_argmax2d(const float* maps, int T, int h, int w, const long long* rows, int n_rows, float* pos,
+                 long long* idx, void* stream);
+
+/* eval.find_k_max_pixels + mask_radius (eval.py:62-111): `num` rounds of argmax,
+ * each followed by map *= (squared distance > radius2).  pos (num, T, 2).
+ * masked (T, h, w) optional: the map after the last round's mask.             */
+int skp_k_max_pixels(const float* maps, int T, int h, int w, int num, float radius2, float* pos,
+                     float* masked, void* stream);
+
+/* eval.mask_radius (eval.py:83-111): out = map * (squared distance to pos > radius2). */
+int skp_mask_radius(const float* maps, int T, int h, int w, const float* pos, float radius2, float* out,
+                    void* stream);
+
+/* eval.pixel_from_weighted_avg (eval.py:113-155): zero pixels farther than
+ * `distance` from the argmax (in place when mutate != 0, like the reference),
+ * then the normalised centroid + 0.5.  distance < 0 disables the cut.          */
+int skp_weighted_avg(float* maps, int T, int h, int w, float distance, int mutate, float* pos, void* stream);
+
+/* ---------------------------------------------------------------- A7 target
+ * optimize_token.gaussian_circles (optimize_token.py:204-242):
+ * out[t,i,j] = mean_q exp(-((j+.5-P[q,t,1]·size)² + (i+.5-P[q,t,0]·size)²)/(2σ²)),
+ * P = pos (num, T, 2) in [0, 1].                                               */
+int skp_gaussian_target(const float* pos, int num, int T, int size, float sigma, float* out, void* stream);
+
+/* ---------------------------------------------------------------- A8-A10 select
+ * ptp_utils.find_top_k_gaussian (ptp_utils.py:86-112): per-token
+ * KL(normalised G(argmax)+eps ‖ softmax(map+eps)), ascending, first top_k
+ * (ties by token id).  kl (T) doubles optional; workspace >= 16*T bytes.       */
+int skp_topk_gaussian(const float* maps, int T, int h, int w, int top_k, float sigma, float epsilon,
+                      int num_subjects, long long* out, double* kl, void* workspace, void* stream);
+
+/* ptp_utils.entropy_sort (ptp_utils.py:165-187): ascending softmax entropy.     */
+int skp_entropy_sort(const float* maps, int T, int h, int w, int top_k, long long* out, double* ent,
+                     void* workspace, void* stream);
+
+/* ptp_utils.furthest_point_sampling (ptp_utils.py:115-159) on the argmax positions
+ * of the candidate rows; strict '>' first-wins, IEEE sqrt distances.
+ * out[top_k] (int64); n_out (device int) = how many were selected.
+ * workspace >= 16 * n_cand bytes.                                              */
+int skp_fps(const float* maps, int T, int h, int w, const long long* cand, int n_cand, int top_k,
+            long long* out, int* n_out, void* workspace, void* stream);
+
+/* ---------------------------------------------------------------- A11 sharpening
+ * optimize.sharpening_loss (optimize.py:166-206): pos = k-max of A / w,
+ * G = gaussian_circles(pos, h, σ), loss = mean((A-G)²).
+ * pos (num, T, 2) is written for the backward; partial >= T doubles.          */
+int skp_sharpen_fwd(const float* A, int T, int h, int w, float sigma, int num_subjects, float* pos,
+                     double* partial, float* loss, void* stream);
+/* dA = gout[0] · 2(A − G)/numel.                                               */
+int skp_sharpen_bwd(const float* A, int T, int h, int w, float sigma, int num_subjects, const float* pos,
+                     const float* gout, float* dA, void* stream);
+
+/* ---------------------------------------------------------------- A12 warp / equivariance
+ * F.grid_sample(x, F.affine_grid(theta), bilinear, zeros, align_corners=False)
+ * (invertable_transform.py:64-70, 86-90).  x (B, C, H, W), theta (B, 2, 3) device. */
+int skp_affine_warp(const float* x, int B, int C, int H, int W, const float* theta, float* out, void* stream);
+/* Adjoint w.r.t. x; gin is OVERWRITTEN (zeroed then accumulated).               */
+int skp_affine_warp_bwd(const float* gout, int B, int C, int H, int W, const float* theta, float* gin,
+                        void* stream);
+
+/* optimize.equivariance_loss (optimize.py:157-163) for one replica:
+ * loss = mean((A − warp(At, theta_inv))²), theta_inv (2,3) the inverse of that
+ * replica's theta (invertable_transform.py:72-92).  partial >= T doubles.        */
+int skp_equiv_fwd(const float* A, const float* At, int T, int h, int w, const float* theta_inv,
+                  double* partial, float* loss, void* stream);
+/* dA = gout·2(A−A')/numel (optional), dAt = warpᵀ(−dA) (overwritten).          */
+int skp_equiv_bwd(const float* A, const float* At, int T, int h, int w, const float* theta_inv,
+                  const float* gout, float* dA, float* dAt, void* stream);
+
+/* ---------------------------------------------------------------- Q·Kᵀ (fp32 MFMA)
+ * C[b,m,n] = alpha · Σ_k A[b,m,k] · B[b,k,n] (+ C if accumulate), arbitrary element
+ * strides; exact-f32 v_mfma_f32_32x32x2_f32.  Used for the capture logits
+ * z = q kᵀ·scale (ptp_utils.py:493/534) and their gradients.                   */
+int skp_bgemm_f32(const float* A, long long sAb, long long sAm, long long sAk, const float* B, long long sBb,
+                  long long sBk, long long sBn, float* C, long long sCb, long long sCm, long long sCn, int batch,
+                  int M, int N, int K, float alpha, int accumulate, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SKP_H */

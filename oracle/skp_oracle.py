@@ -378,7 +378,7 @@ def _base_coords(n):
     i = np.arange(n)
     lin = np.where(i < n // 2, np.float32(-1.0) + i.astype(np.float32) * step,
                    np.float32(1.0) - (n - 1 - i).astype(np.float32) * step).astype(np.float32)
-    return (lin * np.float32((n - 1) / n)).astype(np.float32)
+    return ((lin * np.float32(n - 1)) / np.float32(n)).astype(np.float32)
 
 
 def _grid(theta, H, W):
@@ -393,16 +393,17 @@ def _grid(theta, H, W):
 
 
 def _taps(ix, iy, H, W):
-    x0 = np.floor(ix).astype(np.int64)
-    y0 = np.floor(iy).astype(np.int64)
-    wx1 = (ix - x0).astype(np.float32)
-    wy1 = (iy - y0).astype(np.float32)
+    """grid_sample bilinear taps (nw, ne, sw, se) with ATen's weight formulas."""
+    x0f = np.floor(ix).astype(np.float32)
+    y0f = np.floor(iy).astype(np.float32)
+    x1f, y1f = x0f + F32(1.0), y0f + F32(1.0)
+    wts = [((y0f, x0f), (x1f - ix) * (y1f - iy)), ((y0f, x1f), (ix - x0f) * (y1f - iy)),
+           ((y1f, x0f), (x1f - ix) * (iy - y0f)), ((y1f, x1f), (ix - x0f) * (iy - y0f))]
     out = []
-    for dy, wy in ((0, F32(1.0) - wy1), (1, wy1)):
-        for dx, wx in ((0, F32(1.0) - wx1), (1, wx1)):
-            yy, xx = y0 + dy, x0 + dx
-            ok = (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W)
-            out.append((np.clip(yy, 0, H - 1), np.clip(xx, 0, W - 1), (wy * wx * ok).astype(np.float32)))
+    for (yf, xf), w in wts:
+        yy, xx = yf.astype(np.int64), xf.astype(np.int64)
+        ok = (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W)
+        out.append((np.clip(yy, 0, H - 1), np.clip(xx, 0, W - 1), (w * ok).astype(np.float32)))
     return out
 
 

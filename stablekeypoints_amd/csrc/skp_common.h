@@ -1,0 +1,183 @@
+// Shared device/host helpers for libskp (gfx950, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/skp.h"
+
+namespace skp {
+
+constexpr int WAVE = 64;
+
+// ------------------------------------------------------------------ host-side error plumbing
+void set_error(const std::string& msg);
+
+#define SKP_CHECK_ARG(cond, msg)                 \
+  do {                                           \
+    if (!(cond)) {                               \
+      ::skp::set_error(std::string(__func__) + ": " + (msg)); \
+      return SKP_EBADARG;                        \
+    }                                            \
+  } while (0)
+
+#define SKP_LAUNCH_CHECK()                                                            \
+  do {                                                                                \
+    hipError_t e_ = hipGetLastError();                                                \
+    if (e_ != hipSuccess) {                                                           \
+      ::skp::set_error(std::string(__func__) + ": launch failed: " + hipGetErrorString(e_)); \
+      return SKP_ELAUNCH;                                                             \
+    }                                                                                 \
+  } while (0)
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ------------------------------------------------------------------ wave reductions (64 lanes)
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// torch.argmax order: NaN beats everything; among equals (or NaNs) the lower index wins.
+__device__ __forceinline__ bool argmax_better(float a, int ia, float b, int ib) {
+  const bool na = isnan(a), nb = isnan(b);
+  if (na) return !nb || ia < ib;
+  if (nb) return false;
+  return a > b || (a == b && ia < ib);
+}
+
+__device__ __forceinline__ void wave_argmax(float& v, int& i) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    float ov = __shfl_xor(v, o, 64);
+    int oi = __shfl_xor(i, o, 64);
+    if (argmax_better(ov, oi, v, i)) { v = ov; i = oi; }
+  }
+}
+
+// Block-wide argmax for blockDim.x = 64*k threads; scratch needs 2*(blockDim/64) words.
+__device__ __forceinline__ void block_argmax(float& v, int& i, float* sv, int* si) {
+  wave_argmax(v, i);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (lane == 0) { sv[wid] = v; si[wid] = i; }
+  __syncthreads();
+  if (wid == 0) {
+    v = lane < nw ? sv[lane] : -INFINITY;
+    i = lane < nw ? si[lane] : 0x7fffffff;
+    wave_argmax(v, i);
+    if (lane == 0) { sv[0] = v; si[0] = i; }
+  }
+  __syncthreads();
+  v = sv[0];
+  i = si[0];
+  __syncthreads();
+}
+
+__device__ __forceinline__ double block_sum(double v, double* sd) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (lane == 0) sd[wid] = v;
+  __syncthreads();
+  if (wid == 0) {
+    v = lane < nw ? sd[lane] : 0.0;
+    v = wave_sum(v);
+    if (lane == 0) sd[0] = v;
+  }
+  __syncthreads();
+  v = sd[0];
+  __syncthreads();
+  return v;
+}
+
+__device__ __forceinline__ float block_max(float v, float* sf) {
+  v = wave_max(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (lane == 0) sf[wid] = v;
+  __syncthreads();
+  if (wid == 0) {
+    v = lane < nw ? sf[lane] : -INFINITY;
+    v = wave_max(v);
+    if (lane == 0) sf[0] = v;
+  }
+  __syncthreads();
+  v = sf[0];
+  __syncthreads();
+  return v;
+}
+
+// ------------------------------------------------------------------ interpolation taps
+// torch upsample_bicubic2d, align_corners=False: src = (dst+0.5)·in/out − 0.5 (unclamped),
+// taps floor(src)−1..+2 clamped to [0, in−1], Keys A = −0.75.
+struct Taps4 {
+  int i[4];
+  float w[4];
+};
+
+__device__ __forceinline__ float cubic1(float x) {  // |x| <= 1
+  const float A = -0.75f;
+  return ((A + 2.0f) * x - (A + 3.0f)) * x * x + 1.0f;
+}
+__device__ __forceinline__ float cubic2(float x) {  // 1 < |x| < 2
+  const float A = -0.75f;
+  return ((A * x - 5.0f * A) * x + 8.0f * A) * x - 4.0f * A;
+}
+
+__device__ __forceinline__ Taps4 bicubic_taps(int dst, int n_in, int n_out) {
+  const float scale = (float)n_in / (float)n_out;
+  const float src = scale * ((float)dst + 0.5f) - 0.5f;
+  const float f = floorf(src);
+  const float t = src - f;
+  const int i0 = (int)f;
+  Taps4 r;
+  r.w[0] = cubic2(t + 1.0f);
+  r.w[1] = cubic1(t);
+  r.w[2] = cubic1(1.0f - t);
+  r.w[3] = cubic2(2.0f - t);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) r.i[k] = min(max(i0 - 1 + k, 0), n_in - 1);
+  return r;
+}
+
+// torch bilinear, align_corners=False: src = max((dst+0.5)·in/out − 0.5, 0), upper tap clamped.
+struct Taps2 {
+  int i0, i1;
+  float w0, w1;
+};
+__device__ __forceinline__ Taps2 bilinear_taps(int dst, int n_in, int n_out) {
+  const float scale = (float)n_in / (float)n_out;
+  float src = scale * ((float)dst + 0.5f) - 0.5f;
+  src = src < 0.0f ? 0.0f : src;
+  Taps2 r;
+  r.i0 = (int)src;
+  r.i1 = r.i0 + (r.i0 < n_in - 1 ? 1 : 0);
+  r.w1 = src - (float)r.i0;
+  r.w0 = 1.0f - r.w1;
+  return r;
+}
+
+// affine_grid base coordinate (align_corners=False): linspace(-1, 1, n)[i] * (n-1)/n,
+// with linspace evaluated as ATen does (from the start for the first half, from the end
+// for the second half).
+__device__ __forceinline__ float affine_base(int i, int n) {
+  if (n <= 1) return 0.0f;
+  const float step = 2.0f / (float)(n - 1);
+  const float lin = (i < n / 2) ? (-1.0f + step * (float)i) : (1.0f - step * (float)(n - 1 - i));
+  return (lin * (float)(n - 1)) / (float)n;  // ATen: range * (n - 1) / n
+}
+
+// Correctly rounded float sqrt via double (exact for finite floats).
+__device__ __forceinline__ float sqrt_rn(float x) { return (float)sqrt((double)x); }
+
+}  // namespace skp

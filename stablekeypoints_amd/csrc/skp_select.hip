@@ -1,0 +1,578 @@
+// A4-A10: argmax family, Gaussian targets, token selection (KL / entropy ranking,
+// furthest-point sampling) for gfx950.
+//
+// Reference: eval.py:39-155 (find_max_pixel, find_k_max_pixels, mask_radius,
+// pixel_from_weighted_avg), optimize_token.py:204-242 (gaussian_circle(s)),
+// ptp_utils.py:86-187 (find_top_k_gaussian, furthest_point_sampling, entropy_sort).
+// Every map row is reduced by one 256-thread workgroup (4 waves) with shuffle
+// reductions; index outputs follow torch.argmax (first occurrence, NaN is max) and the
+// reference's strict '>' first-wins loops, so they are bit-exact on identical maps.
+#include "skp_common.h"
+
+using namespace skp;
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxSubjects = 16;
+
+// Scan one row for its argmax (torch order).  Applies the cumulative radius masks of
+// previously found points (eval.mask_radius multiplies by 0/1, so NaN/inf survive as NaN).
+__device__ void row_argmax_masked(const float* __restrict__ m, int h, int w, const float* pr, const float* pc,
+                                  int nmask, float radius2, float& best, int& bi, float* sv, int* si) {
+  best = -INFINITY;
+  bi = 0x7fffffff;
+  const int HW = h * w;
+  for (int e = threadIdx.x; e < HW; e += kThreads) {
+    float v = m[e];
+    if (nmask) {
+      const float x = (float)(e % w), y = (float)(e / w);
+      for (int q = 0; q < nmask; ++q) {
+        const float dx = x - pc[q], dy = y - pr[q];
+        v = v * ((dx * dx + dy * dy > radius2) ? 1.0f : 0.0f);
+      }
+    }
+    if (argmax_better(v, e, best, bi)) { best = v; bi = e; }
+  }
+  block_argmax(best, bi, sv, si);
+}
+
+__global__ __launch_bounds__(kThreads) void argmax_kernel(const float* __restrict__ maps, int T, int h, int w,
+                                                          const long long* __restrict__ rows, float* __restrict__ pos,
+                                                          long long* __restrict__ idx) {
+  __shared__ float sv[kThreads / 64];
+  __shared__ int si[kThreads / 64];
+  const long long row = rows ? rows[blockIdx.x] : blockIdx.x;
+  if (row < 0 || row >= T) {  // invalid row id: poison the output instead of reading out of bounds
+    if (threadIdx.x == 0) {
+      if (pos) { pos[2 * blockIdx.x] = NAN; pos[2 * blockIdx.x + 1] = NAN; }
+      if (idx) idx[blockIdx.x] = -1;
+    }
+    return;
+  }
+  float best;
+  int bi;
+  row_argmax_masked(maps + row * (long long)h * w, h, w, nullptr, nullptr, 0, 0.0f, best, bi, sv, si);
+  if (threadIdx.x == 0) {
+    if (pos) {
+      pos[2 * blockIdx.x] = (float)(bi / w) + 0.5f;
+      pos[2 * blockIdx.x + 1] = (float)(bi % w) + 0.5f;
+    }
+    if (idx) idx[blockIdx.x] = bi;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void kmax_kernel(const float* __restrict__ maps, int T, int h, int w, int num,
+                                                        float radius2, float* __restrict__ pos,
+                                                        float* __restrict__ masked) {
+  __shared__ float sv[kThreads / 64];
+  __shared__ int si[kThreads / 64];
+  __shared__ float pr[kMaxSubjects], pc[kMaxSubjects];
+  const int row = blockIdx.x;
+  const float* m = maps + (size_t)row * h * w;
+  for (int q = 0; q < num; ++q) {
+    float best;
+    int bi;
+    row_argmax_masked(m, h, w, pr, pc, q, radius2, best, bi, sv, si);
+    if (threadIdx.x == 0) {
+      pr[q] = (float)(bi / w) + 0.5f;
+      pc[q] = (float)(bi % w) + 0.5f;
+      pos[((size_t)q * T + row) * 2] = pr[q];
+      pos[((size_t)q * T + row) * 2 + 1] = pc[q];
+    }
+    __syncthreads();
+  }
+  if (masked) {
+    const int HW = h * w;
+    for (int e = threadIdx.x; e < HW; e += kThreads) {
+      float v = m[e];
+      const float x = (float)(e % w), y = (float)(e / w);
+      for (int q = 0; q < num; ++q) {
+        const float dx = x - pc[q], dy = y - pr[q];
+        v = v * ((dx * dx + dy * dy > radius2) ? 1.0f : 0.0f);
+      }
+      masked[(size_t)row * HW + e] = v;
+    }
+  }
+}
+
+__global__ void mask_radius_kernel(const float* __restrict__ maps, int T, int h, int w,
+                                   const float* __restrict__ pos, float radius2, float* __restrict__ out) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t HW = (size_t)h * w;
+  if (e >= (size_t)T * HW) return;
+  const int t = e / HW, p = e % HW;
+  const float dx = (float)(p % w) - pos[2 * t + 1], dy = (float)(p / w) - pos[2 * t];
+  out[e] = maps[e] * ((dx * dx + dy * dy > radius2) ? 1.0f : 0.0f);
+}
+
+__global__ __launch_bounds__(kThreads) void weighted_avg_kernel(float* __restrict__ maps, int h, int w,
+                                                                float distance, int mutate, float* __restrict__ pos) {
+  __shared__ float sv[kThreads / 64];
+  __shared__ int si[kThreads / 64];
+  __shared__ double sd[kThreads / 64];
+  float* m = maps + (size_t)blockIdx.x * h * w;
+  float best;
+  int bi;
+  row_argmax_masked(m, h, w, nullptr, nullptr, 0, 0.0f, best, bi, sv, si);
+  const float r = (float)(bi / w), c = (float)(bi % w);
+  const bool cut = distance >= 0.0f;
+  const int HW = h * w;
+  double tot = 0.0;
+  for (int e = threadIdx.x; e < HW; e += kThreads) {
+    const float x = (float)(e / w), y = (float)(e % w);
+    const float dx = x - r, dy = y - c;
+    const bool drop = cut && (sqrt_rn(dx * dx + dy * dy) > distance);
+    float v = m[e];
+    if (drop) {
+      v = 0.0f;
+      if (mutate) m[e] = 0.0f;
+    }
+    tot += (double)v;
+  }
+  tot = block_sum(tot, sd);
+  const float denom = (float)tot + 1e-6f;
+  double xs = 0.0, ys = 0.0;
+  for (int e = threadIdx.x; e < HW; e += kThreads) {
+    const float x = (float)(e / w), y = (float)(e % w);
+    const float dx = x - r, dy = y - c;
+    const bool drop = cut && (sqrt_rn(dx * dx + dy * dy) > distance);
+    const float v = drop ? 0.0f : m[e];
+    const float nv = v / denom;
+    xs += (double)(x * nv);
+    ys += (double)(y * nv);
+  }
+  xs = block_sum(xs, sd);
+  ys = block_sum(ys, sd);
+  if (threadIdx.x == 0) {
+    pos[2 * blockIdx.x] = (float)xs + 0.5f;
+    pos[2 * blockIdx.x + 1] = (float)ys + 0.5f;
+  }
+}
+
+// gaussian_circle (optimize_token.py:211-223), averaged over subjects (226-242)
+__device__ __forceinline__ float gauss_at(int i, int j, const float* p0, const float* p1, int num, float two_sig2) {
+  float acc = 0.0f;
+  for (int q = 0; q < num; ++q) {
+    const float dj = ((float)j + 0.5f) - p1[q];
+    const float di = ((float)i + 0.5f) - p0[q];
+    const float d2 = dj * dj + di * di;
+    acc += expf(-d2 / two_sig2);
+  }
+  return acc / (float)num;
+}
+
+__global__ void gaussian_target_kernel(const float* __restrict__ pos, int num, int T, int size, float two_sig2,
+                                       float* __restrict__ out) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t S2 = (size_t)size * size;
+  if (e >= (size_t)T * S2) return;
+  const int t = e / S2, p = e % S2;
+  float p0[kMaxSubjects], p1[kMaxSubjects];
+  for (int q = 0; q < num; ++q) {
+    p0[q] = pos[((size_t)q * T + t) * 2] * (float)size;
+    p1[q] = pos[((size_t)q * T + t) * 2 + 1] * (float)size;
+  }
+  out[e] = gauss_at(p / size, p % size, p0, p1, num, two_sig2);
+}
+
+// KL(target ‖ softmax(map + eps)) per token (ptp_utils.py:97-108)
+__global__ __launch_bounds__(kThreads) void kl_gauss_kernel(const float* __restrict__ maps, int h, int w, int num,
+                                                            float radius2, float two_sig2, float eps,
+                                                            double* __restrict__ kl) {
+  __shared__ float sv[kThreads / 64];
+  __shared__ int si[kThreads / 64];
+  __shared__ double sd[kThreads / 64];
+  __shared__ float sf[kThreads / 64];
+  __shared__ float pr[kMaxSubjects], pc[kMaxSubjects];
+  const float* m = maps + (size_t)blockIdx.x * h * w;
+  for (int q = 0; q < num; ++q) {
+    float best;
+    int bi;
+    row_argmax_masked(m, h, w, pr, pc, q, radius2, best, bi, sv, si);
+    if (threadIdx.x == 0) {
+      pr[q] = (float)(bi / w) + 0.5f;
+      pc[q] = (float)(bi % w) + 0.5f;
+    }
+    __syncthreads();
+  }
+  // target centres: (find_k_max_pixels / image_h) * size, size = image_h
+  float p0[kMaxSubjects], p1[kMaxSubjects];
+  for (int q = 0; q < num; ++q) {
+    p0[q] = (pr[q] / (float)h) * (float)h;
+    p1[q] = (pc[q] / (float)h) * (float)h;
+  }
+  const int HW = h * w;
+  float mx = -INFINITY;
+  for (int e = threadIdx.x; e < HW; e += kThreads) mx = fmaxf(mx, m[e] + eps);
+  mx = block_max(mx, sf);
+  double se = 0.0, sg = 0.0;
+  for (int e = threadIdx.x; e < HW; e += kThreads) {
+    se += (double)expf((m[e] + eps) - mx);
+    sg += (double)(gauss_at(e / w, e % w, p0, p1, num, two_sig2) + eps);
+  }
+  se = block_sum(se, sd);
+  sg = block_sum(sg, sd);
+  const float sef = (float)se, sgf = (float)sg;
+  double acc = 0.0;
+  for (int e = threadIdx.x; e < HW; e += kThreads) {
+    const float P = expf((m[e] + eps) - mx) / sef;
+    const float tg = (gauss_at(e / w, e % w, p0, p1, num, two_sig2) + eps) / sgf;
+    acc += (double)tg * ((double)logf(tg) - (double)logf(P));
+  }
+  acc = block_sum(acc, sd);
+  if (threadIdx.x == 0) kl[blockIdx.x] = acc;
+}
+
+// entropy of softmax(map) (ptp_utils.py:179-182; torch Categorical renormalises and clamps)
+__global__ __launch_bounds__(kThreads) void entropy_kernel(const float* __restrict__ maps, int h, int w,
+                                                           double* __restrict__ ent) {
+  __shared__ double sd[kThreads / 64];
+  __shared__ float sf[kThreads / 64];
+  const float* m = maps + (size_t)blockIdx.x * h * w;
+  const int HW = h * w;
+  float mx = -INFINITY;
+  for (int e = threadIdx.x; e < HW; e += kThreads) mx = fmaxf(mx, m[e]);
+  mx = block_max(mx, sf);
+  double se = 0.0;
+  for (int e = threadIdx.x; e < HW; e += kThreads) se += (double)expf(m[e] - mx);
+  se = block_sum(se, sd);
+  const float sef = (float)se;
+  double ps = 0.0;
+  for (int e = threadIdx.x; e < HW; e += kThreads) ps += (double)(expf(m[e] - mx) / sef);
+  ps = block_sum(ps, sd);
+  const float psf = (float)ps;
+  const float lo = 1.1920928955078125e-07f, hi = 1.0f - 1.1920928955078125e-07f;
+  double acc = 0.0;
+  for (int e = threadIdx.x; e < HW; e += kThreads) {
+    const float p = (expf(m[e] - mx) / sef) / psf;
+    const float pcl = fminf(fmaxf(p, lo), hi);
+    acc += (double)p * (double)logf(pcl);
+  }
+  acc = block_sum(acc, sd);
+  if (threadIdx.x == 0) ent[blockIdx.x] = -acc;
+}
+
+// Ascending sort of T double keys (NaN last, ties by index) -> first top_k indices.
+__device__ __forceinline__ bool key_less(double a, int ia, double b, int ib) {
+  const bool na = isnan(a), nb = isnan(b);
+  if (na || nb) return (!na && nb) || (na && nb && ia < ib);
+  return a < b || (a == b && ia < ib);
+}
+
+__global__ __launch_bounds__(1024) void sort_topk_kernel(const double* __restrict__ keys, int T, int n2, int top_k,
+                                                         long long* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* k = reinterpret_cast<double*>(smem);
+  int* id = reinterpret_cast<int*>(k + n2);
+  for (int i = threadIdx.x; i < n2; i += blockDim.x) {
+    k[i] = i < T ? keys[i] : INFINITY;
+    id[i] = i < T ? i : 0x7fffffff;
+  }
+  __syncthreads();
+  for (int size = 2; size <= n2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = threadIdx.x; i < n2; i += blockDim.x) {
+        const int l = i ^ stride;
+        if (l > i) {
+          const bool up = (i & size) == 0;
+          const bool lt = key_less(k[l], id[l], k[i], id[i]);
+          if (up == lt) {
+            const double tk = k[i]; k[i] = k[l]; k[l] = tk;
+            const int ti = id[i]; id[i] = id[l]; id[l] = ti;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = threadIdx.x; i < top_k; i += blockDim.x) out[i] = id[i];
+}
+
+// Furthest-point sampling over candidate positions (ptp_utils.py:115-159), one wave.
+__global__ __launch_bounds__(64) void fps_kernel(const float* __restrict__ cpos, const long long* __restrict__ cand,
+                                                 int C, int h, int top_k, long long* __restrict__ out,
+                                                 int* __restrict__ n_out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* pr = reinterpret_cast<float*>(smem);
+  float* pc = pr + C;
+  long long* tok = reinterpret_cast<long long*>(pc + C);  // 8·C bytes in: 8-aligned
+  long long* sel = tok + C;
+  float* spr = reinterpret_cast<float*>(sel + top_k);
+  float* spc = spr + top_k;
+  const int lane = threadIdx.x;
+  for (int i = lane; i < C; i += 64) {
+    pr[i] = cpos[2 * i] / (float)h;
+    pc[i] = cpos[2 * i + 1] / (float)h;
+    tok[i] = cand[i];
+  }
+  __syncthreads();
+  // 1) furthest pair: reference loops i < j in order with strict '>' (first wins).
+  float best = -1.0f;
+  long long brank = 0x7fffffffffffffffLL;
+  for (int i = lane; i < C; i += 64) {
+    for (int j = i + 1; j < C; ++j) {
+      const float dr = pr[i] - pr[j], dc = pc[i] - pc[j];
+      const float d = sqrt_rn(dr * dr + dc * dc);
+      if (d > best) { best = d; brank = (long long)i * C + j; }
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const long long orank = __shfl_xor(brank, o, 64);
+    if (ob > best || (ob == best && orank < brank)) { best = ob; brank = orank; }
+  }
+  int nsel = 0;
+  if (brank != 0x7fffffffffffffffLL) {
+    const int i0 = (int)(brank / C), j0 = (int)(brank % C);
+    if (lane == 0) {
+      sel[0] = tok[i0]; spr[0] = pr[i0]; spc[0] = pc[i0];
+      sel[1] = tok[j0]; spr[1] = pr[j0]; spc[1] = pc[j0];
+    }
+    nsel = 2;
+  }
+  __syncthreads();
+  // 2) greedy max-min additions (top_k - 2 rounds), candidates skipped if their token is selected
+  for (int round = 0; round < top_k - 2 && nsel >= 2; ++round) {
+    float bd = -1.0f;
+    int bi = 0x7fffffff;
+    for (int i = lane; i < C; i += 64) {
+      bool taken = false;
+      for (int q = 0; q < nsel; ++q) taken |= (sel[q] == tok[i]);
+      if (taken) continue;
+      float dmin = INFINITY;
+      bool nan_seen = false;
+      for (int q = 0; q < nsel; ++q) {
+        const float dr = pr[i] - spr[q], dc = pc[i] - spc[q];
+        const float d = sqrt_rn(dr * dr + dc * dc);
+        nan_seen |= isnan(d);
+        dmin = fminf(dmin, d);
+      }
+      if (nan_seen) dmin = NAN;  // torch.min propagates NaN
+      if (dmin > bd) { bd = dmin; bi = i; }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(bd, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ob > bd || (ob == bd && oi < bi)) { bd = ob; bi = oi; }
+    }
+    if (bi != 0x7fffffff) {
+      if (lane == 0) { sel[nsel] = tok[bi]; spr[nsel] = pr[bi]; spc[nsel] = pc[bi]; }
+      ++nsel;
+    }
+    __syncthreads();
+  }
+  for (int q = lane; q < top_k; q += 64) out[q] = q < nsel ? sel[q] : -1;
+  if (lane == 0 && n_out) *n_out = nsel;
+}
+
+// ------------------------------------------------------------------------------------ losses
+__global__ __launch_bounds__(kThreads) void sharpen_fwd_kernel(const float* __restrict__ A, int T, int h, int w,
+                                                               int num, float radius2, float two_sig2,
+                                                               float* __restrict__ pos, double* __restrict__ partial) {
+  __shared__ float sv[kThreads / 64];
+  __shared__ int si[kThreads / 64];
+  __shared__ double sd[kThreads / 64];
+  __shared__ float pr[kMaxSubjects], pc[kMaxSubjects];
+  const int row = blockIdx.x;
+  const float* m = A + (size_t)row * h * w;
+  for (int q = 0; q < num; ++q) {
+    float best;
+    int bi;
+    row_argmax_masked(m, h, w, pr, pc, q, radius2, best, bi, sv, si);
+    if (threadIdx.x == 0) {
+      pr[q] = (float)(bi / w) + 0.5f;
+      pc[q] = (float)(bi % w) + 0.5f;
+      // sharpening_loss: pos = find_k_max_pixels(A) / A.shape[-1]
+      pos[((size_t)q * T + row) * 2] = pr[q] / (float)w;
+      pos[((size_t)q * T + row) * 2 + 1] = pc[q] / (float)w;
+    }
+    __syncthreads();
+  }
+  float p0[kMaxSubjects], p1[kMaxSubjects];
+  for (int q = 0; q < num; ++q) {
+    p0[q] = (pr[q] / (float)w) * (float)h;
+    p1[q] = (pc[q] / (float)w) * (float)h;
+  }
+  double acc = 0.0;
+  const int HW = h * w;
+  for (int e = threadIdx.x; e < HW; e += kThreads) {
+    const float d = m[e] - gauss_at(e / w, e % w, p0, p1, num, two_sig2);
+    acc += (double)(d * d);
+  }
+  acc = block_sum(acc, sd);
+  if (threadIdx.x == 0) partial[row] = acc;
+}
+
+__global__ void finalize_mean_kernel(const double* __restrict__ partial, int n, double numel, float* __restrict__ out) {
+  __shared__ double sd[kThreads / 64];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) acc += partial[i];
+  acc = block_sum(acc, sd);
+  if (threadIdx.x == 0) out[0] = (float)(acc / numel);
+}
+
+__global__ void sharpen_bwd_kernel(const float* __restrict__ A, int T, int h, int w, int num, float two_sig2,
+                                   const float* __restrict__ pos, const float* __restrict__ gout, float norm,
+                                   float* __restrict__ dA) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t HW = (size_t)h * w;
+  if (e >= (size_t)T * HW) return;
+  const int t = e / HW, p = e % HW;
+  float p0[kMaxSubjects], p1[kMaxSubjects];
+  for (int q = 0; q < num; ++q) {
+    p0[q] = pos[((size_t)q * T + t) * 2] * (float)h;
+    p1[q] = pos[((size_t)q * T + t) * 2 + 1] * (float)h;
+  }
+  const float d = A[e] - gauss_at(p / w, p % w, p0, p1, num, two_sig2);
+  dA[e] = (d * norm) * gout[0];
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------ C ABI
+extern "C" int skp_argmax2d(const float* maps, int T, int h, int w, const long long* rows, int n_rows, float* pos,
+                            long long* idx, void* stream) {
+  SKP_CHECK_ARG(maps && (pos || idx), "null pointer");
+  SKP_CHECK_ARG(T > 0 && h > 0 && w > 0, "non-positive shape");
+  const int nr = rows ? n_rows : T;
+  SKP_CHECK_ARG(nr > 0, "no rows");
+  hipLaunchKernelGGL(argmax_kernel, dim3(nr), dim3(kThreads), 0, as_stream(stream), maps, T, h, w, rows, pos, idx);
+  SKP_LAUNCH_CHECK();
+  return SKP_OK;
+}
+
+extern "C" int skp_k_max_pixels(const float* maps, int T, int h, int w, int num, float radius2, float* pos,
+                                float* masked, void* stream) {
+  SKP_CHECK_ARG(maps && pos, "null pointer");
+  SKP_CHECK_ARG(T > 0 && h > 0 && w > 0, "non-positive shape");
+  SKP_CHECK_ARG(num >= 1 && num <= kMaxSubjects, "num out of range [1, 16]");
+  hipLaunchKernelGGL(kmax_kernel, dim3(T), dim3(kThreads), 0, as_stream(stream), maps, T, h, w, num, radius2, pos,
+                     masked);
+  SKP_LAUNCH_CHECK();
+  return SKP_OK;
+}
+
+extern "C" int skp_mask_radius(const float* maps, int T, int h, int w, const float* pos, float radius2, float* out,
+                               void* stream) {
+  SKP_CHECK_ARG(maps && pos && out, "null pointer");
+  SKP_CHECK_ARG(T > 0 && h > 0 && w > 0, "non-positive shape");
+  const size_t total = (size_t)T * h * w;
+  hipLaunchKernelGGL(mask_radius_kernel, dim3((total + 255) / 256), dim3(256), 0, as_stream(stream), maps, T, h, w, pos,
+                     radius2, out);
+  SKP_LAUNCH_CHECK();
+  return SKP_OK;
+}
+
+extern "C" int skp_weighted_avg(float* maps, int T, int h, int w, float distance, int mutate, float* pos,
+                                void* stream) {
+  SKP_CHECK_ARG(maps && pos, "null pointer");
+  SKP_CHECK_ARG(T > 0 && h > 0 && w > 0, "non-positive shape");
+  hipLaunchKernelGGL(weighted_avg_kernel, dim3(T), dim3(kThreads), 0, as_stream(stream), maps, h, w, distance, mutate,
+                     pos);
+  SKP_LAUNCH_CHECK();
+  return SKP_OK;
+}
+
+extern "C" int skp_gaussian_target(const float* pos, int num, int T, int size, float sigma, float* out, void* stream) {
+  SKP_CHECK_ARG(pos && out, "null pointer");
+  SKP_CHECK_ARG(T > 0 && size > 0, "non-positive shape");
+  SKP_CHECK_ARG(num >= 1 && num <= kMaxSubjects, "num out of range [1, 16]");
+  const float two_sig2 = (float)(2.0 * (double)sigma * (double)sigma);
+  const size_t total = (size_t)T * size * size;
+  hipLaunchKernelGGL(gaussian_target_kernel, dim3((total + 255) / 256), dim3(256), 0, as_stream(stream), pos, num, T,
+                     size, two_sig2, out);
+  SKP_LAUNCH_CHECK();
+  return SKP_OK;
+}
+
+static int launch_sort(const double* keys, int T, int top_k, long long* out, hipStream_t st) {
+  int n2 = 1;
+  while (n2 < T) n2 <<= 1;
+  SKP_CHECK_ARG(n2 <= 8192, "T > 8192 tokens is not supported by the selection sort");
+  const size_t lds = (size_t)n2 * (sizeof(double) + sizeof(int));
+  hipLaunchKernelGGL(sort_topk_kernel, dim3(1), dim3(1024), lds, st, keys, T, n2, top_k, out);
+  SKP_LAUNCH_CHECK();
+  return SKP_OK;
+}
+
+extern "C" int skp_topk_gaussian(const float* maps, int T, int h, int w, int top_k, float sigma, float epsilon,
+                                 int num_subjects, long long* out, double* kl, void* workspace, void* stream) {
+  SKP_CHECK_ARG(maps && out && workspace, "null pointer");
+  SKP_CHECK_ARG(T > 0 && h > 0 && w > 0, "non-positive shape");
+  SKP_CHECK_ARG(top_k >= 0 && top_k <= T, "top_k out of range");
+  SKP_CHECK_ARG(num_subjects >= 1 && num_subjects <= kMaxSubjects, "num_subjects out of range [1, 16]");
+  double* keys = kl ? kl : reinterpret_cast<double*>(workspace);
+  const double rad = 0.05 * (double)h;
+  const float radius2 = (float)(rad * rad);
+  const float two_sig2 = (float)(2.0 * (double)sigma * (double)sigma);
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(kl_gauss_kernel, dim3(T), dim3(kThreads), 0, st, maps, h, w, num_subjects, radius2, two_sig2,
+                     epsilon, keys);
+  SKP_LAUNCH_CHECK();
+  if (top_k == 0) return SKP_OK;
+  return launch_sort(keys, T, top_k, out, st);
+}
+
+extern "C" int skp_entropy_sort(const float* maps, int T, int h, int w, int top_k, long long* out, double* ent,
+                                void* workspace, void* stream) {
+  SKP_CHECK_ARG(maps && out && workspace, "null pointer");
+  SKP_CHECK_ARG(T > 0 && h > 0 && w > 0, "non-positive shape");
+  SKP_CHECK_ARG(top_k >= 0 && top_k <= T, "top_k out of range");
+  double* keys = ent ? ent : reinterpret_cast<double*>(workspace);
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(entropy_kernel, dim3(T), dim3(kThreads), 0, st, maps, h, w, keys);
+  SKP_LAUNCH_CHECK();
+  if (top_k == 0) return SKP_OK;
+  return launch_sort(keys, T, top_k, out, st);
+}
+
+extern "C" int skp_fps(const float* maps, int T, int h, int w, const long long* cand, int n_cand, int top_k,
+                       long long* out, int* n_out, void* workspace, void* stream) {
+  SKP_CHECK_ARG(maps && cand && out && workspace, "null pointer");
+  SKP_CHECK_ARG(T > 0 && h > 0 && w > 0, "non-positive shape");
+  SKP_CHECK_ARG(n_cand >= 2, "furthest_point_sampling needs at least two candidates");
+  SKP_CHECK_ARG(n_cand <= 4096, "n_cand > 4096");
+  SKP_CHECK_ARG(top_k >= 2 && top_k <= 1024, "top_k out of range [2, 1024]");
+  hipStream_t st = as_stream(stream);
+  float* cpos = reinterpret_cast<float*>(workspace);
+  hipLaunchKernelGGL(argmax_kernel, dim3(n_cand), dim3(kThreads), 0, st, maps, T, h, w, cand, cpos,
+                     (long long*)nullptr);
+  SKP_LAUNCH_CHECK();
+  const size_t lds = (size_t)n_cand * 8 + (size_t)n_cand * 8 + (size_t)top_k * 8 + (size_t)top_k * 8;
+  SKP_CHECK_ARG(lds <= 64 * 1024, "fps LDS budget exceeded");
+  hipLaunchKernelGGL(fps_kernel, dim3(1), dim3(64), lds, st, cpos, cand, n_cand, h, top_k, out, n_out);
+  SKP_LAUNCH_CHECK();
+  return SKP_OK;
+}
+
+extern "C" int skp_sharpen_fwd(const float* A, int T, int h, int w, float sigma, int num_subjects, float* pos,
+                               double* partial, float* loss, void* stream) {
+  SKP_CHECK_ARG(A && pos && partial && loss, "null pointer");
+  SKP_CHECK_ARG(T > 0 && h > 0 && w > 0, "non-positive shape");
+  SKP_CHECK_ARG(num_subjects >= 1 && num_subjects <= kMaxSubjects, "num_subjects out of range [1, 16]");
+  const double rad = 0.05 * (double)h;
+  const float radius2 = (float)(rad * rad);
+  const float two_sig2 = (float)(2.0 * (double)sigma * (double)sigma);
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(sharpen_fwd_kernel, dim3(T), dim3(kThreads), 0, st, A, T, h, w, num_subjects, radius2, two_sig2,
+                     pos, partial);
+  SKP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(finalize_mean_kernel, dim3(1), dim3(kThreads), 0, st, partial, T, (double)T * h * w, loss);
+  SKP_LAUNCH_CHECK();
+  return SKP_OK;
+}
+
+extern "C" int skp_sharpen_bwd(const float* A, int T, int h, int w, float sigma, int num_subjects, const float* pos,
+                               const float* gout, float* dA, void* stream) {
+  SKP_CHECK_ARG(A && pos && gout && dA, "null pointer");
+  SKP_CHECK_ARG(T > 0 && h > 0 && w > 0, "non-positive shape");
+  SKP_CHECK_ARG(num_subjects >= 1 && num_subjects <= kMaxSubjects, "num_subjects out of range [1, 16]");
+  const float two_sig2 = (float)(2.0 * (double)sigma * (double)sigma);
+  const float norm = (float)(2.0 / ((double)T * h * w));
+  const size_t total = (size_t)T * h * w;
+  hipLaunchKernelGGL(sharpen_bwd_kernel, dim3((total + 255) / 256), dim3(256), 0, as_stream(stream), A, T, h, w,
+                     num_subjects, two_sig2, pos, gout, norm, dA);
+  SKP_LAUNCH_CHECK();
+  return SKP_OK;
+}

@@ -1,0 +1,60 @@
+"""Random affine warp with exact inverse (reference ``invertable_transform.py:6-92``).
+
+The warp itself (affine_grid + grid_sample, bilinear, zeros, align_corners=False)
+runs as the HIP kernel ``skp_affine_warp`` (with its adjoint for gradients);
+theta is drawn on the host exactly as the reference draws it (``torch.rand`` on
+the CPU generator, in the order angle, scale, tx, ty per sample), so seeded runs
+reproduce the reference's augmentations.
+"""
+import math
+
+import torch
+
+from . import ops
+
+
+class RandomAffineWithInverse:
+    def __init__(self, degrees=0, scale=(1.0, 1.0), translate=(0.0, 0.0)):
+        self.degrees = degrees
+        self.scale = scale
+        self.translate = translate
+        self.last_params = {"theta": torch.eye(2, 3).unsqueeze(0)}
+
+    def create_affine_matrix(self, angle, scale, translations_percent):
+        """invertable_transform.py:22-36."""
+        a = math.radians(angle)
+        theta = torch.tensor([[math.cos(a), math.sin(a), translations_percent[0]],
+                              [-math.sin(a), math.cos(a), translations_percent[1]]], dtype=torch.float)
+        theta[:, :2] = theta[:, :2] * scale
+        return theta.unsqueeze(0)
+
+    def draw_theta(self, batch):
+        """invertable_transform.py:40-57 (same RNG calls, same order)."""
+        thetas = []
+        for _ in range(batch):
+            angle = torch.rand(1).item() * (2 * self.degrees) - self.degrees
+            sf = torch.rand(1).item() * (self.scale[1] - self.scale[0]) + self.scale[0]
+            tp = (torch.rand(1).item() * (2 * self.translate[0]) - self.translate[0],
+                  torch.rand(1).item() * (2 * self.translate[1]) - self.translate[1])
+            thetas.append(self.create_affine_matrix(angle, sf, tp))
+        return torch.cat(thetas, dim=0)
+
+    def __call__(self, img_tensor, theta=None):
+        if theta is None:
+            theta = self.draw_theta(img_tensor.shape[0])
+        self.last_params = {"theta": theta.detach().cpu().float()}
+        return ops.affine_warp(img_tensor, theta.to(img_tensor.device, torch.float32))
+
+    def theta_inverse(self):
+        """2×3 part of the 3×3 inverse of each stored theta (invertable_transform.py:77-84)."""
+        theta = self.last_params["theta"].double()
+        aug = torch.cat([theta, torch.tensor([[[0.0, 0.0, 1.0]]], dtype=torch.float64).expand(theta.shape[0], -1, -1)],
+                        dim=1)
+        return torch.inverse(aug)[:, :2, :].float()
+
+    def inverse(self, img_tensor):
+        """invertable_transform.py:72-92: warp by the inverse of the stored thetas."""
+        th = self.theta_inverse()
+        if th.shape[0] != img_tensor.shape[0]:
+            raise ValueError(f"inverse: {img_tensor.shape[0]} images but {th.shape[0]} stored thetas")
+        return ops.affine_warp(img_tensor, th.to(img_tensor.device))

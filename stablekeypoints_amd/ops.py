@@ -1,0 +1,336 @@
+"""Torch-facing ops over libskp (HIP, gfx950): autograd Functions and plain wrappers.
+
+Every function here launches the HIP kernels through the C ABI (``_lib``) on the
+current HIP stream; there is no CPU or eager-torch fallback for the hot path.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream
+
+F32 = torch.float32
+
+
+def _c(t, dtype=F32):
+    return t.contiguous() if t.dtype == dtype else t.to(dtype).contiguous()
+
+
+# --------------------------------------------------------------------------- Q·Kᵀ on MFMA
+def bgemm(a, b, alpha=1.0, out=None, accumulate=False):
+    """out[z] = alpha · a[z] @ b[z] for 3-D fp32 tensors of any strides (skp_bgemm_f32)."""
+    _lib.require_device(a, b)
+    Z, M, K = a.shape
+    Z2, K2, N = b.shape
+    assert Z == Z2 and K == K2, (a.shape, b.shape)
+    if out is None:
+        out = torch.empty(Z, M, N, device=a.device, dtype=F32)
+    call("skp_bgemm_f32", ptr(a), a.stride(0), a.stride(1), a.stride(2), ptr(b), b.stride(0), b.stride(1),
+         b.stride(2), ptr(out), out.stride(0), out.stride(1), out.stride(2), Z, M, N, K, float(alpha),
+         int(accumulate), stream(a.device))
+    return out
+
+
+class CaptureLogits(torch.autograd.Function):
+    """z = q kᵀ · scale — the layer's cross-attention logits (ptp_utils.py:493 / 534)."""
+
+    @staticmethod
+    def forward(ctx, q, k, scale):
+        q, k = _c(q), _c(k)
+        ctx.save_for_backward(q, k)
+        ctx.scale = scale
+        return bgemm(q, k.transpose(1, 2), scale)
+
+    @staticmethod
+    def backward(ctx, dz):
+        q, k = ctx.saved_tensors
+        dz = _c(dz)
+        dq = dk = None
+        if ctx.needs_input_grad[0]:
+            dq = bgemm(dz, k, ctx.scale)
+        if ctx.needs_input_grad[1]:
+            dk = bgemm(dz.transpose(1, 2), q, ctx.scale)
+        return dq, dk, None
+
+
+def capture_logits(q, k, scale):
+    return CaptureLogits.apply(q, k, float(scale))
+
+
+# --------------------------------------------------------------------------- A1 capture
+class CaptureAttn(torch.autograd.Function):
+    """attn = softmax_N(bicubic_{s→R}(z_low)) — the captured map (ptp_utils.py:513-536)."""
+
+    @staticmethod
+    def forward(ctx, z, s, R):
+        z = _c(z)
+        BH, S, N = z.shape
+        assert S == s * s
+        attn = torch.empty(BH, R * R, N, device=z.device, dtype=F32)
+        call("skp_capture_fwd", ptr(z), BH, s, N, R, ptr(attn), stream(z.device))
+        ctx.save_for_backward(z)
+        ctx.s, ctx.R = s, R
+        return attn
+
+    @staticmethod
+    def backward(ctx, dattn):
+        (z,) = ctx.saved_tensors
+        return capture_bwd(z, ctx.s, ctx.R, dattn), None, None
+
+
+def capture_bwd(z, s, R, dattn, gscale=1.0):
+    BH, S, N = z.shape
+    if dattn.dtype != F32:
+        dattn = dattn.float()
+    sb, sp, sn = dattn.stride()
+    if dattn.shape[0] == 1 and BH > 1:
+        sb = 0
+    ws = torch.empty(BH, R, s, N, device=z.device, dtype=F32)
+    dz = torch.empty_like(z)
+    call("skp_capture_bwd", ptr(z), BH, s, N, R, ptr(dattn), sb, sp, sn, float(gscale), ptr(dz), ptr(ws),
+         stream(z.device))
+    return dz
+
+
+def capture_attn(z, s, R):
+    return CaptureAttn.apply(z, int(s), int(R))
+
+
+# --------------------------------------------------------------------------- A3 aggregate
+class _Aggregate(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, indices, upsample_res, *layers):
+        layers = [_c(t) for t in layers]
+        BH, RR, N = layers[0].shape
+        R = int(round(RR ** 0.5))
+        for t in layers:
+            if t.shape != layers[0].shape:
+                raise ValueError("collect_maps: captured layers must share (BH, R*R, N); got "
+                                 f"{[tuple(x.shape) for x in layers]}")
+        arr = (ctypes.c_void_p * len(layers))(*[t.data_ptr() for t in layers])
+        n_out = N if indices is None else int(indices.numel())
+        out = torch.empty(n_out, R, R, device=layers[0].device, dtype=F32)
+        idx = None if indices is None else indices.to(device=out.device, dtype=torch.int64).contiguous()
+        call("skp_aggregate", ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)), len(layers), BH, RR, N, ptr(idx),
+             n_out, ptr(out), stream(out.device))
+        ctx.meta = (BH, RR, N, R, len(layers))
+        ctx.idx = idx
+        ctx.upsample_res = upsample_res
+        if upsample_res != -1 and upsample_res != R:
+            up = torch.empty(n_out, upsample_res, upsample_res, device=out.device, dtype=F32)
+            call("skp_resize_bilinear", ptr(out), n_out, R, upsample_res, ptr(up), stream(out.device))
+            out = up
+        return out
+
+    @staticmethod
+    def backward(ctx, dmap):
+        BH, RR, N, R, L = ctx.meta
+        dmap = _c(dmap)
+        if ctx.upsample_res != -1 and ctx.upsample_res != R:
+            g = torch.empty(dmap.shape[0], R, R, device=dmap.device, dtype=F32)
+            call("skp_resize_bilinear_bwd", ptr(dmap), dmap.shape[0], R, ctx.upsample_res, ptr(g), stream(dmap.device))
+            dmap = g
+        dmap = dmap.reshape(-1, RR) / float(L * BH)
+        if ctx.idx is not None:
+            full = torch.zeros(N, RR, device=dmap.device, dtype=F32)
+            full.index_add_(0, ctx.idx, dmap)
+            dmap = full
+        # d attn_l[b, p, n] = dmap[n, p] / (L·BH): a stride-0 broadcast view, never materialised
+        g = dmap.t().unsqueeze(0).expand(BH, RR, N)
+        return (None, None) + tuple(g for _ in range(L))
+
+
+def aggregate(layers, indices=None, upsample_res=-1):
+    return _Aggregate.apply(indices, int(upsample_res), *layers)
+
+
+# --------------------------------------------------------------------------- A4-A6 argmax family
+def find_max_pixel(maps):
+    _lib.require_device(maps)
+    maps = _c(maps)
+    T, h, w = maps.shape
+    pos = torch.empty(T, 2, device=maps.device, dtype=F32)
+    call("skp_argmax2d", ptr(maps), T, h, w, None, 0, ptr(pos), None, stream(maps.device))
+    return pos
+
+
+def argmax_index(maps):
+    maps = _c(maps)
+    T, h, w = maps.shape
+    idx = torch.empty(T, device=maps.device, dtype=torch.int64)
+    call("skp_argmax2d", ptr(maps), T, h, w, None, 0, None, ptr(idx), stream(maps.device))
+    return idx
+
+
+def _radius2(h):
+    r = 0.05 * h
+    return float(r ** 2)
+
+
+def find_k_max_pixels(maps, num=3, return_masked=False):
+    _lib.require_device(maps)
+    maps = _c(maps)
+    T, h, w = maps.shape
+    pos = torch.empty(num, T, 2, device=maps.device, dtype=F32)
+    masked = torch.empty_like(maps) if return_masked else None
+    call("skp_k_max_pixels", ptr(maps), T, h, w, int(num), _radius2(h), ptr(pos), ptr(masked), stream(maps.device))
+    return (pos, masked) if return_masked else pos
+
+
+def mask_radius(maps, max_coords, radius):
+    _lib.require_device(maps)
+    maps = _c(maps)
+    T, h, w = maps.shape
+    out = torch.empty_like(maps)
+    call("skp_mask_radius", ptr(maps), T, h, w, ptr(_c(max_coords)), float(radius) ** 2, ptr(out),
+         stream(maps.device))
+    return out
+
+
+def pixel_from_weighted_avg(heatmaps, distance=5):
+    """Mutates ``heatmaps`` in place like the reference (eval.py:137) when it is contiguous fp32."""
+    _lib.require_device(heatmaps)
+    T, h, w = heatmaps.shape
+    work = heatmaps if (heatmaps.is_contiguous() and heatmaps.dtype == F32) else heatmaps.float().contiguous()
+    pos = torch.empty(T, 2, device=heatmaps.device, dtype=F32)
+    call("skp_weighted_avg", ptr(work), T, h, w, float(distance) if distance != -1 else -1.0, 1, ptr(pos),
+         stream(heatmaps.device))
+    if work is not heatmaps:
+        heatmaps.copy_(work)
+    return pos
+
+
+# --------------------------------------------------------------------------- A7 targets
+def gaussian_circles(pos, size, sigma):
+    """pos (num, T, 2) in [0,1] -> (T, size, size); (T, 2) is treated as num = 1."""
+    _lib.require_device(pos)
+    pos = _c(pos)
+    if pos.dim() == 2:
+        pos = pos.unsqueeze(0)
+    num, T, _ = pos.shape
+    out = torch.empty(T, size, size, device=pos.device, dtype=F32)
+    call("skp_gaussian_target", ptr(pos), num, T, int(size), float(sigma), ptr(out), stream(pos.device))
+    return out
+
+
+# --------------------------------------------------------------------------- A8-A10 selection
+def find_top_k_gaussian(maps, top_k, sigma=3, epsilon=1e-5, num_subjects=1, return_kl=False):
+    _lib.require_device(maps)
+    maps = _c(maps)
+    T, h, w = maps.shape
+    out = torch.empty(top_k, device=maps.device, dtype=torch.int64)
+    kl = torch.empty(T, device=maps.device, dtype=torch.float64)
+    call("skp_topk_gaussian", ptr(maps), T, h, w, int(top_k), float(sigma), float(epsilon), int(num_subjects),
+         ptr(out), ptr(kl), ptr(kl), stream(maps.device))
+    return (out, kl) if return_kl else out
+
+
+def entropy_sort(maps, top_k, return_entropy=False):
+    _lib.require_device(maps)
+    maps = _c(maps)
+    T, h, w = maps.shape
+    out = torch.empty(top_k, device=maps.device, dtype=torch.int64)
+    ent = torch.empty(T, device=maps.device, dtype=torch.float64)
+    call("skp_entropy_sort", ptr(maps), T, h, w, int(top_k), ptr(out), ptr(ent), ptr(ent), stream(maps.device))
+    return (out, ent) if return_entropy else out
+
+
+def furthest_point_sampling(maps, top_k, candidates):
+    """Returns (selected int64 (top_k,), count int32 device scalar)."""
+    _lib.require_device(maps)
+    maps = _c(maps)
+    T, h, w = maps.shape
+    cand = candidates.to(device=maps.device, dtype=torch.int64).contiguous()
+    out = torch.empty(top_k, device=maps.device, dtype=torch.int64)
+    n_out = torch.empty(1, device=maps.device, dtype=torch.int32)
+    ws = torch.empty(2 * cand.numel() + 2, device=maps.device, dtype=F32)
+    call("skp_fps", ptr(maps), T, h, w, ptr(cand), cand.numel(), int(top_k), ptr(out), ptr(n_out), ptr(ws),
+         stream(maps.device))
+    return out, n_out
+
+
+# --------------------------------------------------------------------------- A11 / A12 losses
+class SharpeningLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, A, sigma, num_subjects):
+        A = _c(A)
+        T, h, w = A.shape
+        pos = torch.empty(num_subjects, T, 2, device=A.device, dtype=F32)
+        part = torch.empty(T, device=A.device, dtype=torch.float64)
+        loss = torch.empty((), device=A.device, dtype=F32)
+        call("skp_sharpen_fwd", ptr(A), T, h, w, float(sigma), int(num_subjects), ptr(pos), ptr(part), ptr(loss),
+             stream(A.device))
+        ctx.save_for_backward(A, pos)
+        ctx.sigma, ctx.num = sigma, num_subjects
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        A, pos = ctx.saved_tensors
+        T, h, w = A.shape
+        dA = torch.empty_like(A)
+        call("skp_sharpen_bwd", ptr(A), T, h, w, float(ctx.sigma), int(ctx.num), ptr(pos), ptr(_c(g.reshape(1))),
+             ptr(dA), stream(A.device))
+        return dA, None, None
+
+
+def sharpening_loss(A, sigma=1.0, num_subjects=1):
+    _lib.require_device(A)
+    return SharpeningLoss.apply(A, float(sigma), int(num_subjects))
+
+
+class AffineWarp(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, theta):
+        x = _c(x)
+        B, C, H, W = x.shape
+        th = _c(theta.to(x.device))
+        out = torch.empty_like(x)
+        call("skp_affine_warp", ptr(x), B, C, H, W, ptr(th), ptr(out), stream(x.device))
+        ctx.save_for_backward(th)
+        ctx.shape = (B, C, H, W)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (th,) = ctx.saved_tensors
+        B, C, H, W = ctx.shape
+        gin = torch.empty(B, C, H, W, device=g.device, dtype=F32)
+        call("skp_affine_warp_bwd", ptr(_c(g)), B, C, H, W, ptr(th), ptr(gin), stream(g.device))
+        return gin, None
+
+
+def affine_warp(x, theta):
+    """grid_sample(x, affine_grid(theta)) (bilinear, zeros, align_corners=False); x (B,C,H,W)."""
+    _lib.require_device(x)
+    return AffineWarp.apply(x, theta)
+
+
+class EquivarianceLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, A, At, theta_inv):
+        A, At = _c(A), _c(At)
+        T, h, w = A.shape
+        th = _c(theta_inv.to(A.device)).reshape(6)
+        part = torch.empty(T, device=A.device, dtype=torch.float64)
+        loss = torch.empty((), device=A.device, dtype=F32)
+        call("skp_equiv_fwd", ptr(A), ptr(At), T, h, w, ptr(th), ptr(part), ptr(loss), stream(A.device))
+        ctx.save_for_backward(A, At, th)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        A, At, th = ctx.saved_tensors
+        T, h, w = A.shape
+        dA = torch.empty_like(A) if ctx.needs_input_grad[0] else None
+        dAt = torch.empty_like(At)
+        call("skp_equiv_bwd", ptr(A), ptr(At), T, h, w, ptr(th), ptr(_c(g.reshape(1))), ptr(dA), ptr(dAt),
+             stream(A.device))
+        return dA, (dAt if ctx.needs_input_grad[1] else None), None
+
+
+def equivariance_loss_single(A, At, theta_inv):
+    """mean((A − warp(At, theta_inv))²) with gradients into A and At."""
+    _lib.require_device(A, At)
+    return EquivarianceLoss.apply(A, At, theta_inv)

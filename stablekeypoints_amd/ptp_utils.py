@@ -1,0 +1,227 @@
+"""Attention capture hook, store and token selection (mirror of reference ``ptp_utils.py``).
+
+Same names, signatures and semantics as the reference; the capture branch, the
+aggregation it feeds and the selection heuristics run as HIP kernels (libskp).
+
+Capture algebra: the reference recomputes
+``softmax(to_q(bicubic(x)) kᵀ·scale)`` at R×R (``ptp_utils.py:513-536``).
+bicubic and to_q are linear and commute with ·kᵀ, so this equals
+``softmax(bicubic(q kᵀ·scale))`` where ``q kᵀ·scale`` is the layer's own
+normal-path logit matrix at s×s.  The patched forward therefore computes the
+logits once on the matrix cores (``skp_bgemm_f32``), feeds them to the normal
+softmax·V path, and hands them to ``skp_capture_fwd`` for the R×R capture:
+≈248 GFLOP of dense work per capture in the reference becomes ≈1.6 GFLOP plus
+an HBM-bound upsample/softmax kernel.
+"""
+import abc
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import ops
+from .sd.unet import CaptureComplete, attention_core
+
+
+# --------------------------------------------------------------------------- A2 controller / store
+class AttentionControl(abc.ABC):
+    """ptp_utils.py:32-60."""
+
+    def step_callback(self, x_t):
+        return x_t
+
+    def between_steps(self):
+        return
+
+    @property
+    def num_uncond_att_layers(self):
+        return 0
+
+    @abc.abstractmethod
+    def forward(self, dict, is_cross: bool, place_in_unet: str):
+        raise NotImplementedError
+
+    def __call__(self, dict, is_cross: bool, place_in_unet: str):
+        dict = self.forward(dict, is_cross, place_in_unet)
+        return dict["attn"]
+
+    def reset(self):
+        self.cur_step = 0
+        self.cur_att_layer = 0
+
+    def __init__(self):
+        self.cur_step = 0
+        self.num_att_layers = -1
+        self.cur_att_layer = 0
+
+
+class AttentionStore(AttentionControl):
+    """ptp_utils.py:63-83: ``step_store["attn"]`` lists captured (B·H, R², N) maps in order.
+
+    ``early_exit`` (default False = reference behaviour): when True, the patched
+    attention raises ``CaptureComplete`` once the 4th map is stored, so the UNet
+    forward stops there; the reference discards that forward's output anyway
+    (``ptp_utils.py:246-252``) and nothing later feeds the loss.
+    """
+
+    max_captures = 4
+
+    @staticmethod
+    def get_empty_store():
+        return {"attn": []}
+
+    def forward(self, dict, is_cross: bool, place_in_unet: str):
+        self.step_store["attn"].append(dict["attn"])
+        return dict
+
+    def reset(self):
+        super().reset()
+        self.step_store = self.get_empty_store()
+
+    def __init__(self, early_exit=False):
+        super().__init__()
+        self.step_store = self.get_empty_store()
+        self.early_exit = early_exit
+
+
+# --------------------------------------------------------------------------- A1 capture hook
+def register_attention_control(model, controller, feature_upsample_res=256):
+    """ptp_utils.py:472-573: patch every ``CrossAttention`` under children named "*up*"."""
+
+    def ca_forward(self, place_in_unet):
+        to_out = self.to_out
+        if type(to_out) is torch.nn.modules.container.ModuleList:
+            to_out = self.to_out[0]
+
+        def forward(x, context=None, mask=None):
+            batch_size, sequence_length, dim = x.shape
+            h = self.heads
+            q = self.to_q(x)
+            is_cross = context is not None
+            context = context if is_cross else x
+            k = self.to_k(context)
+            v = self.to_v(context)
+            q = self.reshape_heads_to_batch_dim(q)
+            k = self.reshape_heads_to_batch_dim(k)
+            v = self.reshape_heads_to_batch_dim(v)
+            capture = (is_cross and sequence_length <= 32 ** 2
+                       and len(controller.step_store["attn"]) < AttentionStore.max_captures)
+            if capture:
+                s = int(sequence_length ** 0.5)
+                if s * s != sequence_length:
+                    raise ValueError(f"capture needs a square token grid, got {sequence_length}")
+                sim = ops.capture_logits(q, k, self.scale)          # (B·H, s², N), MFMA
+                sim_n = sim
+                if mask is not None:   # the mask applies to the normal path only (ptp_utils.py:496-500)
+                    m = mask.reshape(batch_size, -1)[:, None, :].repeat(h, 1, 1)
+                    sim_n = sim.masked_fill(~m, -torch.finfo(sim.dtype).max)
+                out = torch.bmm(sim_n.softmax(dim=-1), v)
+                attn = ops.capture_attn(sim, s, feature_upsample_res)  # (B·H, R², N), HIP
+                controller({"attn": attn}, is_cross, place_in_unet)
+            else:
+                out = attention_core(q, k, v, self.scale, mask, h)
+            out = to_out(self.reshape_batch_dim_to_heads(out))
+            if capture and getattr(controller, "early_exit", False) and \
+                    len(controller.step_store["attn"]) >= AttentionStore.max_captures:
+                raise CaptureComplete()
+            return out
+
+        return forward
+
+    class DummyController:
+        def __call__(self, *args):
+            return args[0]
+
+        def __init__(self):
+            self.num_att_layers = 0
+            self.step_store = {"attn": []}
+
+    if controller is None:
+        controller = DummyController()
+
+    def register_recr(net_, count, place_in_unet):
+        if net_.__class__.__name__ == "CrossAttention":
+            net_.forward = ca_forward(net_, place_in_unet)
+            return count + 1
+        elif hasattr(net_, "children"):
+            for net__ in net_.children():
+                count = register_recr(net__, count, place_in_unet)
+        return count
+
+    cross_att_count = 0
+    for name, net in model.named_children():
+        if "up" in name:
+            cross_att_count += register_recr(net, 0, "up")
+    controller.num_att_layers = cross_att_count
+    assert cross_att_count != 0, "No cross attention layers found in the model. Please check to make sure " \
+                                 "you're using diffusers==0.8.0."
+
+
+# --------------------------------------------------------------------------- A8-A10 selection
+def find_top_k_gaussian(attention_maps, top_k, sigma=3, epsilon=1e-5, num_subjects=1):
+    """ptp_utils.py:86-112 (skp_topk_gaussian)."""
+    return ops.find_top_k_gaussian(attention_maps, top_k, sigma=sigma, epsilon=epsilon, num_subjects=num_subjects)
+
+
+def furthest_point_sampling(attention_maps, top_k, top_initial_candidates):
+    """ptp_utils.py:115-159 (skp_fps).  Returns the selected token ids (int64, device)."""
+    sel, n = ops.furthest_point_sampling(attention_maps, top_k, top_initial_candidates)
+    if top_k > len(top_initial_candidates):   # the reference returns fewer when candidates run out
+        return sel[: int(n.item())]
+    return sel
+
+
+def entropy_sort(attention_maps, top_k, min_dist=0.05):
+    """ptp_utils.py:165-187 (skp_entropy_sort)."""
+    return ops.entropy_sort(attention_maps, top_k)
+
+
+def random_range(size, min_val, max_val, dtype=torch.float32):
+    return torch.rand(size, dtype=dtype) * (max_val - min_val) + min_val
+
+
+# --------------------------------------------------------------------------- A14 capture driver
+def image2latent(model, image, device):
+    """ptp_utils.py:289-304: (2x−1) → VAE encoder mean · 0.18215 (kept on the device)."""
+    with torch.no_grad():
+        if isinstance(image, np.ndarray):
+            image = torch.from_numpy(image).float().permute(0, 3, 1, 2)
+        if image.dim() == 4 and image.shape[1] == 4:   # already a latent
+            return image.to(device)
+        image = image.to(device, torch.float32) * 2 - 1
+        vae = model.vae.module if isinstance(model.vae, nn.DataParallel) else model.vae
+        return vae.encode(image)["latent_dist"].mean * 0.18215
+
+
+def find_pred_noise(ldm, image, context, noise_level=-1, device="cuda"):
+    """ptp_utils.py:205-231.  The UNet output is None when the store stops the forward early."""
+    with torch.no_grad():
+        latent = image2latent(ldm, image, device)
+    noise = torch.randn_like(latent)
+    t = ldm.scheduler.timesteps[noise_level]
+    noisy_image = ldm.scheduler.add_noise(latent, noise, t)
+    try:
+        pred_noise = ldm.unet(noisy_image, t.repeat(noisy_image.shape[0]),
+                              context.repeat(noisy_image.shape[0], 1, 1))["sample"]
+    except CaptureComplete:
+        pred_noise = None
+    return noise, pred_noise
+
+
+def run_and_find_attn(ldm, image, context, noise_level=-1, device="cuda",
+                      from_where=("down_cross", "mid_cross", "up_cross"), layers=(0, 1, 2, 3, 4, 5),
+                      upsample_res=32, indices=None, controllers=None):
+    """ptp_utils.py:234-272: one UNet pass, then collect_maps + reset per controller."""
+    from .optimize import collect_maps
+    find_pred_noise(ldm, image, context, noise_level=noise_level, device=device)
+    attention_maps = []
+    for controller in controllers:
+        attention_maps.append(collect_maps(controllers[controller], from_where=from_where,
+                                           upsample_res=upsample_res, layers=layers, indices=indices))
+        controllers[controller].reset()
+    return attention_maps
+
+
+def init_random_noise(device, num_words=77, dim=768):
+    """ptp_utils.py:649-650 (CPU RNG, then moved), ``dim`` generalises the hard-coded 768."""
+    return torch.randn(1, num_words, dim).to(device)

@@ -1,0 +1,50 @@
+"""CPU-side checks of the C ABI: the library loads, exports every declared symbol, and
+rejects bad arguments before touching the device (no GPU needed)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    hdr = open(os.path.join(REPO, "include", "skp.h")).read()
+    return sorted(set(re.findall(r"\b(skp_[a-z0-9_]+)\s*\(", hdr)))
+
+
+def test_header_matches_binding_table():
+    from stablekeypoints_amd import _lib
+    assert sorted(_lib.exported_symbols()) == declared_symbols()
+
+
+def test_library_exports_every_symbol():
+    from stablekeypoints_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libskp.so not built (run __graft_entry__.build())")
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [s for s in declared_symbols() if not hasattr(L, s)]
+    assert not missing, missing
+    assert _lib.lib().skp_version() == 1
+
+
+def test_bad_arguments_rejected_without_gpu():
+    from stablekeypoints_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libskp.so not built")
+    L = _lib.lib()
+    rc = L.skp_capture_fwd(None, 8, 16, 500, 128, None, None)
+    assert rc == -1 and b"null" in L.skp_last_error()
+    rc = L.skp_capture_fwd(ctypes.c_void_p(16), 8, 16, 5000, 128, ctypes.c_void_p(16), None)
+    assert rc == -1 and b"1024" in L.skp_last_error()
+    rc = L.skp_fps(ctypes.c_void_p(16), 10, 8, 8, ctypes.c_void_p(16), 1, 4, ctypes.c_void_p(16), None,
+                   ctypes.c_void_p(16), None)
+    assert rc == -1 and b"two candidates" in L.skp_last_error()
+
+
+def test_ops_refuse_cpu_tensors():
+    import torch
+    from stablekeypoints_amd import ops
+    with pytest.raises(ValueError, match="no CPU fallback"):
+        ops.find_max_pixel(torch.zeros(2, 4, 4))

@@ -1,0 +1,294 @@
+"""HIP kernels (through the C ABI) vs the CPU oracle and the reference's golden vectors.
+
+Tolerances (stated per test): index/argmax outputs bit-exact; fp32 maps/losses/grads
+within 1e-4 (north_star) — most are far tighter.
+"""
+import numpy as np
+import pytest
+import torch
+
+import recipes
+from conftest import load_golden
+from oracle import skp_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+def T(a, **kw):
+    return torch.as_tensor(np.ascontiguousarray(a), device=DEV, **kw)
+
+
+def N(t):
+    return t.detach().cpu().numpy()
+
+
+# ----------------------------------------------------------------------------- MFMA GEMM
+@pytest.mark.parametrize("Z,M,Nn,K", [(1, 32, 32, 2), (8, 256, 500, 160), (8, 1024, 500, 80), (3, 37, 53, 19)])
+def test_bgemm_matches_fp64(Z, M, Nn, K):
+    from stablekeypoints_amd import ops
+    g = torch.Generator().manual_seed(M + Nn + K)
+    a = torch.randn(Z, M, K, generator=g)
+    b = torch.randn(Z, K, Nn, generator=g)
+    out = ops.bgemm(a.to(DEV), b.to(DEV), alpha=0.5)
+    ref = 0.5 * (a.double() @ b.double())
+    assert torch.allclose(out.cpu().double(), ref, atol=1e-4, rtol=1e-5)
+    # transposed operand views (strided, as used for q kᵀ and dzᵀ q)
+    out2 = ops.bgemm(a.to(DEV), b.transpose(1, 2).contiguous().to(DEV).transpose(1, 2))
+    assert torch.allclose(out2.cpu().double(), ref * 2, atol=1e-4, rtol=1e-5)
+
+
+def test_bgemm_layout_identity_asymmetric():
+    from stablekeypoints_amd import ops
+    a = torch.eye(40).unsqueeze(0)
+    b = torch.arange(40 * 33, dtype=torch.float32).reshape(1, 40, 33)
+    out = ops.bgemm(a.to(DEV), b.to(DEV))
+    assert torch.equal(out.cpu(), b)
+
+
+# ----------------------------------------------------------------------------- A1 capture
+@pytest.mark.parametrize("H,s,R,Nn", [(8, 4, 32, 16), (8, 8, 32, 16), (2, 16, 128, 500), (2, 32, 128, 500),
+                                      (3, 5, 13, 70), (1, 16, 128, 1)])
+def test_capture_fwd_vs_oracle(H, s, R, Nn):
+    from stablekeypoints_amd import ops
+    z = recipes.random_logits(H * 1000 + s, (H, s * s, Nn), scale=3.0)
+    got = N(ops.capture_attn(T(z), s, R))
+    ref = O.capture_fwd(z, s, R)
+    assert np.abs(got - ref).max() < 1e-6
+    assert np.allclose(got.sum(-1), 1.0, atol=1e-5)
+
+
+@pytest.mark.parametrize("H,s,R,Nn", [(8, 4, 32, 16), (2, 16, 128, 500), (2, 32, 128, 300), (3, 5, 13, 70)])
+def test_capture_bwd_dense_and_broadcast(H, s, R, Nn):
+    from stablekeypoints_amd import ops
+    z = recipes.random_logits(7 + s, (H, s * s, Nn), scale=2.0)
+    g = recipes.random_logits(9 + s, (H, R * R, Nn))
+    got = N(ops.capture_bwd(T(z), s, R, T(g)))
+    ref = O.capture_bwd(z, s, R, g)
+    assert np.abs(got - ref).max() < 1e-4 * max(1.0, np.abs(ref).max())
+    # broadcast gradient: the layer-mean backward of collect_maps (stride-0 over heads, token-major)
+    dmap = recipes.random_logits(11 + s, (Nn, R * R))
+    gb = torch.as_tensor(dmap, device=DEV).t().unsqueeze(0).expand(H, R * R, Nn)
+    got_b = N(ops.capture_bwd(T(z), s, R, gb))
+    ref_b = O.capture_bwd(z, s, R, np.broadcast_to(dmap.T[None], (H, R * R, Nn)).astype(np.float32))
+    assert np.abs(got_b - ref_b).max() < 1e-4 * max(1.0, np.abs(ref_b).max())
+
+
+# ----------------------------------------------------------------------------- A3 aggregate
+def test_aggregate_variants_vs_oracle():
+    from stablekeypoints_amd import ops
+    layers = [recipes.uniform(20 + i, (8, 32 * 32, 50)) for i in range(4)]
+    tl = [T(a) for a in layers]
+    assert np.allclose(N(ops.aggregate(tl)), O.collect_maps(layers), atol=1e-6)
+    assert np.allclose(N(ops.aggregate(tl[:3])), O.collect_maps(layers[:3], layers=(0, 1, 2)), atol=1e-6)
+    idx = np.array([5, 0, 49, 5])
+    got = N(ops.aggregate(tl, indices=torch.as_tensor(idx), upsample_res=80))
+    ref = O.collect_maps(layers, indices=idx, upsample_res=80)
+    assert np.allclose(got, ref, atol=1e-6)
+    # unaligned token count (scalar path)
+    odd = [recipes.uniform(40 + i, (2, 16 * 16, 37)) for i in range(2)]
+    assert np.allclose(N(ops.aggregate([T(a) for a in odd])), O.collect_maps(odd, layers=(0, 1)), atol=1e-6)
+
+
+def test_aggregate_full_shape_properties():
+    """N=500, R=128, 4 layers × 8 heads: every pixel's token distribution sums to 1."""
+    from stablekeypoints_amd import ops
+    zs = [recipes.random_logits(60 + i, (8, s * s, 500), scale=2.0) for i, s in enumerate((16, 16, 16, 32))]
+    attn = [ops.capture_attn(T(z), s, 128) for z, s in zip(zs, (16, 16, 16, 32))]
+    m = N(ops.aggregate(attn))
+    assert m.shape == (500, 128, 128)
+    assert np.allclose(m.sum(0), 1.0, atol=1e-4)
+    ref = O.collect_maps([O.capture_fwd(z, s, 128) for z, s in zip(zs, (16, 16, 16, 32))])
+    assert np.abs(m - ref).max() < 1e-6
+
+
+# ----------------------------------------------------------------------------- A4-A7
+def test_argmax_family_vs_golden():
+    from stablekeypoints_amd import ops
+    g = load_golden("argmax")
+    assert np.array_equal(N(ops.find_max_pixel(T(g["edge"]))), g["edge_max"])
+    assert np.array_equal(N(ops.find_k_max_pixels(T(g["edge"]), 3)), g["edge_k3"], equal_nan=True)
+    assert np.array_equal(N(ops.find_k_max_pixels(T(g["maps32"]), 3)), g["maps32_k3"])
+    pt = ops.find_max_pixel(T(g["maps32"]))
+    assert np.array_equal(N(ops.mask_radius(T(g["maps32"]), pt, 0.05 * 32 * 3)), g["maps32_mask"])
+    wa = T(g["maps32"])
+    pos = ops.pixel_from_weighted_avg(wa, 5)
+    assert np.allclose(N(pos), g["maps32_wavg"], atol=1e-5)
+    assert np.array_equal(N(wa), g["maps32_wavg_mutated"])
+    assert np.allclose(N(ops.pixel_from_weighted_avg(T(g["maps32"]), -1)), g["maps32_wavg_nodist"], atol=1e-4)
+    big = recipes.attention_like_maps(12, 10, 512)
+    assert recipes.sha256(big) == str(g["maps512_sha"])
+    assert np.array_equal(N(ops.find_max_pixel(T(big))), g["maps512_max"])
+    assert np.allclose(N(ops.pixel_from_weighted_avg(T(big))), g["maps512_wavg"], atol=1e-4)
+
+
+def test_argmax_random_ties_nan_bitexact():
+    from stablekeypoints_amd import ops
+    rng = np.random.default_rng(5)
+    m = rng.integers(0, 4, (64, 37, 29)).astype(np.float32)     # heavy ties
+    m[3, 10, 10] = np.nan
+    m[7, 0, 0] = np.nan
+    m[7, 5, 5] = np.nan
+    m[9] = -np.inf
+    assert np.array_equal(N(ops.find_max_pixel(T(m))), O.find_max_pixel(m))
+    assert np.array_equal(N(ops.find_k_max_pixels(T(m), 4)), O.find_k_max_pixels(m, 4), equal_nan=True)
+
+
+def test_gaussian_targets_vs_golden():
+    from stablekeypoints_amd import ops
+    g = load_golden("gaussian")
+    for size, sigma in ((32, 2.0), (128, 2.0), (20, 3.0)):
+        assert np.allclose(N(ops.gaussian_circles(T(g["pos"]), size, sigma)), g[f"circles_{size}_{sigma}"], atol=1e-6)
+
+
+# ----------------------------------------------------------------------------- A8-A10
+def test_selection_vs_golden_full_shape():
+    from stablekeypoints_amd import ops
+    g = load_golden("select")
+    maps = recipes.attention_like_maps(31, 500, 128)
+    maps_t = recipes.attention_like_maps(32, 500, 128)
+    cand = ops.find_top_k_gaussian(T(maps), 25, sigma=2.0)
+    assert np.array_equal(N(cand), g["topk_gauss25"])
+    assert np.array_equal(N(ops.find_top_k_gaussian(T(maps), 25, sigma=2.0, num_subjects=2)), g["topk_gauss25_s2"])
+    assert np.array_equal(N(ops.entropy_sort(T(maps * 100.0), 25)), g["entropy25_sharp"])
+    sel, n = ops.furthest_point_sampling(T(maps_t), 10, cand)
+    assert int(n.item()) == 10 and np.array_equal(N(sel), g["fps10"])
+    sel2, _ = ops.furthest_point_sampling(T(maps), 10, cand)
+    assert np.array_equal(N(sel2), g["fps10_same"])
+
+
+def test_selection_small_and_ties_vs_golden():
+    from stablekeypoints_amd import ops
+    g = load_golden("select")
+    c = ops.find_top_k_gaussian(T(g["maps_small"]), 12, sigma=2.0)
+    assert np.array_equal(N(c), g["small_topk12"])
+    sel, _ = ops.furthest_point_sampling(T(g["maps_small"]), 5, c)
+    assert np.array_equal(N(sel), g["small_fps5"])
+    sel, _ = ops.furthest_point_sampling(T(g["tie_maps"]), 4, torch.tensor([5, 2, 4, 0, 1]))
+    assert np.array_equal(N(sel), g["tie_fps4"])
+
+
+def test_kl_values_vs_oracle():
+    from stablekeypoints_amd import ops
+    maps = recipes.attention_like_maps(34, 64, 64)
+    _, kl = ops.find_top_k_gaussian(T(maps), 10, sigma=2.0, return_kl=True)
+    assert np.allclose(N(kl), O.kl_to_gaussian(maps, 2.0), rtol=1e-5, atol=1e-7)
+
+
+# ----------------------------------------------------------------------------- A11/A12
+def test_losses_vs_golden():
+    from stablekeypoints_amd import ops
+    g = load_golden("losses")
+    for ns in (1, 2):
+        A = T(g["A"]).requires_grad_(True)
+        l = ops.sharpening_loss(A, 2.0, ns)
+        l.backward()
+        assert np.allclose(N(l), g[f"sharp_ns{ns}"], rtol=1e-5)
+        assert np.allclose(N(A.grad), g[f"dA_sharp_ns{ns}"], atol=1e-9, rtol=1e-4)
+    assert np.allclose(N(ops.affine_warp(T(g["img"]), T(g["theta"]))), g["warped"], atol=1e-5)
+    ti = O.theta_inverse(g["theta"])
+    A = T(g["A"]).requires_grad_(True)
+    At = T(g["At"]).requires_grad_(True)
+    l = ops.equivariance_loss_single(A, At, T(ti[1]))
+    l.backward()
+    assert np.allclose(N(l), g["equiv"], rtol=1e-4)
+    assert np.allclose(N(A.grad), g["dA_equiv"], atol=1e-8, rtol=1e-3)
+    assert np.allclose(N(At.grad), g["dAt_equiv"], atol=1e-8, rtol=1e-3)
+
+
+def test_affine_warp_adjoint():
+    """<warp(x), y> == <x, warpᵀ(y)> (linearity/adjoint property at full image size)."""
+    from stablekeypoints_amd import ops
+    x = torch.rand(2, 3, 512, 512, device=DEV, requires_grad=True)
+    th = torch.tensor([[[0.9, 0.1, 0.05], [-0.1, 0.9, -0.2]], [[0.8, -0.2, 0.2], [0.2, 0.8, 0.1]]], device=DEV)
+    y = torch.rand(2, 3, 512, 512, device=DEV)
+    out = ops.affine_warp(x, th)
+    (out * y).sum().backward()
+    lhs = (out.double() * y.double()).sum()
+    rhs = (x.double() * x.grad.double()).sum()
+    assert abs(float(lhs - rhs)) < 1e-6 * abs(float(lhs))
+
+
+# ----------------------------------------------------------------------------- composed paths
+def test_capture_hook_end_to_end_small():
+    """register_attention_control + collect_maps + backward == reference (capture_small golden)."""
+    from stablekeypoints_amd import ptp_utils, optimize
+    from stablekeypoints_amd.sd.unet import CrossAttention
+    g = load_golden("capture_small")
+    R = int(g["R"])
+    shapes = [(4, 64), (4, 64), (4, 64), (8, 32)]
+
+    class Tree(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.up_blocks = torch.nn.ModuleList()
+            for i, (s, c) in enumerate(shapes):
+                m = CrossAttention(c, cross_attention_dim=24, heads=8, dim_head=c // 8)
+                m.load_state_dict({k.split(".", 1)[1]: torch.from_numpy(g[k]) for k in g.files
+                                   if k.startswith(f"w{i}.")})
+                self.up_blocks.append(m)
+    tree = Tree().to(DEV)
+    ctl = ptp_utils.AttentionStore()
+    ptp_utils.register_attention_control(tree, ctl, feature_upsample_res=R)
+    xs = [T(g[f"x{i}"]).requires_grad_(True) for i in range(4)]
+    ctx = T(g["ctx"]).requires_grad_(True)
+    outs = [m(x, context=ctx) for m, x in zip(tree.up_blocks, xs)]
+    for i in range(4):
+        assert np.allclose(N(ctl.step_store["attn"][i]), g[f"attn{i}"], atol=1e-6)
+        assert np.allclose(N(outs[i]), g[f"out{i}"], atol=1e-5)
+    maps = optimize.collect_maps(ctl, upsample_res=-1, layers=[0, 1, 2, 3])
+    assert np.allclose(N(maps), g["map"], atol=1e-6)
+    (maps * T(g["wsel"])).sum().backward()
+    for i in range(4):
+        assert np.allclose(N(xs[i].grad), g[f"dx{i}"], atol=1e-5, rtol=1e-4)
+    assert np.allclose(N(ctx.grad), g["dctx"], atol=1e-5, rtol=1e-4)
+
+
+def test_token_opt_step_tiny_vs_reference():
+    """One optimize.py:362-445 micro-iteration on the tiny SD-1.5-shaped model vs the reference."""
+    from stablekeypoints_amd import optimize, ptp_utils
+    from stablekeypoints_amd.invertable_transform import RandomAffineWithInverse
+    from stablekeypoints_amd.sd import build_sd15, TINY_CONFIG
+    g = load_golden("step_tiny")
+    R = int(g["R"])
+    ldm = build_sd15(seed=0, config=TINY_CONFIG)
+    psum = float(sum(p.double().sum() for p in list(ldm.unet.parameters()) + list(ldm.vae.parameters())))
+    assert abs(psum - float(g["param_sum"])) < 1e-6, "tiny model regeneration differs from the golden's"
+    ldm.to(DEV)
+    noises = [T(g["noise0"]), T(g["noise1"])]
+    inner = ldm.scheduler
+
+    class Sched:
+        timesteps = inner.timesteps
+
+        def add_noise(self, x, noise, t):
+            return inner.add_noise(x, noises.pop(0), t)
+    ldm.scheduler = Sched()
+    ctl = ptp_utils.AttentionStore(early_exit=True)
+    ptp_utils.register_attention_control(ldm.unet, ctl, feature_upsample_res=R)
+    controllers = {torch.device(DEV): ctl}
+    ctx = T(g["ctx"]).requires_grad_(True)
+    kw = dict(layers=[0, 1, 2, 3], upsample_res=-1, device=DEV, controllers=controllers)
+    maps = ptp_utils.run_and_find_attn(ldm, T(g["img"]), ctx, **kw)
+    Tr = RandomAffineWithInverse(degrees=15, scale=(0.8, 1.0), translate=(0.25, 0.25))
+    timg = Tr(T(g["img"]), theta=torch.from_numpy(g["theta"]))
+    assert np.allclose(N(timg), g["timg"], atol=1e-5)
+    maps_t = ptp_utils.run_and_find_attn(ldm, timg, ctx, **kw)
+    assert np.allclose(N(maps[0]), g["map"], atol=1e-5)
+    assert np.allclose(N(maps_t[0]), g["map_t"], atol=1e-5)
+    cand = ptp_utils.find_top_k_gaussian(maps[0], 8, sigma=2.0)
+    idx = ptp_utils.furthest_point_sampling(maps_t[0], 4, cand)
+    assert np.array_equal(N(cand), g["cand"]) and np.array_equal(N(idx), g["idx"])
+    sharp = optimize.sharpening_loss(maps[0][idx], sigma=2.0)
+    eq = optimize.equivariance_loss(maps[0][idx], maps_t[0][idx][None], Tr, 0)
+    loss = (eq * 1000.0 + sharp * 100.0) / 4
+    loss.backward()
+    assert np.allclose(N(sharp), g["sharp"], rtol=1e-4) and np.allclose(N(eq), g["eq"], rtol=1e-3)
+    assert np.allclose(N(ctx.grad), g["dctx"], rtol=1e-3, atol=1e-7)
