@@ -1,0 +1,318 @@
+"""Benchmark: StableKeypoints token-optimisation throughput on MI355X (images/sec).
+
+Workload (BASELINE.json configs[1]: "CelebA-wild 512² N=500 tokens, 1×MI355X"): SD-1.5
+UNet/VAE with seeded random weights (no checkpoint offline), synthetic 512×512 images
+(seeded torch.rand), N=500 tokens × 768, feature_upsample_res=128, the reference's
+default hyper-parameters (gaussian top-k 25 → furthest-point 10, σ=2, weights 100/1000,
+Adam lr 5e-3, batch_size 4 per GPU).
+
+One "step" = one optimiser step = ``--accum`` (default 4) micro-iterations per rank
+(reference optimize.py:362-448), each = 2 captures (image + random affine warp) +
+selection + losses + backward through the UNet into the token embedding, then the
+gradient all-reduce (RCCL) and Adam.  Weak scaling: every rank processes ``accum``
+images per step.  ``value`` = images processed by all ranks ÷ the max-over-ranks time.
+
+Launch: ``python bench.py`` (1 GPU) or ``python -m torch.distributed.run --nproc-per-node N
+--master-addr 127.0.0.1 bench.py --gpus N``.  Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK = 8.0e12          # MI355X_MICROARCH.md: 8.0 TB/s spec
+HBM_MEASURED_COPY = 6.29e12
+
+
+class KernelTimer:
+    """HIP events around each launch of the named kernels, on the launching (current) stream."""
+
+    def __init__(self, names):
+        self.names = set(names)
+        self.events = {n: [] for n in names}
+        self.nbytes = {n: [] for n in names}
+        self.enabled = False
+
+    def record(self, name, nbytes):
+        timer = self
+
+        class _Ctx:
+            def __enter__(self_):
+                if timer.enabled and name in timer.names:
+                    self_.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    self_.ev[0].record()
+                else:
+                    self_.ev = None
+                return self_
+
+            def __exit__(self_, *a):
+                if self_.ev is not None:
+                    self_.ev[1].record()
+                    timer.events[name].append(self_.ev)
+                    timer.nbytes[name].append(nbytes)
+                return False
+        return _Ctx()
+
+    def summary(self, name):
+        ev = self.events[name]
+        if not ev:
+            return None
+        ms = [a.elapsed_time(b) for a, b in ev]
+        return {"launches": len(ms), "avg_ms": float(np.mean(ms)), "bytes_per_launch": float(np.mean(self.nbytes[name]))}
+
+
+# ------------------------------------------------------------------------------ CPU baseline (port)
+def cpu_baseline(args):
+    """One micro-iteration of the same workload on the host CPU: torch-CPU UNet/VAE
+    (same architecture and seed) + the numpy oracle for every hot-path row (capture,
+    aggregate, selection, losses and their backward).  kind = "port"."""
+    from oracle import skp_oracle as O
+    from stablekeypoints_amd.sd import build_sd15
+    from stablekeypoints_amd.sd.unet import CaptureComplete, attention_core
+    from stablekeypoints_amd.datasets import SyntheticDataset
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    ldm = build_sd15(seed=0, device="cpu")
+    R = args.res // 4
+
+    class OCapture(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, z, s):
+            zn = z.detach().numpy()
+            a = O.capture_fwd(zn, s, R)
+            ctx.zn, ctx.s = zn, s
+            return torch.from_numpy(a)
+
+        @staticmethod
+        def backward(ctx, g):
+            return torch.from_numpy(O.capture_bwd(ctx.zn, ctx.s, R, g.numpy())), None
+
+    class OAggregate(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, *layers):
+            ctx.shapes = [t.shape for t in layers]
+            return torch.from_numpy(O.collect_maps([t.numpy() for t in layers]))
+
+        @staticmethod
+        def backward(ctx, g):
+            return tuple(torch.from_numpy(np.ascontiguousarray(x))
+                         for x in O.collect_maps_bwd(ctx.shapes, g.numpy()))
+
+    class OSharp(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, A, sigma):
+            l, dA = O.sharpening_loss(A.detach().numpy(), sigma)
+            ctx.dA = torch.from_numpy(dA)
+            return torch.tensor(l)
+
+        @staticmethod
+        def backward(ctx, g):
+            return ctx.dA * g, None
+
+    class OEquiv(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, A, At, theta):
+            l, dA, dAt = O.equivariance_loss(A.detach().numpy(), At.detach().numpy(), theta, 0)
+            ctx.g = (torch.from_numpy(dA), torch.from_numpy(dAt))
+            return torch.tensor(l)
+
+        @staticmethod
+        def backward(ctx, g):
+            return ctx.g[0] * g, ctx.g[1] * g, None
+
+    store = []
+
+    def patch(mod):
+        def fwd(x, context=None, mask=None):
+            B, S, C = x.shape
+            q = mod.reshape_heads_to_batch_dim(mod.to_q(x))
+            ctxt = x if context is None else context
+            k = mod.reshape_heads_to_batch_dim(mod.to_k(ctxt))
+            v = mod.reshape_heads_to_batch_dim(mod.to_v(ctxt))
+            if context is not None and S <= 1024 and len(store) < 4:
+                sim = torch.bmm(q, k.transpose(1, 2)) * mod.scale
+                out = torch.bmm(sim.softmax(-1), v)
+                store.append(OCapture.apply(sim, int(S ** 0.5)))
+            else:
+                out = attention_core(q, k, v, mod.scale)
+            out = mod.to_out[0](mod.reshape_batch_dim_to_heads(out))
+            if len(store) >= 4:
+                raise CaptureComplete()
+            return out
+        return fwd
+    for name, child in ldm.unet.named_children():
+        if "up" in name:
+            for m in child.modules():
+                if m.__class__.__name__ == "CrossAttention":
+                    m.forward = patch(m)
+
+    torch.manual_seed(0)
+    context = torch.randn(1, args.tokens, 768).requires_grad_(True)
+    img = SyntheticDataset(n=1, size=args.res, seed=0)[0]["img"][None]
+
+    def capture(image):
+        with torch.no_grad():
+            lat = ldm.vae.encode(image * 2 - 1)["latent_dist"].mean * 0.18215
+        t = ldm.scheduler.timesteps[-1]
+        noisy = ldm.scheduler.add_noise(lat, torch.randn_like(lat), t)
+        store.clear()
+        try:
+            ldm.unet(noisy, t.repeat(1), context)
+        except CaptureComplete:
+            pass
+        return OAggregate.apply(*store)
+
+    t0 = time.time()
+    m = capture(img)
+    u = torch.rand(1, 4).numpy()
+    theta = O.affine_params(u, 15.0, (0.8, 1.0), (0.25, 0.25))
+    timg = torch.from_numpy(O.affine_warp(img.numpy(), theta))
+    mt = capture(timg)
+    cand = O.find_top_k_gaussian(m.detach().numpy(), 25, sigma=2.0)
+    idx = torch.from_numpy(O.furthest_point_sampling(mt.detach().numpy(), 10, cand))
+    sh = OSharp.apply(m[idx], 2.0)
+    eq = OEquiv.apply(m[idx], mt[idx], theta)
+    loss = (eq * 1000.0 + sh * 100.0) / args.accum
+    loss.backward()
+    assert context.grad is not None and torch.isfinite(context.grad).all()
+    dt = time.time() - t0
+    cpu = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": 1.0 / dt, "unit": "images/sec", "cores": threads, "kind": "port",
+            "sample": f"1 image = 1 token-opt micro-iteration (2 captures + select + losses + backward), "
+                      f"N={args.tokens}, {args.res}²; torch-CPU SD-1.5 UNet/VAE + numpy oracle; {dt:.1f} s on {cpu}"}
+
+
+# ------------------------------------------------------------------------------ GPU bench
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--accum", type=int, default=4, help="images per rank per optimiser step (batch_size/num_gpus)")
+    ap.add_argument("--tokens", type=int, default=500)
+    ap.add_argument("--res", type=int, default=512)
+    ap.add_argument("--upsample-res", type=int, default=128)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
+                    help="JSON with PMC-derived HBM bytes per launch of the roofline kernel")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from stablekeypoints_amd import ops
+    from stablekeypoints_amd.optimize import TokenOptimizer
+    from stablekeypoints_amd.optimize_token import load_ldm
+    from stablekeypoints_amd.datasets import SyntheticDataset
+
+    ldm, controllers, num_gpus = load_ldm(dev, "runwayml/stable-diffusion-v1-5", feature_upsample_res=args.upsample_res)
+    torch.manual_seed(0)
+    context = torch.randn(1, args.tokens, 768).to(dev)
+    torch.manual_seed(1234 + rank)
+    opt = TokenOptimizer(ldm, controllers, context, accum=args.accum, device=dev)
+    data = SyntheticDataset(n=16, size=args.res, seed=rank)
+    imgs = [data[i]["img"][None].to(dev) for i in range(len(data))]
+    timer = KernelTimer(["skp_aggregate", "skp_capture_fwd", "skp_capture_bwd"])
+    ops.set_kernel_timer(timer)
+
+    counter = [0]
+
+    def step():
+        for _ in range(args.accum):
+            opt.micro_step(imgs[counter[0] % len(imgs)])
+            counter[0] += 1
+        return opt.optimizer_step()
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    torch.cuda.synchronize()
+    timer.enabled = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        rec = step()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    timer.enabled = False
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    images = world * args.accum * args.steps
+    value = images / elapsed
+
+    agg = timer.summary("skp_aggregate")
+    roof = None
+    if agg:
+        achieved = agg["bytes_per_launch"] / (agg["avg_ms"] * 1e-3)
+        traffic = None
+        if os.path.exists(args.traffic):
+            try:
+                traffic = json.load(open(args.traffic)).get("skp_aggregate", {}).get("hbm_bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
+        roof = {"kernel": "skp_aggregate", "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
+                "unit": "GB/s", "frac": achieved / HBM_PEAK, "traffic": traffic,
+                "avg_launch_ms": agg["avg_ms"], "launches": agg["launches"],
+                "algorithmic_bytes_per_launch": agg["bytes_per_launch"],
+                "frac_of_measured_copy": achieved / HBM_MEASURED_COPY}
+    extra = {}
+    for k in ("skp_capture_fwd", "skp_capture_bwd"):
+        s = timer.summary(k)
+        if s:
+            extra[k] = {"avg_ms": s["avg_ms"], "launches": s["launches"],
+                        "GB/s_algorithmic": s["bytes_per_launch"] / (s["avg_ms"] * 1e-3) / 1e9}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        ops.set_kernel_timer(None)
+        cpu = cpu_baseline(args)
+
+    if rank == 0:
+        out = {"metric": "images/sec (token-opt step, 512², N=500 tokens)", "value": value, "unit": "images/sec",
+               "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+               "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded torch.rand 512² images, random-init SD-1.5)",
+               "config": {"workload": "CelebA-wild-shaped 512², N=500 tokens, SD-1.5 fp32, feature_upsample_res=128, "
+                                      "batch_size 4 per GPU (BASELINE.json configs[1])",
+                          "global_batch": world * args.accum, "tokens": args.tokens, "image_res": args.res,
+                          "feature_upsample_res": args.upsample_res, "parallelism": f"dp{world} (RCCL grad all-reduce)"},
+               "roofline": roof, "cpu_baseline": cpu, "kernels": extra,
+               "last_loss": float(rec["loss"])}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

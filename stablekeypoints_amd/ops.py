@@ -12,6 +12,27 @@ from ._lib import call, ptr, stream
 
 F32 = torch.float32
 
+# Optional per-kernel timer (bench.py): an object with record(name, nbytes) returning a
+# context manager that brackets one launch with HIP events on the current stream.
+_TIMER = None
+
+
+def set_kernel_timer(timer):
+    global _TIMER
+    _TIMER = timer
+
+
+class _NoTimer:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def _timed(name, nbytes=0):
+    return _TIMER.record(name, nbytes) if _TIMER is not None else _NoTimer()
+
 
 def _c(t, dtype=F32):
     return t.contiguous() if t.dtype == dtype else t.to(dtype).contiguous()
@@ -68,7 +89,8 @@ class CaptureAttn(torch.autograd.Function):
         BH, S, N = z.shape
         assert S == s * s
         attn = torch.empty(BH, R * R, N, device=z.device, dtype=F32)
-        call("skp_capture_fwd", ptr(z), BH, s, N, R, ptr(attn), stream(z.device))
+        with _timed("skp_capture_fwd", (BH * R * R * N + BH * S * N) * 4):
+            call("skp_capture_fwd", ptr(z), BH, s, N, R, ptr(attn), stream(z.device))
         ctx.save_for_backward(z)
         ctx.s, ctx.R = s, R
         return attn
@@ -88,8 +110,9 @@ def capture_bwd(z, s, R, dattn, gscale=1.0):
         sb = 0
     ws = torch.empty(BH, R, s, N, device=z.device, dtype=F32)
     dz = torch.empty_like(z)
-    call("skp_capture_bwd", ptr(z), BH, s, N, R, ptr(dattn), sb, sp, sn, float(gscale), ptr(dz), ptr(ws),
-         stream(z.device))
+    with _timed("skp_capture_bwd", (BH * S * N * 2 + BH * R * s * N * 2) * 4):
+        call("skp_capture_bwd", ptr(z), BH, s, N, R, ptr(dattn), sb, sp, sn, float(gscale), ptr(dz), ptr(ws),
+             stream(z.device))
     return dz
 
 
@@ -112,8 +135,9 @@ class _Aggregate(torch.autograd.Function):
         n_out = N if indices is None else int(indices.numel())
         out = torch.empty(n_out, R, R, device=layers[0].device, dtype=F32)
         idx = None if indices is None else indices.to(device=out.device, dtype=torch.int64).contiguous()
-        call("skp_aggregate", ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)), len(layers), BH, RR, N, ptr(idx),
-             n_out, ptr(out), stream(out.device))
+        with _timed("skp_aggregate", (len(layers) * BH * RR * N + n_out * RR) * 4):
+            call("skp_aggregate", ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)), len(layers), BH, RR, N,
+                 ptr(idx), n_out, ptr(out), stream(out.device))
         ctx.meta = (BH, RR, N, R, len(layers))
         ctx.idx = idx
         ctx.upsample_res = upsample_res

@@ -76,101 +76,125 @@ def _world():
     return 1, 0
 
 
+class TokenOptimizer:
+    """One rank's share of the token optimisation (optimize.py:337-471 loop body).
+
+    ``micro_step(image)`` runs one reference micro-iteration on one image: capture
+    on the image and on its random affine warp, top-k selection, furthest-point
+    sampling, sharpening + equivariance losses, backward into ``context``.
+    ``optimizer_step()`` all-reduces the gradient over ranks (SUM ÷ world) and
+    applies Adam, as the reference does every ``batch_size // num_gpus`` micro-steps.
+    """
+
+    def __init__(self, ldm, controllers, context, lr=5e-3, top_k_strategy="gaussian", top_k=10,
+                 furthest_point_num_samples=25, sigma=2.0, num_subjects=1, sharpening_loss_weight=100,
+                 equivariance_attn_loss_weight=1000.0, accum=4, noise_level=-1, layers=(0, 1, 2, 3),
+                 from_where=("down_cross", "mid_cross", "up_cross"), augment_degrees=15, augment_scale=(0.8, 1.0),
+                 augment_translate=(0.25, 0.25), device="cuda"):
+        self.ldm, self.controllers, self.device = ldm, controllers, device
+        self.context = context
+        self.context.requires_grad = True
+        self.optimizer = torch.optim.Adam([self.context], lr=lr)
+        self.top_k_strategy, self.top_k, self.fps_n = top_k_strategy, top_k, furthest_point_num_samples
+        self.sigma, self.num_subjects = sigma, num_subjects
+        self.w_sharp, self.w_eq = sharpening_loss_weight, equivariance_attn_loss_weight
+        self.accum = accum
+        self.kw = dict(layers=layers, noise_level=noise_level, from_where=from_where, upsample_res=-1, device=device,
+                       controllers=controllers)
+        self.transform = RandomAffineWithInverse(degrees=augment_degrees, scale=augment_scale,
+                                                 translate=augment_translate)
+        self.world, self.rank = _world()
+        self.reset_running()
+
+    def reset_running(self):
+        self.run_eq = self.run_sh = self.run_tot = 0.0
+
+    def micro_step(self, image):
+        attn_map = ptp_utils.run_and_find_attn(self.ldm, image, self.context, **self.kw)[0]
+        transformed_img = self.transform(image)
+        attention_map_transformed = ptp_utils.run_and_find_attn(self.ldm, transformed_img, self.context, **self.kw)[0]
+        if self.top_k_strategy == "entropy":
+            cand = ptp_utils.entropy_sort(attn_map, self.fps_n)
+        elif self.top_k_strategy == "gaussian":
+            cand = ptp_utils.find_top_k_gaussian(attn_map, self.fps_n, sigma=self.sigma, num_subjects=self.num_subjects)
+        elif self.top_k_strategy == "consistent":
+            cand = torch.arange(self.fps_n, device=attn_map.device)
+        else:
+            raise NotImplementedError
+        idx = ptp_utils.furthest_point_sampling(attention_map_transformed, self.top_k, cand)
+        sh = sharpening_loss(attn_map[idx], device=self.device, sigma=self.sigma, num_subjects=self.num_subjects)
+        eq = equivariance_loss(attn_map[idx], attention_map_transformed[idx][None], self.transform, 0)
+        loss = eq * self.w_eq + sh * self.w_sharp
+        self.run_eq = self.run_eq + eq.detach() / self.accum * self.w_eq
+        self.run_sh = self.run_sh + sh.detach() / self.accum * self.w_sharp
+        self.run_tot = self.run_tot + loss.detach() / self.accum
+        (loss / self.accum).backward()
+        return idx
+
+    def optimizer_step(self):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(self.context.grad, op=dist.ReduceOp.SUM)
+            self.context.grad.div_(self.world)
+            stats = torch.stack([torch.as_tensor(x, device=self.context.device, dtype=torch.float32).reshape(())
+                                 for x in (self.run_tot, self.run_eq, self.run_sh)])
+            dist.all_reduce(stats, op=dist.ReduceOp.SUM)
+            self.run_tot, self.run_eq, self.run_sh = (stats / self.world).unbind(0)
+        self.optimizer.step()
+        self.optimizer.zero_grad()
+        rec = {"loss": self.run_tot, "running_equivariance_attn_loss": self.run_eq,
+               "running_sharpening_loss": self.run_sh}
+        self.reset_running()
+        return rec
+
+
 def optimize_embedding(ldm, top_k_strategy="entropy", wandb_log=True, context=None, device="cuda", num_steps=2000,
                        from_where=("down_cross", "mid_cross", "up_cross"), upsample_res=256, layers=(0, 1, 2, 3, 4, 5),
                        lr=5e-3, noise_level=-1, num_tokens=1000, top_k=10, augment_degrees=30,
                        augment_scale=(0.9, 1.1), augment_translate=(0.1, 0.1), dataset_loc="~", sigma=1.0,
                        sharpening_loss_weight=100, equivariance_attn_loss_weight=100, batch_size=4, num_gpus=1,
                        dataset_name="celeba_aligned", max_len=-1, min_dist=0.05, furthest_point_num_samples=50,
-                       controllers=None, validation=False, num_subjects=1, dataset=None, log=None, seed=None,
-                       step_callback=None):
-    """optimize.py:269-475.  Extra keyword-only conveniences: ``dataset`` (an object
-    yielding {"img": (3,H,W)}; overrides dataset_name), ``log`` (callable receiving
-    the per-step metrics dict instead of wandb/print), ``seed`` (per-rank sampler
-    seed), ``step_callback(iteration)`` (called after every micro-iteration)."""
+                       controllers=None, validation=False, num_subjects=1, dataset=None, log=None, seed=None):
+    """optimize.py:269-475.  Extra keyword conveniences: ``dataset`` (object yielding
+    {"img": (3,H,W)}; overrides dataset_name), ``log`` (callable receiving each
+    optimiser step's metrics instead of print), ``seed`` (sampler seed; rank added)."""
     world, rank = _world()
-    if num_gpus != world:
-        num_gpus = world   # one process per GPU: the replica count is the world size
+    num_gpus = world   # one process per GPU: the replica count is the world size
     if dataset is None:
         dataset = _make_dataset(dataset_name, dataset_loc, max_len, validation)
-    invertible_transform = RandomAffineWithInverse(degrees=augment_degrees, scale=augment_scale,
-                                                   translate=augment_translate)
     if context is None:
         context = ptp_utils.init_random_noise(device, num_words=num_tokens)
-    context.requires_grad = True
-    optimizer = torch.optim.Adam([context], lr=lr)
-
     accum = batch_size // num_gpus
-    n_iter = int(num_steps * accum)
-    gen = torch.Generator().manual_seed(seed if seed is not None else torch.initial_seed() % (2 ** 31))
-    sampler_gen = torch.Generator().manual_seed(int(torch.randint(0, 2 ** 31 - 1, (1,), generator=gen)) + rank)
+    opt = TokenOptimizer(ldm, controllers, context, lr=lr, top_k_strategy=top_k_strategy, top_k=top_k,
+                         furthest_point_num_samples=furthest_point_num_samples, sigma=sigma,
+                         num_subjects=num_subjects, sharpening_loss_weight=sharpening_loss_weight,
+                         equivariance_attn_loss_weight=equivariance_attn_loss_weight, accum=max(accum, 1),
+                         noise_level=noise_level, layers=layers, from_where=from_where,
+                         augment_degrees=augment_degrees, augment_scale=augment_scale,
+                         augment_translate=augment_translate, device=device)
+    n_iter = int(num_steps * accum)   # batch_size < num_gpus gives 0 iterations, as in the reference
+    base = seed if seed is not None else int(torch.randint(0, 2 ** 31 - 1, (1,)))
+    sampler_gen = torch.Generator().manual_seed(base + rank)
     order = torch.randperm(len(dataset), generator=sampler_gen)
     pos = 0
-
-    start = time.time()
-    it_start = time.time()
-    run_eq = run_sh = run_tot = 0.0
+    start = it_start = time.time()
     for iteration in range(n_iter):
         if pos >= len(order):
             order = torch.randperm(len(dataset), generator=sampler_gen)
             pos = 0
         image = dataset[int(order[pos])]["img"][None].to(device, non_blocking=True)
         pos += 1
-
-        kw = dict(layers=layers, noise_level=noise_level, from_where=from_where, upsample_res=-1, device=device,
-                  controllers=controllers)
-        attn_maps = ptp_utils.run_and_find_attn(ldm, image, context, **kw)
-        transformed_img = invertible_transform(image)
-        attention_maps_transformed = ptp_utils.run_and_find_attn(ldm, transformed_img, context, **kw)
-
-        attn_map, attention_map_transformed = attn_maps[0], attention_maps_transformed[0]
-        if top_k_strategy == "entropy":
-            top_embedding_indices = ptp_utils.entropy_sort(attn_map, furthest_point_num_samples)
-        elif top_k_strategy == "gaussian":
-            top_embedding_indices = ptp_utils.find_top_k_gaussian(attn_map, furthest_point_num_samples, sigma=sigma,
-                                                                  num_subjects=num_subjects)
-        elif top_k_strategy == "consistent":
-            top_embedding_indices = torch.arange(furthest_point_num_samples, device=attn_map.device)
-        else:
-            raise NotImplementedError
-        top_embedding_indices = ptp_utils.furthest_point_sampling(attention_map_transformed, top_k,
-                                                                  top_embedding_indices)
-        _sharpening_loss = sharpening_loss(attn_map[top_embedding_indices], device=device, sigma=sigma,
-                                           num_subjects=num_subjects)
-        _loss_equivariance_attn = equivariance_loss(attn_map[top_embedding_indices],
-                                                    attention_map_transformed[top_embedding_indices][None],
-                                                    invertible_transform, 0)
-
-        loss = _loss_equivariance_attn * equivariance_attn_loss_weight + _sharpening_loss * sharpening_loss_weight
-        run_eq = run_eq + _loss_equivariance_attn.detach() / accum * equivariance_attn_loss_weight
-        run_sh = run_sh + _sharpening_loss.detach() / accum * sharpening_loss_weight
-        run_tot = run_tot + loss.detach() / accum
-        loss = loss / accum
-        loss.backward()
-        if step_callback is not None:
-            step_callback(iteration)
-
+        opt.micro_step(image)
         if (iteration + 1) % accum == 0:
-            if world > 1:
-                import torch.distributed as dist
-                dist.all_reduce(context.grad, op=dist.ReduceOp.SUM)
-                context.grad.div_(world)
-                stats = torch.stack([run_tot, run_eq, run_sh])
-                dist.all_reduce(stats, op=dist.ReduceOp.SUM)
-                run_tot, run_eq, run_sh = (stats / world).unbind(0)
-            optimizer.step()
-            optimizer.zero_grad()
-            rec = {"loss": float(run_tot), "running_equivariance_attn_loss": float(run_eq),
-                   "running_sharpening_loss": float(run_sh), "iteration time": time.time() - it_start}
+            rec = {k: float(v) for k, v in opt.optimizer_step().items()}
+            rec["iteration time"] = time.time() - it_start
             if log is not None:
                 log(rec)
-            elif rank == 0 and wandb_log:
-                print(json.dumps(rec), flush=True)
             elif rank == 0:
-                print(f"loss: {rec['loss']}, _loss_equivariance_attn: {rec['running_equivariance_attn_loss']} "
+                print(json.dumps(rec) if wandb_log else
+                      f"loss: {rec['loss']}, _loss_equivariance_attn: {rec['running_equivariance_attn_loss']} "
                       f"sharpening_loss: {rec['running_sharpening_loss']}, iteration time: {rec['iteration time']}",
                       flush=True)
-            run_eq = run_sh = run_tot = 0.0
             it_start = time.time()
     if rank == 0 and log is None:
         print(f"optimization took {time.time() - start} seconds", flush=True)

@@ -255,6 +255,14 @@ def gen_step_tiny():
     parts = build_sd15(seed=0, config=TINY_CONFIG)
     psum = float(sum(p.double().sum() for p in list(parts.unet.parameters()) + list(parts.vae.parameters())))
     parts.scheduler = _RecordingScheduler(parts.scheduler)
+    latents = []
+    enc = parts.vae.encode
+
+    def recording_encode(x, *a, **k):   # record image2latent's VAE output (ptp_utils.py:300-303)
+        out = enc(x, *a, **k)
+        latents.append(out["latent_dist"].mean.detach().clone() * 0.18215)
+        return out
+    parts.vae.encode = recording_encode
     R, N = 32, 16
     controllers = {torch.device("cpu"): pu.AttentionStore()}
 
@@ -281,7 +289,8 @@ def gen_step_tiny():
     loss.backward()
     out = {"R": R, "N": N, "param_sum": psum, "img": _np(img), "ctx": _np(ctx), "timg": _np(timg),
            "theta": _np(T.last_params["theta"]), "noise0": _np(parts.scheduler.noises[0]),
-           "noise1": _np(parts.scheduler.noises[1]), "map": _np(maps[0]), "map_t": _np(maps_t[0]),
+           "noise1": _np(parts.scheduler.noises[1]), "latent0": _np(latents[0]), "latent1": _np(latents[1]),
+           "map": _np(maps[0]), "map_t": _np(maps_t[0]),
            "cand": _np(cand), "idx": _np(idx), "sharp": _np(sharp), "eq": _np(eq), "loss": _np(loss),
            "dctx": _np(ctx.grad)}
     np.savez_compressed(os.path.join(HERE, "step_tiny.npz"), **out)
