@@ -22,8 +22,12 @@ class StableDiffusionParts:
         return self
 
 
-TINY_CONFIG = dict(unet=dict(block_out_channels=(32, 64, 64, 64), cross_attention_dim=32),
-                   vae=dict(block_out_channels=(32, 32, 64, 64)))
+# Toy widths with SD-1.5's block structure, for golden vectors and CPU tests.  8 GroupNorm
+# groups and 128² inputs keep it well conditioned (at 64² with 32 groups the 1×1 bottleneck
+# normalises 2 values per group and a 1e-6 input change moves the maps by 1e-3).
+TINY_CONFIG = dict(unet=dict(block_out_channels=(32, 64, 64, 64), cross_attention_dim=32, norm_num_groups=8),
+                   vae=dict(block_out_channels=(32, 32, 64, 64), norm_num_groups=8))
+TINY_IMAGE = 128
 
 
 def build_sd15(seed=0, device="cpu", weights=None, config=None):

@@ -196,10 +196,11 @@ class Upsample2D(nn.Module):
 
 # --------------------------------------------------------------------------- blocks
 class CrossAttnDownBlock2D(nn.Module):
-    def __init__(self, in_ch, out_ch, temb, heads, ctx_dim, add_downsample):
+    def __init__(self, in_ch, out_ch, temb, heads, ctx_dim, add_downsample, groups=32):
         super().__init__()
-        self.resnets = nn.ModuleList([ResnetBlock2D(in_ch if i == 0 else out_ch, out_ch, temb) for i in range(2)])
-        self.attentions = nn.ModuleList([Transformer2DModel(heads, out_ch // heads, out_ch, ctx_dim) for _ in range(2)])
+        self.resnets = nn.ModuleList([ResnetBlock2D(in_ch if i == 0 else out_ch, out_ch, temb, groups) for i in range(2)])
+        self.attentions = nn.ModuleList([Transformer2DModel(heads, out_ch // heads, out_ch, ctx_dim, groups)
+                                         for _ in range(2)])
         self.downsamplers = nn.ModuleList([Downsample2D(out_ch)]) if add_downsample else None
 
     def forward(self, h, temb, context):
@@ -214,9 +215,9 @@ class CrossAttnDownBlock2D(nn.Module):
 
 
 class DownBlock2D(nn.Module):
-    def __init__(self, in_ch, out_ch, temb, add_downsample):
+    def __init__(self, in_ch, out_ch, temb, add_downsample, groups=32):
         super().__init__()
-        self.resnets = nn.ModuleList([ResnetBlock2D(in_ch if i == 0 else out_ch, out_ch, temb) for i in range(2)])
+        self.resnets = nn.ModuleList([ResnetBlock2D(in_ch if i == 0 else out_ch, out_ch, temb, groups) for i in range(2)])
         self.downsamplers = nn.ModuleList([Downsample2D(out_ch)]) if add_downsample else None
 
     def forward(self, h, temb, context=None):
@@ -231,20 +232,21 @@ class DownBlock2D(nn.Module):
 
 
 class _UpBase(nn.Module):
-    def _make_resnets(self, in_ch, out_ch, prev_ch, temb):
+    def _make_resnets(self, in_ch, out_ch, prev_ch, temb, groups=32):
         res = []
         for i in range(3):
             skip = in_ch if i == 2 else out_ch
             rin = prev_ch if i == 0 else out_ch
-            res.append(ResnetBlock2D(rin + skip, out_ch, temb))
+            res.append(ResnetBlock2D(rin + skip, out_ch, temb, groups))
         return nn.ModuleList(res)
 
 
 class CrossAttnUpBlock2D(_UpBase):
-    def __init__(self, in_ch, out_ch, prev_ch, temb, heads, ctx_dim, add_upsample):
+    def __init__(self, in_ch, out_ch, prev_ch, temb, heads, ctx_dim, add_upsample, groups=32):
         super().__init__()
-        self.resnets = self._make_resnets(in_ch, out_ch, prev_ch, temb)
-        self.attentions = nn.ModuleList([Transformer2DModel(heads, out_ch // heads, out_ch, ctx_dim) for _ in range(3)])
+        self.resnets = self._make_resnets(in_ch, out_ch, prev_ch, temb, groups)
+        self.attentions = nn.ModuleList([Transformer2DModel(heads, out_ch // heads, out_ch, ctx_dim, groups)
+                                         for _ in range(3)])
         self.upsamplers = nn.ModuleList([Upsample2D(out_ch)]) if add_upsample else None
 
     def forward(self, h, res_tuple, temb, context, upsample_size=None):
@@ -259,9 +261,9 @@ class CrossAttnUpBlock2D(_UpBase):
 
 
 class UpBlock2D(_UpBase):
-    def __init__(self, in_ch, out_ch, prev_ch, temb, add_upsample):
+    def __init__(self, in_ch, out_ch, prev_ch, temb, add_upsample, groups=32):
         super().__init__()
-        self.resnets = self._make_resnets(in_ch, out_ch, prev_ch, temb)
+        self.resnets = self._make_resnets(in_ch, out_ch, prev_ch, temb, groups)
         self.upsamplers = nn.ModuleList([Upsample2D(out_ch)]) if add_upsample else None
 
     def forward(self, h, res_tuple, temb, context=None, upsample_size=None):
@@ -275,10 +277,10 @@ class UpBlock2D(_UpBase):
 
 
 class UNetMidBlock2DCrossAttn(nn.Module):
-    def __init__(self, ch, temb, heads, ctx_dim):
+    def __init__(self, ch, temb, heads, ctx_dim, groups=32):
         super().__init__()
-        self.resnets = nn.ModuleList([ResnetBlock2D(ch, ch, temb) for _ in range(2)])
-        self.attentions = nn.ModuleList([Transformer2DModel(heads, ch // heads, ch, ctx_dim)])
+        self.resnets = nn.ModuleList([ResnetBlock2D(ch, ch, temb, groups) for _ in range(2)])
+        self.attentions = nn.ModuleList([Transformer2DModel(heads, ch // heads, ch, ctx_dim, groups)])
 
     def forward(self, h, temb, context):
         h = self.resnets[0](h, temb)
@@ -311,7 +313,7 @@ class UNet2DConditionModel(nn.Module):
     """SD-1.5 UNet: blocks (320, 640, 1280, 1280), 8 heads, cross-attention dim 768."""
 
     def __init__(self, in_channels=4, out_channels=4, block_out_channels=(320, 640, 1280, 1280),
-                 cross_attention_dim=768, attention_head_dim=8):
+                 cross_attention_dim=768, attention_head_dim=8, norm_num_groups=32):
         super().__init__()
         ch0 = block_out_channels[0]
         temb = ch0 * 4
@@ -324,10 +326,12 @@ class UNet2DConditionModel(nn.Module):
             in_ch, out_ch = out_ch, block_out_channels[i]
             last = i == 3
             if i < 3:
-                self.down_blocks.append(CrossAttnDownBlock2D(in_ch, out_ch, temb, heads, cross_attention_dim, not last))
+                self.down_blocks.append(CrossAttnDownBlock2D(in_ch, out_ch, temb, heads, cross_attention_dim, not last,
+                                                             norm_num_groups))
             else:
-                self.down_blocks.append(DownBlock2D(in_ch, out_ch, temb, not last))
-        self.mid_block = UNetMidBlock2DCrossAttn(block_out_channels[-1], temb, heads, cross_attention_dim)
+                self.down_blocks.append(DownBlock2D(in_ch, out_ch, temb, not last, norm_num_groups))
+        self.mid_block = UNetMidBlock2DCrossAttn(block_out_channels[-1], temb, heads, cross_attention_dim,
+                                                 norm_num_groups)
         self.up_blocks = nn.ModuleList()
         rev = list(reversed(block_out_channels))
         out_ch = rev[0]
@@ -336,10 +340,11 @@ class UNet2DConditionModel(nn.Module):
             in_ch = rev[min(i + 1, 3)]
             last = i == 3
             if i == 0:
-                self.up_blocks.append(UpBlock2D(in_ch, out_ch, prev_ch, temb, not last))
+                self.up_blocks.append(UpBlock2D(in_ch, out_ch, prev_ch, temb, not last, norm_num_groups))
             else:
-                self.up_blocks.append(CrossAttnUpBlock2D(in_ch, out_ch, prev_ch, temb, heads, cross_attention_dim, not last))
-        self.conv_norm_out = nn.GroupNorm(32, ch0, eps=1e-5)
+                self.up_blocks.append(CrossAttnUpBlock2D(in_ch, out_ch, prev_ch, temb, heads, cross_attention_dim,
+                                                         not last, norm_num_groups))
+        self.conv_norm_out = nn.GroupNorm(norm_num_groups, ch0, eps=1e-5)
         self.conv_act = nn.SiLU()
         self.conv_out = nn.Conv2d(ch0, out_channels, 3, padding=1)
         self.time_proj_dim = ch0

@@ -35,10 +35,11 @@ class AttentionBlock(nn.Module):
 
 
 class DownEncoderBlock2D(nn.Module):
-    def __init__(self, in_ch, out_ch, add_downsample):
+    def __init__(self, in_ch, out_ch, add_downsample, groups=32):
         super().__init__()
         self.resnets = nn.ModuleList(
-            [ResnetBlock2D(in_ch if i == 0 else out_ch, out_ch, temb_channels=None, eps=1e-6) for i in range(2)])
+            [ResnetBlock2D(in_ch if i == 0 else out_ch, out_ch, temb_channels=None, groups=groups, eps=1e-6)
+             for i in range(2)])
         self.downsamplers = nn.ModuleList([Downsample2D(out_ch, padding=0)]) if add_downsample else None
 
     def forward(self, x):
@@ -50,10 +51,11 @@ class DownEncoderBlock2D(nn.Module):
 
 
 class UNetMidBlock2D(nn.Module):
-    def __init__(self, ch):
+    def __init__(self, ch, groups=32):
         super().__init__()
-        self.resnets = nn.ModuleList([ResnetBlock2D(ch, ch, temb_channels=None, eps=1e-6) for _ in range(2)])
-        self.attentions = nn.ModuleList([AttentionBlock(ch)])
+        self.resnets = nn.ModuleList([ResnetBlock2D(ch, ch, temb_channels=None, groups=groups, eps=1e-6)
+                                      for _ in range(2)])
+        self.attentions = nn.ModuleList([AttentionBlock(ch, groups)])
 
     def forward(self, x):
         x = self.resnets[0](x)
@@ -62,16 +64,17 @@ class UNetMidBlock2D(nn.Module):
 
 
 class Encoder(nn.Module):
-    def __init__(self, in_channels=3, block_out_channels=(128, 256, 512, 512), latent_channels=4):
+    def __init__(self, in_channels=3, block_out_channels=(128, 256, 512, 512), latent_channels=4, norm_num_groups=32):
         super().__init__()
+        g = norm_num_groups
         self.conv_in = nn.Conv2d(in_channels, block_out_channels[0], 3, padding=1)
         self.down_blocks = nn.ModuleList()
         out_ch = block_out_channels[0]
         for i, ch in enumerate(block_out_channels):
             in_ch, out_ch = out_ch, ch
-            self.down_blocks.append(DownEncoderBlock2D(in_ch, out_ch, i < len(block_out_channels) - 1))
-        self.mid_block = UNetMidBlock2D(block_out_channels[-1])
-        self.conv_norm_out = nn.GroupNorm(32, block_out_channels[-1], eps=1e-6)
+            self.down_blocks.append(DownEncoderBlock2D(in_ch, out_ch, i < len(block_out_channels) - 1, g))
+        self.mid_block = UNetMidBlock2D(block_out_channels[-1], g)
+        self.conv_norm_out = nn.GroupNorm(g, block_out_channels[-1], eps=1e-6)
         self.conv_act = nn.SiLU()
         self.conv_out = nn.Conv2d(block_out_channels[-1], 2 * latent_channels, 3, padding=1)
 
@@ -89,9 +92,10 @@ class DiagonalGaussianDistribution:
 
 
 class AutoencoderKL(nn.Module):
-    def __init__(self, latent_channels=4, block_out_channels=(128, 256, 512, 512)):
+    def __init__(self, latent_channels=4, block_out_channels=(128, 256, 512, 512), norm_num_groups=32):
         super().__init__()
-        self.encoder = Encoder(block_out_channels=tuple(block_out_channels), latent_channels=latent_channels)
+        self.encoder = Encoder(block_out_channels=tuple(block_out_channels), latent_channels=latent_channels,
+                               norm_num_groups=norm_num_groups)
         self.quant_conv = nn.Conv2d(2 * latent_channels, 2 * latent_channels, 1)
 
     def encode(self, x, return_dict=True):

@@ -251,7 +251,7 @@ def gen_step_tiny():
     """One token-opt micro-iteration (optimize.py:362-445) on the tiny SD-1.5-shaped model, CPU."""
     pu, opt = REFM.ptp_utils, REFM.optimize
     it = REFM.invertable_transform
-    from stablekeypoints_amd.sd import build_sd15, TINY_CONFIG
+    from stablekeypoints_amd.sd import build_sd15, TINY_CONFIG, TINY_IMAGE
     parts = build_sd15(seed=0, config=TINY_CONFIG)
     psum = float(sum(p.double().sum() for p in list(parts.unet.parameters()) + list(parts.vae.parameters())))
     parts.scheduler = _RecordingScheduler(parts.scheduler)
@@ -269,7 +269,7 @@ def gen_step_tiny():
     def hook_fn(module, inp):   # optimize_token.py:59-68
         pu.register_attention_control(module, controllers[inp[0].device], feature_upsample_res=R)
     parts.unet.register_forward_pre_hook(hook_fn)
-    img = torch.from_numpy(recipes.uniform(51, (1, 3, 64, 64)))
+    img = torch.from_numpy(recipes.uniform(51, (1, 3, TINY_IMAGE, TINY_IMAGE)))
     ctx = torch.from_numpy(recipes.random_logits(52, (1, N, 32))).requires_grad_(True)
     T = it.RandomAffineWithInverse(degrees=15, scale=(0.8, 1.0), translate=(0.25, 0.25))
     kw = dict(layers=[0, 1, 2, 3], noise_level=-1, from_where=["down_cross", "mid_cross", "up_cross"],
