@@ -13,6 +13,8 @@
 // The backward recomputes the same rows, forms dZ = a ⊙ (g − Σ a g), applies the
 // horizontal adjoint into per-wave register accumulators (deterministic, no atomics),
 // writes row partials, and a second kernel applies the vertical adjoint.
+#include <algorithm>
+
 #include "skp_common.h"
 
 using namespace skp;
@@ -23,82 +25,139 @@ constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / WAVE;
 
 // ------------------------------------------------------------------------------------ fwd
-template <int NCH>
+// Lanes own token quads (4 consecutive tokens): V reads are ds_read_b128 and each pixel row
+// of attn leaves as 1 KiB float4 wave stores.  NQ = quads per lane (N <= 256*NQ).
+template <int NQ, bool VEC>
 __global__ __launch_bounds__(kThreads) void capture_fwd_kernel(const float* __restrict__ z, int BH, int s, int N,
                                                                int R, float* __restrict__ attn) {
   extern __shared__ __attribute__((aligned(16))) float V[];
-  constexpr int Np = NCH * WAVE;
+  constexpr int Np = NQ * 4 * WAVE;
   // block -> (b, y) with b fastest: consecutive blocks (one per XCD under round-robin
   // dispatch) take different heads, so each XCD's L2 keeps the z_low of the heads it serves.
   const int b = blockIdx.x % BH;
   const int y = blockIdx.x / BH;
   const Taps4 ty = bicubic_taps(y, s, R);
   const float* zb = z + (size_t)b * s * s * N;
-  for (int e = threadIdx.x; e < s * Np; e += kThreads) {
-    const int j = e / Np, n = e - j * Np;
-    float v = 0.0f;
-    if (n < N) {
-      v = ty.w[0] * zb[(size_t)(ty.i[0] * s + j) * N + n];
-      v += ty.w[1] * zb[(size_t)(ty.i[1] * s + j) * N + n];
-      v += ty.w[2] * zb[(size_t)(ty.i[2] * s + j) * N + n];
-      v += ty.w[3] * zb[(size_t)(ty.i[3] * s + j) * N + n];
+  if (VEC) {
+    float4* V4 = reinterpret_cast<float4*>(V);
+    const float4* r0 = reinterpret_cast<const float4*>(zb + (size_t)ty.i[0] * s * N);
+    const float4* r1 = reinterpret_cast<const float4*>(zb + (size_t)ty.i[1] * s * N);
+    const float4* r2 = reinterpret_cast<const float4*>(zb + (size_t)ty.i[2] * s * N);
+    const float4* r3 = reinterpret_cast<const float4*>(zb + (size_t)ty.i[3] * s * N);
+    const int nq = N / 4, Nq = N / 4, Npq = Np / 4;
+    for (int e = threadIdx.x; e < s * Npq; e += kThreads) {
+      const int j = e / Npq, q = e - j * Npq;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (q < nq) {
+        const size_t o = (size_t)j * Nq + q;
+        const float4 a0 = r0[o], a1 = r1[o], a2 = r2[o], a3 = r3[o];
+        v.x = ty.w[0] * a0.x + ty.w[1] * a1.x + ty.w[2] * a2.x + ty.w[3] * a3.x;
+        v.y = ty.w[0] * a0.y + ty.w[1] * a1.y + ty.w[2] * a2.y + ty.w[3] * a3.y;
+        v.z = ty.w[0] * a0.z + ty.w[1] * a1.z + ty.w[2] * a2.z + ty.w[3] * a3.z;
+        v.w = ty.w[0] * a0.w + ty.w[1] * a1.w + ty.w[2] * a2.w + ty.w[3] * a3.w;
+      }
+      V4[e] = v;
     }
-    V[e] = v;
+  } else {
+    for (int e = threadIdx.x; e < s * Np; e += kThreads) {
+      const int j = e / Np, n = e - j * Np;
+      float v = 0.0f;
+      if (n < N) {
+        v = ty.w[0] * zb[(size_t)(ty.i[0] * s + j) * N + n];
+        v += ty.w[1] * zb[(size_t)(ty.i[1] * s + j) * N + n];
+        v += ty.w[2] * zb[(size_t)(ty.i[2] * s + j) * N + n];
+        v += ty.w[3] * zb[(size_t)(ty.i[3] * s + j) * N + n];
+      }
+      V[e] = v;
+    }
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const float4* V4 = reinterpret_cast<const float4*>(V);
+  constexpr int Npq = Np / 4;
   float* orow = attn + ((size_t)b * R * R + (size_t)y * R) * N;
   for (int x = wid; x < R; x += kWaves) {
     const Taps4 tx = bicubic_taps(x, s, R);
-    float zc[NCH];
+    float4 zc[NQ];
     float m = -INFINITY;
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const int n = c * WAVE + lane;
-      float v = tx.w[0] * V[tx.i[0] * Np + n];
-      v += tx.w[1] * V[tx.i[1] * Np + n];
-      v += tx.w[2] * V[tx.i[2] * Np + n];
-      v += tx.w[3] * V[tx.i[3] * Np + n];
-      zc[c] = n < N ? v : -INFINITY;
-      m = fmaxf(m, zc[c]);
+    for (int c = 0; c < NQ; ++c) {
+      const int q = c * WAVE + lane;
+      const float4 a0 = V4[tx.i[0] * Npq + q], a1 = V4[tx.i[1] * Npq + q];
+      const float4 a2 = V4[tx.i[2] * Npq + q], a3 = V4[tx.i[3] * Npq + q];
+      float4 v;
+      v.x = tx.w[0] * a0.x + tx.w[1] * a1.x + tx.w[2] * a2.x + tx.w[3] * a3.x;
+      v.y = tx.w[0] * a0.y + tx.w[1] * a1.y + tx.w[2] * a2.y + tx.w[3] * a3.y;
+      v.z = tx.w[0] * a0.z + tx.w[1] * a1.z + tx.w[2] * a2.z + tx.w[3] * a3.z;
+      v.w = tx.w[0] * a0.w + tx.w[1] * a1.w + tx.w[2] * a2.w + tx.w[3] * a3.w;
+      const int n = 4 * q;
+      v.x = n < N ? v.x : -INFINITY;
+      v.y = n + 1 < N ? v.y : -INFINITY;
+      v.z = n + 2 < N ? v.z : -INFINITY;
+      v.w = n + 3 < N ? v.w : -INFINITY;
+      zc[c] = v;
+      m = fmaxf(m, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
     }
     m = wave_max(m);
     float ssum = 0.0f;
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const int n = c * WAVE + lane;
-      const float e = n < N ? expf(zc[c] - m) : 0.0f;
-      zc[c] = e;
-      ssum += e;
+    for (int c = 0; c < NQ; ++c) {
+      zc[c].x = __expf(zc[c].x - m);
+      zc[c].y = __expf(zc[c].y - m);
+      zc[c].z = __expf(zc[c].z - m);
+      zc[c].w = __expf(zc[c].w - m);
+      ssum += (zc[c].x + zc[c].y) + (zc[c].z + zc[c].w);
     }
     ssum = wave_sum(ssum);
+    const float inv = 1.0f / ssum;
     float* o = orow + (size_t)x * N;
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const int n = c * WAVE + lane;
-      if (n < N) o[n] = zc[c] / ssum;
+    for (int c = 0; c < NQ; ++c) {
+      const int n = 4 * (c * WAVE + lane);
+      const float4 v = make_float4(zc[c].x * inv, zc[c].y * inv, zc[c].z * inv, zc[c].w * inv);
+      if (VEC) {
+        if (n < N) *reinterpret_cast<float4*>(o + n) = v;
+      } else {
+        if (n < N) o[n] = v.x;
+        if (n + 1 < N) o[n + 1] = v.y;
+        if (n + 2 < N) o[n + 2] = v.z;
+        if (n + 3 < N) o[n + 3] = v.w;
+      }
     }
   }
 }
 
 // ------------------------------------------------------------------------------------ bwd
-// Phase A: one block per (b, y).  Wave w owns low-res columns j in [w·JPW, (w+1)·JPW).
-constexpr int kChunk = 16;  // output pixels per staged chunk
+// Phase A: one 512-thread block per (b, y).  Chunks of CH output pixels:
+//   (1) stage g for the chunk in LDS (strided global reads, scaled by gscale),
+//   (2) one wave per pixel recomputes the softmax row a and overwrites g with
+//       dZ = a ⊙ (g − Σ a g),
+//   (3) thread t owns tokens t, t+512, …: it applies the horizontal bicubic adjoint of the
+//       chunk into a register window of kWin low-res columns (uniform weights), then adds
+//       the window into its own dV[j][n] LDS cells.  Every dV cell has one owner thread and a
+//       fixed order, so the result is deterministic.
+// The host picks CH so that every chunk's taps fit in the window.
+constexpr int kBwdThreads = 512;
+constexpr int kBwdWaves = kBwdThreads / WAVE;
+constexpr int kWin = 8;
 
-template <int NCH, int JPW>
-__global__ __launch_bounds__(kThreads) void capture_bwd_rows_kernel(const float* __restrict__ z, int BH, int s,
-                                                                    int N, int R, const float* __restrict__ g,
-                                                                    long long sb, long long sp, long long sn,
-                                                                    float gscale, float* __restrict__ ws) {
+template <int NT>  // tokens per thread in the adjoint: N <= 512*NT (wave softmax uses 64-lane chunks)
+__global__ __launch_bounds__(kBwdThreads) void capture_bwd_rows_kernel(const float* __restrict__ z, int BH, int s,
+                                                                       int N, int R, int CH,
+                                                                       const float* __restrict__ g, long long sb,
+                                                                       long long sp, long long sn, float gscale,
+                                                                       float* __restrict__ ws) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  constexpr int Np = NCH * WAVE;
-  float* V = lds;               // s × Np
-  float* G = lds + s * Np;      // kChunk × Np
+  constexpr int Np = NT * kBwdThreads;
+  constexpr int NCH = Np / WAVE;
+  float* V = lds;                 // s × Np
+  float* dV = lds + s * Np;       // s × Np
+  float* G = dV + s * Np;         // CH × Np
   const int b = blockIdx.x % BH;
   const int y = blockIdx.x / BH;
   const Taps4 ty = bicubic_taps(y, s, R);
   const float* zb = z + (size_t)b * s * s * N;
-  for (int e = threadIdx.x; e < s * Np; e += kThreads) {
+  for (int e = threadIdx.x; e < s * Np; e += kBwdThreads) {
     const int j = e / Np, n = e - j * Np;
     float v = 0.0f;
     if (n < N) {
@@ -108,33 +167,27 @@ __global__ __launch_bounds__(kThreads) void capture_bwd_rows_kernel(const float*
       v += ty.w[3] * zb[(size_t)(ty.i[3] * s + j) * N + n];
     }
     V[e] = v;
+    dV[e] = 0.0f;
   }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int jbase = wid * JPW;
-  float acc[JPW][NCH];
-#pragma unroll
-  for (int jj = 0; jj < JPW; ++jj)
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) acc[jj][c] = 0.0f;
-
   const float* gb = g + (long long)b * sb + (long long)y * R * sp;
-  for (int x0 = 0; x0 < R; x0 += kChunk) {
-    __syncthreads();  // previous chunk's G fully consumed (and V ready on the first pass)
+  for (int x0 = 0; x0 < R; x0 += CH) {
+    __syncthreads();  // previous chunk's G consumed (and V/dV initialised on the first pass)
     if (sn == 1) {
-      for (int e = threadIdx.x; e < kChunk * Np; e += kThreads) {
+      for (int e = threadIdx.x; e < CH * Np; e += kBwdThreads) {
         const int xx = e / Np, n = e - xx * Np;
         const int x = x0 + xx;
         G[e] = (n < N && x < R) ? gb[(long long)x * sp + n] * gscale : 0.0f;
       }
     } else {
-      for (int e = threadIdx.x; e < kChunk * Np; e += kThreads) {
-        const int n = e / kChunk, xx = e - n * kChunk;
+      for (int e = threadIdx.x; e < CH * Np; e += kBwdThreads) {
+        const int n = e / CH, xx = e - n * CH;
         const int x = x0 + xx;
         G[xx * Np + n] = (n < N && x < R) ? gb[(long long)x * sp + (long long)n * sn] * gscale : 0.0f;
       }
     }
     __syncthreads();
-    for (int xx = wid; xx < kChunk; xx += kWaves) {
+    for (int xx = wid; xx < CH; xx += kBwdWaves) {
       const int x = x0 + xx;
       if (x >= R) break;
       const Taps4 tx = bicubic_taps(x, s, R);
@@ -154,15 +207,15 @@ __global__ __launch_bounds__(kThreads) void capture_bwd_rows_kernel(const float*
       float ssum = 0.0f;
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
-        const int n = c * WAVE + lane;
-        a[c] = n < N ? expf(a[c] - m) : 0.0f;
+        a[c] = __expf(a[c] - m);
         ssum += a[c];
       }
       ssum = wave_sum(ssum);
+      const float inv = 1.0f / ssum;
       float dot = 0.0f;
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
-        a[c] = a[c] / ssum;
+        a[c] *= inv;
         dot += a[c] * G[xx * Np + c * WAVE + lane];
       }
       dot = wave_sum(dot);
@@ -173,46 +226,59 @@ __global__ __launch_bounds__(kThreads) void capture_bwd_rows_kernel(const float*
       }
     }
     __syncthreads();
-    // horizontal adjoint of this chunk into the wave's own columns (fixed order -> deterministic)
-    for (int xx = 0; xx < kChunk; ++xx) {
-      const int x = x0 + xx;
-      if (x >= R) break;
-      const Taps4 tx = bicubic_taps(x, s, R);
+    // horizontal adjoint of the chunk into a kWin-column register window
+    const int xlast = min(x0 + CH, R) - 1;
+    const int jlo = bicubic_taps(x0, s, R).i[0];
+    float acc[kWin][NT];
 #pragma unroll
-      for (int jj = 0; jj < JPW; ++jj) {
-        const int j = jbase + jj;
+    for (int sl = 0; sl < kWin; ++sl)
+#pragma unroll
+      for (int r = 0; r < NT; ++r) acc[sl][r] = 0.0f;
+    for (int x = x0; x <= xlast; ++x) {
+      const Taps4 tx = bicubic_taps(x, s, R);
+      float wv[kWin];
+#pragma unroll
+      for (int sl = 0; sl < kWin; ++sl) {
         float w = 0.0f;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) w += (tx.i[k] == j) ? tx.w[k] : 0.0f;
-        if (w != 0.0f && j < s) {
+        for (int k = 0; k < 4; ++k) w += (tx.i[k] - jlo == sl) ? tx.w[k] : 0.0f;
+        wv[sl] = w;
+      }
 #pragma unroll
-          for (int c = 0; c < NCH; ++c) acc[jj][c] += w * G[xx * Np + c * WAVE + lane];
-        }
+      for (int r = 0; r < NT; ++r) {
+        const float gv = G[(x - x0) * Np + r * kBwdThreads + threadIdx.x];
+#pragma unroll
+        for (int sl = 0; sl < kWin; ++sl) acc[sl][r] += wv[sl] * gv;
+      }
+    }
+#pragma unroll
+    for (int sl = 0; sl < kWin; ++sl) {
+      const int j = jlo + sl;
+      if (j < s) {
+#pragma unroll
+        for (int r = 0; r < NT; ++r) dV[j * Np + r * kBwdThreads + threadIdx.x] += acc[sl][r];
       }
     }
   }
+  __syncthreads();
   // ws layout (BH, R, s, N): row partials of the vertical adjoint's input
   float* wrow = ws + ((size_t)b * R + y) * (size_t)s * N;
-#pragma unroll
-  for (int jj = 0; jj < JPW; ++jj) {
-    const int j = jbase + jj;
-    if (j >= s) continue;
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const int n = c * WAVE + lane;
-      if (n < N) wrow[(size_t)j * N + n] = acc[jj][c];
-    }
+  for (int e = threadIdx.x; e < s * N; e += kBwdThreads) {
+    const int j = e / N, n = e - j * N;
+    wrow[e] = dV[j * Np + n];
   }
 }
 
-// Phase B: dz[b][i·s + j][n] = Σ_y wy(y→i) · ws[b][y][j][n]; one block per (b, i).
+// Phase B: dz[b][i·s + j][n] = Σ_y wy(y→i) · ws[b][y][j][n]; block = (b, i, element chunk).
+constexpr int kColChunk = 1024;
 __global__ __launch_bounds__(kThreads) void capture_bwd_cols_kernel(const float* __restrict__ ws, int BH, int s,
                                                                     int N, int R, float* __restrict__ dz) {
   __shared__ int ylist[1024];
   __shared__ float wlist[1024];
   __shared__ int ny;
-  const int b = blockIdx.x % BH;
-  const int i = blockIdx.x / BH;
+  const int bi = blockIdx.x;
+  const int b = bi % BH;
+  const int i = bi / BH;
   if (threadIdx.x == 0) {
     int cnt = 0;
     for (int y = 0; y < R; ++y) {
@@ -230,7 +296,8 @@ __global__ __launch_bounds__(kThreads) void capture_bwd_cols_kernel(const float*
   const size_t plane = (size_t)s * N;
   const float* wb = ws + (size_t)b * R * plane;
   float* out = dz + ((size_t)b * s * s + (size_t)i * s) * N;
-  for (int e = threadIdx.x; e < s * N; e += kThreads) {
+  const int e0 = blockIdx.y * kColChunk;
+  for (int e = e0 + threadIdx.x; e < min((int)plane, e0 + kColChunk); e += kThreads) {
     float acc = 0.0f;
     for (int t = 0; t < cnt; ++t) acc += wlist[t] * wb[(size_t)ylist[t] * plane + e];
     out[e] = acc;
@@ -242,66 +309,69 @@ struct LayerPtrs {
   const float* p[SKP_MAX_LAYERS];
 };
 
-constexpr int kTileP = 64, kTileN = 64;
+// One block owns kAggP consecutive pixels × ALL N tokens.  In every (layer, b) slab those
+// pixels are one contiguous run of kAggP·N floats, so the block streams it with 16-B loads in
+// address order (no partially used cache lines at row seams), keeps the 32 slab sums in
+// registers, and transposes the (pixel, token) tile through LDS for token-major stores.
+constexpr int kAggP = 16;
+constexpr int kAggThreads = 256;
 
-template <bool VEC>
-__global__ __launch_bounds__(kThreads) void aggregate_kernel(LayerPtrs lp, int L, int BH, int RR, int N,
-                                                             float count, float* __restrict__ out) {
-  __shared__ float T[kTileN][kTileP + 1];
-  const int p0 = blockIdx.x * kTileP, n0 = blockIdx.y * kTileN;
-  const int t = threadIdx.x, q = t & 15, r = t >> 4;
-  const int n = n0 + 4 * q;
-  float acc[4][4];
+template <int NV>  // float4 loads per thread per slab: kAggP*N <= 4*kAggThreads*NV
+__global__ __launch_bounds__(kAggThreads) void aggregate_kernel(LayerPtrs lp, int L, int BH, int RR, int N,
+                                                                float count, float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float tile[];   // kAggP*N floats
+  const int p0 = blockIdx.x * kAggP;
+  const int np = min(kAggP, RR - p0);
+  const int flat = np * N;                     // valid floats in this block's run
+  const int t = threadIdx.x;
+  float4 acc[NV];
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int v = 0; v < NV; ++v) acc[v] = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int nslab = L * BH;
+  for (int sl = 0; sl < nslab; sl += 2) {
+    float4 a[NV], c[NV];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) acc[a][c] = 0.0f;
-  for (int l = 0; l < L; ++l) {
-    const float* base = lp.p[l];
-#pragma unroll 2
-    for (int b = 0; b < BH; ++b) {
-      const float* bb = base + (size_t)b * RR * N;
-      float4 v[4];
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        const int p = p0 + r + 16 * a;
-        v[a] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (p < RR) {
-          const float* src = bb + (size_t)p * N + n;
-          if (VEC) {
-            if (n + 3 < N) v[a] = *reinterpret_cast<const float4*>(src);
-            else {
-              if (n < N) v[a].x = src[0];
-              if (n + 1 < N) v[a].y = src[1];
-              if (n + 2 < N) v[a].z = src[2];
-            }
-          } else {
-            if (n < N) v[a].x = src[0];
-            if (n + 1 < N) v[a].y = src[1];
-            if (n + 2 < N) v[a].z = src[2];
-            if (n + 3 < N) v[a].w = src[3];
-          }
-        }
+    for (int v = 0; v < NV; ++v) {
+      const int f = 4 * (t + v * kAggThreads);
+      const float4* src0 = reinterpret_cast<const float4*>(lp.p[sl / BH] + ((size_t)(sl % BH) * RR + p0) * N + f);
+      a[v] = f < flat ? *src0 : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (sl + 1 < nslab) {
+        const float4* src1 =
+            reinterpret_cast<const float4*>(lp.p[(sl + 1) / BH] + ((size_t)((sl + 1) % BH) * RR + p0) * N + f);
+        c[v] = f < flat ? *src1 : make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        c[v] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
+    }
 #pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        acc[a][0] += v[a].x;
-        acc[a][1] += v[a].y;
-        acc[a][2] += v[a].z;
-        acc[a][3] += v[a].w;
-      }
+    for (int v = 0; v < NV; ++v) {
+      acc[v].x += a[v].x; acc[v].y += a[v].y; acc[v].z += a[v].z; acc[v].w += a[v].w;
+      acc[v].x += c[v].x; acc[v].y += c[v].y; acc[v].z += c[v].z; acc[v].w += c[v].w;
     }
   }
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) T[4 * q + c][r + 16 * a] = acc[a][c];
-  __syncthreads();
-  const int pl = t & 63;
-  for (int nl = t >> 6; nl < kTileN; nl += kThreads / 64) {
-    const int nn = n0 + nl, pp = p0 + pl;
-    if (nn < N && pp < RR) out[(size_t)nn * RR + pp] = T[nl][pl] / count;
+  for (int v = 0; v < NV; ++v) {
+    const int f = 4 * (t + v * kAggThreads);
+    if (f < flat) *reinterpret_cast<float4*>(tile + f) = acc[v];
   }
+  __syncthreads();
+  // tile[pl·N + n] -> out[n·RR + p0 + pl]: 16 lanes write one token's 64-B pixel run
+  for (int e = t; e < np * N; e += kAggThreads) {
+    const int n = e / np, pl = e - n * np;
+    out[(size_t)n * RR + p0 + pl] = tile[pl * N + n] / count;
+  }
+}
+
+// Fallback for unaligned layouts (N % 4 != 0 or misaligned base pointers): scalar loads.
+__global__ __launch_bounds__(kAggThreads) void aggregate_scalar_kernel(LayerPtrs lp, int L, int BH, int RR, int N,
+                                                                       float count, float* __restrict__ out) {
+  const size_t e = (size_t)blockIdx.x * kAggThreads + threadIdx.x;   // (p, n) in slab order
+  if (e >= (size_t)RR * N) return;
+  const int p = e / N, n = e % N;
+  float acc = 0.0f;
+  for (int l = 0; l < L; ++l)
+    for (int b = 0; b < BH; ++b) acc += lp.p[l][(size_t)b * RR * N + e];
+  out[(size_t)n * RR + p] = acc / count;
 }
 
 __global__ __launch_bounds__(kThreads) void aggregate_index_kernel(LayerPtrs lp, int L, int BH, int RR, int N,
@@ -361,28 +431,60 @@ __global__ void bilinear_bwd_kernel(const float* __restrict__ gout, int C, int R
   gin[e] = acc;
 }
 
-template <int NCH>
-int launch_fwd(const float* z, int BH, int s, int N, int R, float* attn, hipStream_t st) {
-  const size_t lds = (size_t)s * NCH * WAVE * sizeof(float);
-  hipLaunchKernelGGL(capture_fwd_kernel<NCH>, dim3(BH * R), dim3(kThreads), lds, st, z, BH, s, N, R, attn);
-  return 0;
+template <int NQ>
+void launch_fwd(const float* z, int BH, int s, int N, int R, float* attn, hipStream_t st) {
+  const size_t lds = (size_t)s * NQ * 4 * WAVE * sizeof(float);
+  const bool vec = (N % 4 == 0) && ((reinterpret_cast<uintptr_t>(z) & 15) == 0) &&
+                   ((reinterpret_cast<uintptr_t>(attn) & 15) == 0);
+  if (vec)
+    hipLaunchKernelGGL((capture_fwd_kernel<NQ, true>), dim3(BH * R), dim3(kThreads), lds, st, z, BH, s, N, R, attn);
+  else
+    hipLaunchKernelGGL((capture_fwd_kernel<NQ, false>), dim3(BH * R), dim3(kThreads), lds, st, z, BH, s, N, R, attn);
 }
 
-template <int NCH, int JPW>
-void launch_bwd_rows(const float* z, int BH, int s, int N, int R, const float* g, long long sb, long long sp,
+template <int NT>
+void launch_bwd_rows(const float* z, int BH, int s, int N, int R, int CH, const float* g, long long sb, long long sp,
                      long long sn, float gscale, float* ws, hipStream_t st) {
-  const size_t lds = (size_t)(s + kChunk) * NCH * WAVE * sizeof(float);
-  hipLaunchKernelGGL((capture_bwd_rows_kernel<NCH, JPW>), dim3(BH * R), dim3(kThreads), lds, st, z, BH, s, N, R, g,
+  const size_t lds = (size_t)(2 * s + CH) * NT * kBwdThreads * sizeof(float);
+  hipLaunchKernelGGL((capture_bwd_rows_kernel<NT>), dim3(BH * R), dim3(kBwdThreads), lds, st, z, BH, s, N, R, CH, g,
                      sb, sp, sn, gscale, ws);
 }
 
-int nch_for(int N) {
-  if (N <= 64) return 1;
-  if (N <= 128) return 2;
-  if (N <= 256) return 4;
-  if (N <= 512) return 8;
-  if (N <= 1024) return 16;
+int nq_for(int N) {  // float4 quads per lane for the forward
+  if (N <= 256) return 1;
+  if (N <= 512) return 2;
+  if (N <= 1024) return 4;
   return -1;
+}
+
+int nt_for(int N) {  // tokens per thread for the backward
+  if (N <= 512) return 1;
+  if (N <= 1024) return 2;
+  return -1;
+}
+
+// host mirror of bicubic_taps (first/last tap of a pixel) to size the adjoint chunks
+void host_taps(int dst, int n_in, int n_out, int& lo, int& hi) {
+  const float scale = (float)n_in / (float)n_out;
+  const float src = scale * ((float)dst + 0.5f) - 0.5f;
+  const int i0 = (int)floorf(src);
+  lo = std::min(std::max(i0 - 1, 0), n_in - 1);
+  hi = std::min(std::max(i0 + 2, 0), n_in - 1);
+}
+
+// largest chunk (<= 16 pixels) whose tap columns always fit the kWin window
+int pick_chunk(int s, int R) {
+  for (int ch = 16; ch >= 1; --ch) {
+    bool ok = true;
+    for (int x0 = 0; x0 < R && ok; x0 += ch) {
+      int lo, hi, l2, h2;
+      host_taps(x0, s, R, lo, hi);
+      host_taps(std::min(x0 + ch, R) - 1, s, R, l2, h2);
+      ok = (h2 - lo) < kWin;
+    }
+    if (ok) return ch;
+  }
+  return 1;
 }
 
 }  // namespace
@@ -390,16 +492,14 @@ int nch_for(int N) {
 extern "C" int skp_capture_fwd(const float* z_low, int BH, int s, int N, int R, float* attn, void* stream) {
   SKP_CHECK_ARG(z_low && attn, "null pointer");
   SKP_CHECK_ARG(BH > 0 && s > 0 && R > 0 && N > 0, "non-positive shape");
-  const int nch = nch_for(N);
-  SKP_CHECK_ARG(nch > 0, "N > 1024 tokens is not supported");
-  SKP_CHECK_ARG((size_t)s * nch * WAVE * 4 <= 160 * 1024, "s*N too large for LDS");
+  const int nq = nq_for(N);
+  SKP_CHECK_ARG(nq > 0, "N > 1024 tokens is not supported");
+  SKP_CHECK_ARG((size_t)s * nq * 4 * WAVE * 4 <= 160 * 1024, "s*N too large for LDS");
   hipStream_t st = as_stream(stream);
-  switch (nch) {
+  switch (nq) {
     case 1: launch_fwd<1>(z_low, BH, s, N, R, attn, st); break;
     case 2: launch_fwd<2>(z_low, BH, s, N, R, attn, st); break;
-    case 4: launch_fwd<4>(z_low, BH, s, N, R, attn, st); break;
-    case 8: launch_fwd<8>(z_low, BH, s, N, R, attn, st); break;
-    default: launch_fwd<16>(z_low, BH, s, N, R, attn, st); break;
+    default: launch_fwd<4>(z_low, BH, s, N, R, attn, st); break;
   }
   SKP_LAUNCH_CHECK();
   return SKP_OK;
@@ -411,28 +511,17 @@ extern "C" int skp_capture_bwd(const float* z_low, int BH, int s, int N, int R, 
   SKP_CHECK_ARG(z_low && dattn && dz_low && workspace, "null pointer");
   SKP_CHECK_ARG(BH > 0 && s > 0 && R > 0 && N > 0, "non-positive shape");
   SKP_CHECK_ARG(R <= 1024, "R > 1024 is not supported");
-  const int nch = nch_for(N);
-  SKP_CHECK_ARG(nch > 0, "N > 1024 tokens is not supported");
-  SKP_CHECK_ARG(s <= 64, "s > 64 is not supported");
-  SKP_CHECK_ARG((size_t)(s + kChunk) * nch * WAVE * 4 <= 160 * 1024, "s*N too large for LDS");
+  const int nt = nt_for(N);
+  SKP_CHECK_ARG(nt > 0, "N > 1024 tokens is not supported");
+  const int CH = pick_chunk(s, R);
+  SKP_CHECK_ARG((size_t)(2 * s + CH) * nt * kBwdThreads * 4 <= 160 * 1024, "s*N too large for LDS");
   hipStream_t st = as_stream(stream);
-  const int jpw = (s + kWaves - 1) / kWaves;  // low-res columns per wave
-#define SKP_BWD_J(NC)                                                                            \
-  if (jpw <= 1) launch_bwd_rows<NC, 1>(z_low, BH, s, N, R, dattn, sb, sp, sn, gscale, workspace, st); \
-  else if (jpw <= 2) launch_bwd_rows<NC, 2>(z_low, BH, s, N, R, dattn, sb, sp, sn, gscale, workspace, st); \
-  else if (jpw <= 4) launch_bwd_rows<NC, 4>(z_low, BH, s, N, R, dattn, sb, sp, sn, gscale, workspace, st); \
-  else if (jpw <= 8) launch_bwd_rows<NC, 8>(z_low, BH, s, N, R, dattn, sb, sp, sn, gscale, workspace, st); \
-  else launch_bwd_rows<NC, 16>(z_low, BH, s, N, R, dattn, sb, sp, sn, gscale, workspace, st);
-  switch (nch) {
-    case 1: SKP_BWD_J(1) break;
-    case 2: SKP_BWD_J(2) break;
-    case 4: SKP_BWD_J(4) break;
-    case 8: SKP_BWD_J(8) break;
-    default: SKP_BWD_J(16) break;
-  }
-#undef SKP_BWD_J
+  if (nt == 1) launch_bwd_rows<1>(z_low, BH, s, N, R, CH, dattn, sb, sp, sn, gscale, workspace, st);
+  else launch_bwd_rows<2>(z_low, BH, s, N, R, CH, dattn, sb, sp, sn, gscale, workspace, st);
   SKP_LAUNCH_CHECK();
-  hipLaunchKernelGGL(capture_bwd_cols_kernel, dim3(BH * s), dim3(kThreads), 0, st, workspace, BH, s, N, R, dz_low);
+  const int chunks = (s * N + kColChunk - 1) / kColChunk;
+  hipLaunchKernelGGL(capture_bwd_cols_kernel, dim3(BH * s, chunks), dim3(kThreads), 0, st, workspace, BH, s, N, R,
+                     dz_low);
   SKP_LAUNCH_CHECK();
   return SKP_OK;
 }
@@ -456,11 +545,22 @@ extern "C" int skp_aggregate(const float* const* layers, int L, int BH, int RR, 
     hipLaunchKernelGGL(aggregate_index_kernel, dim3((RR + kThreads - 1) / kThreads, n_out), dim3(kThreads), 0, st, lp,
                        L, BH, RR, N, indices, n_out, count, out);
   } else {
-    dim3 grid((RR + kTileP - 1) / kTileP, (N + kTileN - 1) / kTileN);
-    if (aligned)
-      hipLaunchKernelGGL(aggregate_kernel<true>, grid, dim3(kThreads), 0, st, lp, L, BH, RR, N, count, out);
-    else
-      hipLaunchKernelGGL(aggregate_kernel<false>, grid, dim3(kThreads), 0, st, lp, L, BH, RR, N, count, out);
+    const int nv = (kAggP * N + 4 * kAggThreads - 1) / (4 * kAggThreads);
+    const bool vec = aligned && (RR % kAggP == 0) && nv <= 8;
+    const size_t lds = (size_t)kAggP * N * sizeof(float);
+    const dim3 grid((RR + kAggP - 1) / kAggP);
+    if (!vec) {
+      hipLaunchKernelGGL(aggregate_scalar_kernel, dim3(((size_t)RR * N + kAggThreads - 1) / kAggThreads),
+                         dim3(kAggThreads), 0, st, lp, L, BH, RR, N, count, out);
+    } else if (nv <= 1) {
+      hipLaunchKernelGGL(aggregate_kernel<1>, grid, dim3(kAggThreads), lds, st, lp, L, BH, RR, N, count, out);
+    } else if (nv <= 2) {
+      hipLaunchKernelGGL(aggregate_kernel<2>, grid, dim3(kAggThreads), lds, st, lp, L, BH, RR, N, count, out);
+    } else if (nv <= 4) {
+      hipLaunchKernelGGL(aggregate_kernel<4>, grid, dim3(kAggThreads), lds, st, lp, L, BH, RR, N, count, out);
+    } else {
+      hipLaunchKernelGGL(aggregate_kernel<8>, grid, dim3(kAggThreads), lds, st, lp, L, BH, RR, N, count, out);
+    }
   }
   SKP_LAUNCH_CHECK();
   return SKP_OK;
