@@ -150,13 +150,30 @@ __global__ __launch_bounds__(kBwdThreads) void capture_bwd_rows_kernel(const flo
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int Np = NT * kBwdThreads;
   constexpr int NCH = Np / WAVE;
-  float* V = lds;                 // s × Np
-  float* dV = lds + s * Np;       // s × Np
-  float* G = dV + s * Np;         // CH × Np
+  float* V = lds;                   // s × Np      vertical bicubic pass of z_low for row y
+  float* dV = V + s * Np;           // s × Np      horizontal adjoint accumulator (thread-owned cells)
+  float* G = dV + s * Np;           // CH × Np     g, then dZ, of the current pixel chunk
+  float* WV = G + CH * Np;          // R × kWin    per-pixel adjoint weights on its chunk's window
+  int* TI = reinterpret_cast<int*>(WV + R * kWin);   // R × 4 tap columns (forward recompute)
+  float* TW = reinterpret_cast<float*>(TI + R * 4);  // R × 4 tap weights
   const int b = blockIdx.x % BH;
   const int y = blockIdx.x / BH;
   const Taps4 ty = bicubic_taps(y, s, R);
   const float* zb = z + (size_t)b * s * s * N;
+  // per-pixel tables: taps, and the weights of each pixel on its chunk's kWin-column window
+  for (int x = threadIdx.x; x < R; x += kBwdThreads) {
+    const Taps4 tx = bicubic_taps(x, s, R);
+    const int jlo = bicubic_taps((x / CH) * CH, s, R).i[0];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { TI[x * 4 + k] = tx.i[k]; TW[x * 4 + k] = tx.w[k]; }
+#pragma unroll
+    for (int sl = 0; sl < kWin; ++sl) {
+      float w = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) w += (tx.i[k] - jlo == sl) ? tx.w[k] : 0.0f;
+      WV[x * kWin + sl] = w;
+    }
+  }
   for (int e = threadIdx.x; e < s * Np; e += kBwdThreads) {
     const int j = e / Np, n = e - j * Np;
     float v = 0.0f;
@@ -171,35 +188,48 @@ __global__ __launch_bounds__(kBwdThreads) void capture_bwd_rows_kernel(const flo
   }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const float* gb = g + (long long)b * sb + (long long)y * R * sp;
+  // token-major broadcast gradient (sp == 1, e.g. the collect_maps backward): float4 over pixels
+  const bool g4 = (sn != 1) && (sp == 1) && (sn % 4 == 0) && (CH % 4 == 0) &&
+                  ((reinterpret_cast<uintptr_t>(gb) & 15) == 0);
   for (int x0 = 0; x0 < R; x0 += CH) {
-    __syncthreads();  // previous chunk's G consumed (and V/dV initialised on the first pass)
+    __syncthreads();  // previous chunk's G consumed (and tables/V/dV ready on the first pass)
+    const int nx = min(CH, R - x0);
     if (sn == 1) {
       for (int e = threadIdx.x; e < CH * Np; e += kBwdThreads) {
         const int xx = e / Np, n = e - xx * Np;
-        const int x = x0 + xx;
-        G[e] = (n < N && x < R) ? gb[(long long)x * sp + n] * gscale : 0.0f;
+        G[e] = (n < N && xx < nx) ? gb[(long long)(x0 + xx) * sp + n] * gscale : 0.0f;
+      }
+    } else if (g4 && nx == CH) {
+      const int qx = CH / 4;
+      for (int e = threadIdx.x; e < qx * Np; e += kBwdThreads) {
+        const int n = e / qx, xq = e - n * qx;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (n < N) v = *reinterpret_cast<const float4*>(gb + (long long)n * sn + x0 + 4 * xq);
+        G[(4 * xq + 0) * Np + n] = v.x * gscale;
+        G[(4 * xq + 1) * Np + n] = v.y * gscale;
+        G[(4 * xq + 2) * Np + n] = v.z * gscale;
+        G[(4 * xq + 3) * Np + n] = v.w * gscale;
       }
     } else {
       for (int e = threadIdx.x; e < CH * Np; e += kBwdThreads) {
         const int n = e / CH, xx = e - n * CH;
-        const int x = x0 + xx;
-        G[xx * Np + n] = (n < N && x < R) ? gb[(long long)x * sp + (long long)n * sn] * gscale : 0.0f;
+        G[xx * Np + n] = (n < N && xx < nx) ? gb[(long long)(x0 + xx) * sp + (long long)n * sn] * gscale : 0.0f;
       }
     }
     __syncthreads();
-    for (int xx = wid; xx < CH; xx += kBwdWaves) {
+    for (int xx = wid; xx < nx; xx += kBwdWaves) {
       const int x = x0 + xx;
-      if (x >= R) break;
-      const Taps4 tx = bicubic_taps(x, s, R);
+      const int i0 = TI[x * 4], i1 = TI[x * 4 + 1], i2 = TI[x * 4 + 2], i3 = TI[x * 4 + 3];
+      const float w0 = TW[x * 4], w1 = TW[x * 4 + 1], w2 = TW[x * 4 + 2], w3 = TW[x * 4 + 3];
       float a[NCH];
       float m = -INFINITY;
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
         const int n = c * WAVE + lane;
-        float v = tx.w[0] * V[tx.i[0] * Np + n];
-        v += tx.w[1] * V[tx.i[1] * Np + n];
-        v += tx.w[2] * V[tx.i[2] * Np + n];
-        v += tx.w[3] * V[tx.i[3] * Np + n];
+        float v = w0 * V[i0 * Np + n];
+        v += w1 * V[i1 * Np + n];
+        v += w2 * V[i2 * Np + n];
+        v += w3 * V[i3 * Np + n];
         a[c] = n < N ? v : -INFINITY;
         m = fmaxf(m, a[c]);
       }
@@ -226,27 +256,20 @@ __global__ __launch_bounds__(kBwdThreads) void capture_bwd_rows_kernel(const flo
       }
     }
     __syncthreads();
-    // horizontal adjoint of the chunk into a kWin-column register window
-    const int xlast = min(x0 + CH, R) - 1;
-    const int jlo = bicubic_taps(x0, s, R).i[0];
+    // horizontal adjoint of the chunk into a kWin-column register window (weights from WV)
+    const int jlo = TI[x0 * 4];
     float acc[kWin][NT];
 #pragma unroll
     for (int sl = 0; sl < kWin; ++sl)
 #pragma unroll
       for (int r = 0; r < NT; ++r) acc[sl][r] = 0.0f;
-    for (int x = x0; x <= xlast; ++x) {
-      const Taps4 tx = bicubic_taps(x, s, R);
-      float wv[kWin];
-#pragma unroll
-      for (int sl = 0; sl < kWin; ++sl) {
-        float w = 0.0f;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) w += (tx.i[k] - jlo == sl) ? tx.w[k] : 0.0f;
-        wv[sl] = w;
-      }
+    for (int xx = 0; xx < nx; ++xx) {
+      const float4 wa = *reinterpret_cast<const float4*>(WV + (x0 + xx) * kWin);
+      const float4 wb = *reinterpret_cast<const float4*>(WV + (x0 + xx) * kWin + 4);
+      const float wv[kWin] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
 #pragma unroll
       for (int r = 0; r < NT; ++r) {
-        const float gv = G[(x - x0) * Np + r * kBwdThreads + threadIdx.x];
+        const float gv = G[xx * Np + r * kBwdThreads + threadIdx.x];
 #pragma unroll
         for (int sl = 0; sl < kWin; ++sl) acc[sl][r] += wv[sl] * gv;
       }
@@ -273,33 +296,32 @@ __global__ __launch_bounds__(kBwdThreads) void capture_bwd_rows_kernel(const flo
 constexpr int kColChunk = 1024;
 __global__ __launch_bounds__(kThreads) void capture_bwd_cols_kernel(const float* __restrict__ ws, int BH, int s,
                                                                     int N, int R, float* __restrict__ dz) {
-  __shared__ int ylist[1024];
-  __shared__ float wlist[1024];
-  __shared__ int ny;
-  const int bi = blockIdx.x;
-  const int b = bi % BH;
-  const int i = bi / BH;
-  if (threadIdx.x == 0) {
-    int cnt = 0;
-    for (int y = 0; y < R; ++y) {
-      const Taps4 ty = bicubic_taps(y, s, R);
-      float w = 0.0f;
-      bool hit = false;
-      for (int k = 0; k < 4; ++k)
-        if (ty.i[k] == i) { w += ty.w[k]; hit = true; }
-      if (hit && w != 0.0f) { ylist[cnt] = y; wlist[cnt] = w; ++cnt; }
-    }
-    ny = cnt;
+  __shared__ float wy[1024];
+  __shared__ int ylo, yhi;
+  const int b = blockIdx.x % BH;
+  const int i = blockIdx.x / BH;
+  if (threadIdx.x == 0) { ylo = R; yhi = -1; }
+  __syncthreads();
+  for (int y = threadIdx.x; y < R; y += kThreads) {   // weight of low-res row i in output row y
+    const Taps4 ty = bicubic_taps(y, s, R);
+    float w = 0.0f;
+    bool hit = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (ty.i[k] == i) { w += ty.w[k]; hit = true; }
+    wy[y] = w;
+    if (hit) { atomicMin(&ylo, y); atomicMax(&yhi, y); }
   }
   __syncthreads();
-  const int cnt = ny;
+  const int y0 = ylo, y1 = yhi;
   const size_t plane = (size_t)s * N;
   const float* wb = ws + (size_t)b * R * plane;
   float* out = dz + ((size_t)b * s * s + (size_t)i * s) * N;
   const int e0 = blockIdx.y * kColChunk;
-  for (int e = e0 + threadIdx.x; e < min((int)plane, e0 + kColChunk); e += kThreads) {
+  const int e1 = min((int)plane, e0 + kColChunk);
+  for (int e = e0 + threadIdx.x; e < e1; e += kThreads) {
     float acc = 0.0f;
-    for (int t = 0; t < cnt; ++t) acc += wlist[t] * wb[(size_t)ylist[t] * plane + e];
+    for (int y = y0; y <= y1; ++y) acc += wy[y] * wb[(size_t)y * plane + e];
     out[e] = acc;
   }
 }
@@ -442,12 +464,19 @@ void launch_fwd(const float* z, int BH, int s, int N, int R, float* attn, hipStr
     hipLaunchKernelGGL((capture_fwd_kernel<NQ, false>), dim3(BH * R), dim3(kThreads), lds, st, z, BH, s, N, R, attn);
 }
 
+size_t bwd_rows_lds(int s, int N, int R, int CH);
+
 template <int NT>
 void launch_bwd_rows(const float* z, int BH, int s, int N, int R, int CH, const float* g, long long sb, long long sp,
                      long long sn, float gscale, float* ws, hipStream_t st) {
-  const size_t lds = (size_t)(2 * s + CH) * NT * kBwdThreads * sizeof(float);
+  const size_t lds = bwd_rows_lds(s, N, R, CH);
   hipLaunchKernelGGL((capture_bwd_rows_kernel<NT>), dim3(BH * R), dim3(kBwdThreads), lds, st, z, BH, s, N, R, CH, g,
                      sb, sp, sn, gscale, ws);
+}
+
+int nt_for(int N);
+size_t bwd_rows_lds(int s, int N, int R, int CH) {
+  return (size_t)(2 * s + CH) * nt_for(N) * kBwdThreads * sizeof(float) + (size_t)R * (kWin + 8) * sizeof(float);
 }
 
 int nq_for(int N) {  // float4 quads per lane for the forward
@@ -514,7 +543,7 @@ extern "C" int skp_capture_bwd(const float* z_low, int BH, int s, int N, int R, 
   const int nt = nt_for(N);
   SKP_CHECK_ARG(nt > 0, "N > 1024 tokens is not supported");
   const int CH = pick_chunk(s, R);
-  SKP_CHECK_ARG((size_t)(2 * s + CH) * nt * kBwdThreads * 4 <= 160 * 1024, "s*N too large for LDS");
+  SKP_CHECK_ARG(bwd_rows_lds(s, N, R, CH) <= 160 * 1024, "s*N too large for LDS");
   hipStream_t st = as_stream(stream);
   if (nt == 1) launch_bwd_rows<1>(z_low, BH, s, N, R, CH, dattn, sb, sp, sn, gscale, workspace, st);
   else launch_bwd_rows<2>(z_low, BH, s, N, R, CH, dattn, sb, sp, sn, gscale, workspace, st);

@@ -1,0 +1,64 @@
+"""Kernel micro-benchmark of the hot-path HIP kernels at SD-1.5 / N=500 shapes (dev tool).
+
+Runs each kernel `--iters` times on random inputs and prints HIP-event averages; meant to be
+run under `rocprofv3 --kernel-trace --stats` (or `--pmc ...`) for per-kernel breakdowns.
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from stablekeypoints_amd import ops  # noqa: E402
+
+
+def timed(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--tokens", type=int, default=500)
+    ap.add_argument("--only", default="")
+    args = ap.parse_args()
+    dev = "cuda:0"
+    N, R, H = args.tokens, 128, 8
+    g = torch.Generator(device=dev).manual_seed(0)
+    zs = {s: torch.randn(H, s * s, N, device=dev, generator=g) * 2 for s in (16, 32)}
+    attn = {s: ops.capture_attn(zs[s], s, R) for s in (16, 32)}
+    layers = [attn[16], attn[16], attn[16], attn[32]]
+    dmap = torch.randn(N, R * R, device=dev, generator=g)
+    gb = dmap.t().unsqueeze(0).expand(H, R * R, N)
+    res = {}
+    todo = args.only.split(",") if args.only else ["fwd16", "fwd32", "agg", "bwd16", "bwd32", "bwd16_dense"]
+    for name in todo:
+        if name == "fwd16":
+            res[name] = timed(lambda: ops.capture_attn(zs[16], 16, R), args.iters)
+        elif name == "fwd32":
+            res[name] = timed(lambda: ops.capture_attn(zs[32], 32, R), args.iters)
+        elif name == "agg":
+            res[name] = timed(lambda: ops.aggregate(layers), args.iters)
+        elif name == "bwd16":
+            res[name] = timed(lambda: ops.capture_bwd(zs[16], 16, R, gb), args.iters)
+        elif name == "bwd32":
+            res[name] = timed(lambda: ops.capture_bwd(zs[32], 32, R, gb), args.iters)
+        elif name == "bwd16_dense":
+            res[name] = timed(lambda: ops.capture_bwd(zs[16], 16, R, attn[16]), args.iters)
+    agg_bytes = (4 * H * R * R * N + N * R * R) * 4
+    for k, v in res.items():
+        extra = f"  {agg_bytes / (v * 1e-3) / 1e9:.0f} GB/s" if k == "agg" else ""
+        print(f"{k:12s} {v * 1e3:9.1f} us{extra}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
