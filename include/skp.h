@@ -41,11 +41,12 @@ int skp_version(void);
  *   z_low (BH, s*s, N) -> attn (BH, R*R, N).                                     */
 int skp_capture_fwd(const float* z_low, int BH, int s, int N, int R, float* attn, void* stream);
 
-/* Backward of skp_capture_fwd: dz_low = bicubicᵀ( a ⊙ (g − Σ_n a g) ).
- * g = dattn is read with element strides (sb, sp, sn) so a broadcast gradient
- * (e.g. sb = 0 from the layer mean of collect_maps) needs no materialisation.
- * `workspace` holds BH*R*s*N floats (the row-adjoint partials).               */
-int skp_capture_bwd(const float* z_low, int BH, int s, int N, int R, const float* dattn, long long sb,
+/* Backward of skp_capture_fwd: dz_low = bicubicᵀ( a ⊙ (g − Σ_n a g) ), g = gscale·dattn.
+ * Row b of g starts at dattn + (b / group)·sb and is read with strides (sp, sn), so a
+ * broadcast gradient needs no materialisation: the layer/head mean of collect_maps gives
+ * group = BH, sb = 0; a per-image map gradient (B, N, R²) gives group = heads,
+ * sb = N·R², sp = 1, sn = R².  `workspace` holds BH*R*s*N floats (row-adjoint partials). */
+int skp_capture_bwd(const float* z_low, int BH, int s, int N, int R, const float* dattn, int group, long long sb,
                     long long sp, long long sn, float gscale, float* dz_low, float* workspace, void* stream);
 
 /* ---------------------------------------------------------------- A3 aggregate

@@ -144,7 +144,8 @@ constexpr int kWin = 8;
 template <int NT>  // tokens per thread in the adjoint: N <= 512*NT (wave softmax uses 64-lane chunks)
 __global__ __launch_bounds__(kBwdThreads) void capture_bwd_rows_kernel(const float* __restrict__ z, int BH, int s,
                                                                        int N, int R, int CH,
-                                                                       const float* __restrict__ g, long long sb,
+                                                                       const float* __restrict__ g, int group,
+                                                                       long long sb,
                                                                        long long sp, long long sn, float gscale,
                                                                        float* __restrict__ ws) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -187,7 +188,7 @@ __global__ __launch_bounds__(kBwdThreads) void capture_bwd_rows_kernel(const flo
     dV[e] = 0.0f;
   }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const float* gb = g + (long long)b * sb + (long long)y * R * sp;
+  const float* gb = g + (long long)(b / group) * sb + (long long)y * R * sp;
   // token-major broadcast gradient (sp == 1, e.g. the collect_maps backward): float4 over pixels
   const bool g4 = (sn != 1) && (sp == 1) && (sn % 4 == 0) && (CH % 4 == 0) &&
                   ((reinterpret_cast<uintptr_t>(gb) & 15) == 0);
@@ -467,11 +468,11 @@ void launch_fwd(const float* z, int BH, int s, int N, int R, float* attn, hipStr
 size_t bwd_rows_lds(int s, int N, int R, int CH);
 
 template <int NT>
-void launch_bwd_rows(const float* z, int BH, int s, int N, int R, int CH, const float* g, long long sb, long long sp,
-                     long long sn, float gscale, float* ws, hipStream_t st) {
+void launch_bwd_rows(const float* z, int BH, int s, int N, int R, int CH, const float* g, int group, long long sb,
+                     long long sp, long long sn, float gscale, float* ws, hipStream_t st) {
   const size_t lds = bwd_rows_lds(s, N, R, CH);
   hipLaunchKernelGGL((capture_bwd_rows_kernel<NT>), dim3(BH * R), dim3(kBwdThreads), lds, st, z, BH, s, N, R, CH, g,
-                     sb, sp, sn, gscale, ws);
+                     group, sb, sp, sn, gscale, ws);
 }
 
 int nt_for(int N);
@@ -501,9 +502,11 @@ void host_taps(int dst, int n_in, int n_out, int& lo, int& hi) {
   hi = std::min(std::max(i0 + 2, 0), n_in - 1);
 }
 
-// largest chunk (<= 16 pixels) whose tap columns always fit the kWin window
-int pick_chunk(int s, int R) {
+// largest chunk (<= 16 pixels) whose tap columns always fit the kWin window and whose
+// LDS footprint fits one CU
+int pick_chunk(int s, int N, int R) {
   for (int ch = 16; ch >= 1; --ch) {
+    if (bwd_rows_lds(s, N, R, ch) > 160 * 1024) continue;
     bool ok = true;
     for (int x0 = 0; x0 < R && ok; x0 += ch) {
       int lo, hi, l2, h2;
@@ -534,19 +537,20 @@ extern "C" int skp_capture_fwd(const float* z_low, int BH, int s, int N, int R, 
   return SKP_OK;
 }
 
-extern "C" int skp_capture_bwd(const float* z_low, int BH, int s, int N, int R, const float* dattn, long long sb,
-                               long long sp, long long sn, float gscale, float* dz_low, float* workspace,
-                               void* stream) {
+extern "C" int skp_capture_bwd(const float* z_low, int BH, int s, int N, int R, const float* dattn, int group,
+                               long long sb, long long sp, long long sn, float gscale, float* dz_low,
+                               float* workspace, void* stream) {
   SKP_CHECK_ARG(z_low && dattn && dz_low && workspace, "null pointer");
+  SKP_CHECK_ARG(group >= 1, "group must be >= 1");
   SKP_CHECK_ARG(BH > 0 && s > 0 && R > 0 && N > 0, "non-positive shape");
   SKP_CHECK_ARG(R <= 1024, "R > 1024 is not supported");
   const int nt = nt_for(N);
   SKP_CHECK_ARG(nt > 0, "N > 1024 tokens is not supported");
-  const int CH = pick_chunk(s, R);
+  const int CH = pick_chunk(s, N, R);
   SKP_CHECK_ARG(bwd_rows_lds(s, N, R, CH) <= 160 * 1024, "s*N too large for LDS");
   hipStream_t st = as_stream(stream);
-  if (nt == 1) launch_bwd_rows<1>(z_low, BH, s, N, R, CH, dattn, sb, sp, sn, gscale, workspace, st);
-  else launch_bwd_rows<2>(z_low, BH, s, N, R, CH, dattn, sb, sp, sn, gscale, workspace, st);
+  if (nt == 1) launch_bwd_rows<1>(z_low, BH, s, N, R, CH, dattn, group, sb, sp, sn, gscale, workspace, st);
+  else launch_bwd_rows<2>(z_low, BH, s, N, R, CH, dattn, group, sb, sp, sn, gscale, workspace, st);
   SKP_LAUNCH_CHECK();
   const int chunks = (s * N + kColChunk - 1) / kColChunk;
   hipLaunchKernelGGL(capture_bwd_cols_kernel, dim3(BH * s, chunks), dim3(kThreads), 0, st, workspace, BH, s, N, R,

@@ -101,18 +101,23 @@ class CaptureAttn(torch.autograd.Function):
         return capture_bwd(z, ctx.s, ctx.R, dattn), None, None
 
 
-def capture_bwd(z, s, R, dattn, gscale=1.0):
+def capture_bwd(z, s, R, dattn, gscale=1.0, group=1, strides=None):
+    """dz_low for g = gscale·dattn; ``dattn`` (BH, R², N) of any strides, or with ``group``/
+    ``strides`` = (sb, sp, sn) a per-group gradient (row b uses group b // group)."""
     BH, S, N = z.shape
     if dattn.dtype != F32:
         dattn = dattn.float()
-    sb, sp, sn = dattn.stride()
-    if dattn.shape[0] == 1 and BH > 1:
-        sb = 0
+    if strides is None:
+        sb, sp, sn = dattn.stride()
+        if dattn.shape[0] == 1 and BH > 1:
+            sb = 0
+    else:
+        sb, sp, sn = strides
     ws = torch.empty(BH, R, s, N, device=z.device, dtype=F32)
     dz = torch.empty_like(z)
     with _timed("skp_capture_bwd", (BH * S * N * 2 + BH * R * s * N * 2) * 4):
-        call("skp_capture_bwd", ptr(z), BH, s, N, R, ptr(dattn), sb, sp, sn, float(gscale), ptr(dz), ptr(ws),
-             stream(z.device))
+        call("skp_capture_bwd", ptr(z), BH, s, N, R, ptr(dattn), int(group), sb, sp, sn, float(gscale), ptr(dz),
+             ptr(ws), stream(z.device))
     return dz
 
 
@@ -167,6 +172,82 @@ class _Aggregate(torch.autograd.Function):
 
 def aggregate(layers, indices=None, upsample_res=-1):
     return _Aggregate.apply(indices, int(upsample_res), *layers)
+
+
+class CaptureMaps(torch.autograd.Function):
+    """Per-image maps straight from the captured layers' logits (fused capture + aggregate).
+
+    zs[l]: (B·H, s_l², N) logits of captured layer l.  Output (B, N, R, R):
+    map[b] = mean over layers and the H heads of image b of softmax(bicubic(z)).
+    The (B·H, R², N) attention is produced into scratch and reduced (skp_capture_fwd +
+    skp_aggregate), never saved; the backward hands each layer's kernel the per-image map
+    gradient as a broadcast (group = H), so no (B·H, R², N) gradient is materialised.
+    """
+
+    @staticmethod
+    def forward(ctx, B, R, sizes, *zs):
+        zs = [_c(z) for z in zs]
+        BH, _, N = zs[0].shape
+        H = BH // B
+        L = len(zs)
+        dev = zs[0].device
+        RR = R * R
+        attn = [torch.empty(BH, RR, N, device=dev, dtype=F32) for _ in range(L)]
+        for z, a, s in zip(zs, attn, sizes):
+            with _timed("skp_capture_fwd", (BH * RR * N + BH * s * s * N) * 4):
+                call("skp_capture_fwd", ptr(z), BH, s, N, R, ptr(a), stream(dev))
+        out = torch.empty(B, N, R, R, device=dev, dtype=F32)
+        for b in range(B):
+            off = b * H * RR * N * 4
+            arr = (ctypes.c_void_p * L)(*[a.data_ptr() + off for a in attn])
+            with _timed("skp_aggregate", (L * H * RR * N + N * RR) * 4):
+                call("skp_aggregate", ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)), L, H, RR, N, None, N,
+                     ptr(out[b]), stream(dev))
+        del attn
+        ctx.save_for_backward(*zs)
+        ctx.meta = (B, H, R, N, list(sizes))
+        return out
+
+    @staticmethod
+    def backward(ctx, dmaps):
+        zs = ctx.saved_tensors
+        B, H, R, N, sizes = ctx.meta
+        dmaps = _c(dmaps)                       # (B, N, R, R)
+        RR = R * R
+        scale = 1.0 / float(len(zs) * H)
+        dzs = [capture_bwd(z, s, R, dmaps, gscale=scale, group=H, strides=(N * RR, 1, RR))
+               for z, s in zip(zs, sizes)]
+        return (None, None, None) + tuple(dzs)
+
+
+def capture_maps(zs, sizes, B, R):
+    """Per-image (B, N, R, R) maps from captured logits (see CaptureMaps)."""
+    return CaptureMaps.apply(int(B), int(R), tuple(int(s) for s in sizes), *zs)
+
+
+class _Resize(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, Ro):
+        x = _c(x)
+        C, R, _ = x.shape
+        out = torch.empty(C, Ro, Ro, device=x.device, dtype=F32)
+        call("skp_resize_bilinear", ptr(x), C, R, Ro, ptr(out), stream(x.device))
+        ctx.R = R
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = _c(g)
+        C, Ro, _ = g.shape
+        gin = torch.empty(C, ctx.R, ctx.R, device=g.device, dtype=F32)
+        call("skp_resize_bilinear_bwd", ptr(g), C, ctx.R, Ro, ptr(gin), stream(g.device))
+        return gin, None
+
+
+def resize_bilinear(x, Ro):
+    """(C, R, R) -> (C, Ro, Ro), F.interpolate(bilinear, align_corners=False) (optimize.py:63-70)."""
+    _lib.require_device(x)
+    return _Resize.apply(x, int(Ro))
 
 
 # --------------------------------------------------------------------------- A4-A6 argmax family

@@ -26,6 +26,18 @@ def collect_maps(controller, from_where=("up_cross",), upsample_res=512, layers=
     ``upsample_res != -1``; the bilinear resize is applied after the mean, which is
     equal because both are linear.
     """
+    if getattr(controller, "stores_logits", False):
+        # LogitStore: per-image fused maps, then the reference's mean over images (B·heads)
+        R = getattr(controller, "feature_upsample_res", None)
+        BH = controller.step_store["attn"][0].shape[0]
+        H = controller.heads
+        out = controller.maps_per_image(BH // H, R, layers).mean(dim=0)
+        if indices is not None:
+            out = out[torch.as_tensor(indices, device=out.device)]
+        if upsample_res != -1 and upsample_res != out.shape[-1]:
+            out = ops.resize_bilinear(out, upsample_res)
+        controller.reset()
+        return out
     attention_maps = controller.step_store["attn"]
     chosen = [a for li, a in enumerate(attention_maps) if li in layers]
     if not chosen:
@@ -90,8 +102,19 @@ class TokenOptimizer:
                  furthest_point_num_samples=25, sigma=2.0, num_subjects=1, sharpening_loss_weight=100,
                  equivariance_attn_loss_weight=1000.0, accum=4, noise_level=-1, layers=(0, 1, 2, 3),
                  from_where=("down_cross", "mid_cross", "up_cross"), augment_degrees=15, augment_scale=(0.8, 1.0),
-                 augment_translate=(0.25, 0.25), device="cuda"):
+                 augment_translate=(0.25, 0.25), device="cuda", batch_captures=True):
         self.ldm, self.controllers, self.device = ldm, controllers, device
+        # batch_captures: run the image and its warp through ONE B=2 VAE/UNet pass
+        # (run_and_find_attn_per_image); False = the reference's two sequential passes.
+        self.batch_captures = batch_captures
+        self._orig_controllers = controllers
+        if batch_captures:
+            # the fast path captures logits (LogitStore) and builds per-image maps fused
+            R = getattr(ldm, "feature_upsample_res", 128)
+            store = ptp_utils.LogitStore(early_exit=True)
+            store.feature_upsample_res = R
+            ptp_utils.register_attention_control(ldm.unet, store, feature_upsample_res=R)
+            self.controllers = {k: store for k in controllers} if controllers else {torch.device(device): store}
         self.context = context
         self.context.requires_grad = True
         self.optimizer = torch.optim.Adam([self.context], lr=lr)
@@ -106,13 +129,27 @@ class TokenOptimizer:
         self.world, self.rank = _world()
         self.reset_running()
 
+    def restore_hooks(self):
+        """Point the patched attention back at the caller's controllers."""
+        if self.batch_captures and self._orig_controllers:
+            ctl = next(iter(self._orig_controllers.values()))
+            R = getattr(self.ldm, "feature_upsample_res", 128)
+            ptp_utils.register_attention_control(self.ldm.unet, ctl, feature_upsample_res=R)
+
     def reset_running(self):
         self.run_eq = self.run_sh = self.run_tot = 0.0
 
     def micro_step(self, image):
-        attn_map = ptp_utils.run_and_find_attn(self.ldm, image, self.context, **self.kw)[0]
-        transformed_img = self.transform(image)
-        attention_map_transformed = ptp_utils.run_and_find_attn(self.ldm, transformed_img, self.context, **self.kw)[0]
+        if self.batch_captures:
+            transformed_img = self.transform(image)
+            attn_map, attention_map_transformed = ptp_utils.run_and_find_attn_per_image(
+                self.ldm, torch.cat([image, transformed_img]), self.context, noise_level=self.kw["noise_level"],
+                device=self.device, layers=self.kw["layers"], controllers=self.controllers)[0]
+        else:
+            attn_map = ptp_utils.run_and_find_attn(self.ldm, image, self.context, **self.kw)[0]
+            transformed_img = self.transform(image)
+            attention_map_transformed = ptp_utils.run_and_find_attn(self.ldm, transformed_img, self.context,
+                                                                     **self.kw)[0]
         if self.top_k_strategy == "entropy":
             cand = ptp_utils.entropy_sort(attn_map, self.fps_n)
         elif self.top_k_strategy == "gaussian":
@@ -196,6 +233,7 @@ def optimize_embedding(ldm, top_k_strategy="entropy", wandb_log=True, context=No
                       f"sharpening_loss: {rec['running_sharpening_loss']}, iteration time: {rec['iteration time']}",
                       flush=True)
             it_start = time.time()
+    opt.restore_hooks()
     if rank == 0 and log is None:
         print(f"optimization took {time.time() - start} seconds", flush=True)
     return context.detach()

@@ -84,6 +84,33 @@ class AttentionStore(AttentionControl):
         self.early_exit = early_exit
 
 
+class LogitStore(AttentionStore):
+    """Fast-path store: keeps each captured layer's low-resolution logits (B·H, s², N)
+    instead of the (B·H, R², N) attention; maps are produced by the fused
+    ``ops.capture_maps`` (per image) when collected, and the backward never
+    materialises a (B·H, R², N) gradient.  ``step_store["attn"]`` holds the logits and
+    ``step_store["size"]`` the grid side s of each."""
+
+    stores_logits = True
+
+    @staticmethod
+    def get_empty_store():
+        return {"attn": [], "size": []}
+
+    def forward(self, dict, is_cross: bool, place_in_unet: str):
+        self.step_store["attn"].append(dict["attn"])
+        self.step_store["size"].append(dict["size"])
+        self.heads = dict.get("heads", getattr(self, "heads", 8))
+        return dict
+
+    def maps_per_image(self, B, R, layers=(0, 1, 2, 3)):
+        zs = [z for li, z in enumerate(self.step_store["attn"]) if li in layers]
+        ss = [sz for li, sz in enumerate(self.step_store["size"]) if li in layers]
+        if not zs:
+            raise RuntimeError("LogitStore: no captured layers (is the hook registered?)")
+        return ops.capture_maps(zs, ss, B, R)
+
+
 # --------------------------------------------------------------------------- A1 capture hook
 def register_attention_control(model, controller, feature_upsample_res=256):
     """ptp_utils.py:472-573: patch every ``CrossAttention`` under children named "*up*"."""
@@ -116,8 +143,11 @@ def register_attention_control(model, controller, feature_upsample_res=256):
                     m = mask.reshape(batch_size, -1)[:, None, :].repeat(h, 1, 1)
                     sim_n = sim.masked_fill(~m, -torch.finfo(sim.dtype).max)
                 out = torch.bmm(sim_n.softmax(dim=-1), v)
-                attn = ops.capture_attn(sim, s, feature_upsample_res)  # (B·H, R², N), HIP
-                controller({"attn": attn}, is_cross, place_in_unet)
+                if getattr(controller, "stores_logits", False):
+                    controller({"attn": sim, "size": s, "heads": h}, is_cross, place_in_unet)
+                else:
+                    attn = ops.capture_attn(sim, s, feature_upsample_res)  # (B·H, R², N), HIP
+                    controller({"attn": attn}, is_cross, place_in_unet)
             else:
                 out = attention_core(q, k, v, self.scale, mask, h)
             out = to_out(self.reshape_batch_dim_to_heads(out))
@@ -220,6 +250,45 @@ def run_and_find_attn(ldm, image, context, noise_level=-1, device="cuda",
                                            upsample_res=upsample_res, layers=layers, indices=indices))
         controllers[controller].reset()
     return attention_maps
+
+
+def run_and_find_attn_per_image(ldm, images, context, noise_level=-1, device="cuda", layers=(0, 1, 2, 3),
+                                upsample_res=-1, indices=None, controllers=None):
+    """Batched capture: ONE VAE + UNet pass over B images, maps aggregated PER IMAGE.
+
+    Equivalent to B calls of ``run_and_find_attn`` with one image each (every UNet/VAE op is
+    per-sample; each image gets its own noise draw), but at batch B on the GPU.  The
+    reference's ``collect_maps`` averages over B·heads (optimize.py:75), which would mix
+    images at B > 1, so each image's (H, R², N) slice of the stored layers is aggregated
+    separately.  Returns a list (per controller) of lists (per image) of (N', R', R') maps.
+    """
+    find_pred_noise(ldm, images, context, noise_level=noise_level, device=device)
+    B = images.shape[0]
+    out = []
+    for key in controllers:
+        ctl = controllers[key]
+        if getattr(ctl, "stores_logits", False):
+            maps = ctl.maps_per_image(B, ldm.feature_upsample_res, layers)
+            res = []
+            for b in range(B):
+                m = maps[b]
+                if indices is not None:
+                    m = m[torch.as_tensor(indices, device=m.device)]
+                if upsample_res != -1 and upsample_res != m.shape[-1]:
+                    m = ops.resize_bilinear(m, upsample_res)
+                res.append(m)
+            out.append(res)
+            ctl.reset()
+            continue
+        stored = [a for li, a in enumerate(ctl.step_store["attn"]) if li in layers]
+        if not stored:
+            raise RuntimeError("no captured attention maps (is the hook registered?)")
+        H = stored[0].shape[0] // B
+        idx = None if indices is None else torch.as_tensor(indices, dtype=torch.int64)
+        out.append([ops.aggregate([a[b * H:(b + 1) * H] for a in stored], indices=idx, upsample_res=upsample_res)
+                    for b in range(B)])
+        ctl.reset()
+    return out
 
 
 def init_random_noise(device, num_words=77, dim=768):

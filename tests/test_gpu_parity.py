@@ -300,3 +300,57 @@ def test_token_opt_step_tiny_vs_reference():
     loss.backward()
     assert np.allclose(N(sharp), g["sharp"], rtol=1e-4) and np.allclose(N(eq), g["eq"], rtol=1e-3)
     assert np.allclose(N(ctx.grad), g["dctx"], rtol=1e-3, atol=1e-7)
+
+
+# ----------------------------------------------------------------------------- fused per-image path
+def test_capture_maps_per_image_fwd_bwd():
+    """CaptureMaps (B=2 images × 8 heads, 4 layers) == per-image capture+aggregate, fwd and bwd."""
+    from stablekeypoints_amd import ops
+    B, H, R, Nn = 2, 8, 32, 40
+    sizes = (4, 4, 4, 8)
+    zs = [recipes.random_logits(80 + i, (B * H, s * s, Nn), scale=2.0) for i, s in enumerate(sizes)]
+    zt = [T(z).requires_grad_(True) for z in zs]
+    maps = ops.capture_maps(zt, sizes, B, R)
+    attn = [O.capture_fwd(z, s, R) for z, s in zip(zs, sizes)]
+    for b in range(B):
+        ref = O.collect_maps([a[b * H:(b + 1) * H] for a in attn])
+        assert np.abs(N(maps[b]) - ref).max() < 1e-6
+    w = recipes.random_logits(90, (B, Nn, R, R))
+    (maps * T(w)).sum().backward()
+    for i, (z, s) in enumerate(zip(zs, sizes)):
+        dattn = np.concatenate([O.collect_maps_bwd([(H, R * R, Nn)] * 4, w[b])[i] for b in range(B)])
+        ref = O.capture_bwd(z, s, R, dattn)
+        assert np.abs(N(zt[i].grad) - ref).max() < 1e-4 * max(1.0, np.abs(ref).max())
+
+
+def test_batched_captures_match_sequential_tiny():
+    """TokenOptimizer: one B=2 pass (LogitStore, fused maps) == the reference's two passes."""
+    from stablekeypoints_amd import ptp_utils
+    from stablekeypoints_amd.optimize import TokenOptimizer
+    from stablekeypoints_amd.optimize_token import load_ldm
+    from stablekeypoints_amd.sd import TINY_CONFIG, TINY_IMAGE
+    res = {}
+    for batched in (False, True):
+        ldm, ctls, _ = load_ldm(DEV, "random", feature_upsample_res=32, config=TINY_CONFIG)
+        inner = ldm.scheduler
+        noises = [torch.randn(1, 4, TINY_IMAGE // 8, TINY_IMAGE // 8, generator=torch.Generator().manual_seed(i))
+                  .to(DEV) for i in range(2)]
+
+        class Sched:
+            timesteps = inner.timesteps
+
+            def add_noise(self, x, noise, t):
+                nz = torch.cat(noises[:x.shape[0]]) if x.shape[0] == 2 else noises.pop(0)
+                return inner.add_noise(x, nz, t)
+        ldm.scheduler = Sched()
+        ctx = torch.from_numpy(recipes.random_logits(52, (1, 16, 32))).to(DEV)
+        opt = TokenOptimizer(ldm, ctls, ctx, top_k=4, furthest_point_num_samples=8, accum=4, device=DEV,
+                             batch_captures=batched)
+        img = torch.from_numpy(recipes.uniform(51, (1, 3, TINY_IMAGE, TINY_IMAGE))).to(DEV)
+        th = torch.tensor([[[0.88, -0.14, -0.2], [0.14, 0.88, 0.19]]])
+        opt.transform.draw_theta = lambda batch: th
+        idx = opt.micro_step(img)
+        res[batched] = (N(idx), float(opt.run_tot), N(opt.context.grad))
+    assert np.array_equal(res[False][0], res[True][0])
+    assert abs(res[False][1] - res[True][1]) < 1e-5 * abs(res[False][1])
+    assert np.allclose(res[False][2], res[True][2], rtol=1e-3, atol=1e-8)
