@@ -140,6 +140,16 @@ class TokenOptimizer:
         self.run_eq = self.run_sh = self.run_tot = 0.0
 
     def micro_step(self, image):
+        """One reference micro-iteration on ``image`` (1, 3, H, W): loss, backward, running stats."""
+        loss, eq, sh, idx = self.image_loss(image)
+        self.run_eq = self.run_eq + eq.detach() / self.accum * self.w_eq
+        self.run_sh = self.run_sh + sh.detach() / self.accum * self.w_sharp
+        self.run_tot = self.run_tot + loss.detach() / self.accum
+        (loss / self.accum).backward()
+        return idx
+
+    def image_loss(self, image):
+        """optimize.py:372-437 for one image: (weighted loss, equivariance, sharpening, indices)."""
         if self.batch_captures:
             transformed_img = self.transform(image)
             attn_map, attention_map_transformed = ptp_utils.run_and_find_attn_per_image(
@@ -162,11 +172,7 @@ class TokenOptimizer:
         sh = sharpening_loss(attn_map[idx], device=self.device, sigma=self.sigma, num_subjects=self.num_subjects)
         eq = equivariance_loss(attn_map[idx], attention_map_transformed[idx][None], self.transform, 0)
         loss = eq * self.w_eq + sh * self.w_sharp
-        self.run_eq = self.run_eq + eq.detach() / self.accum * self.w_eq
-        self.run_sh = self.run_sh + sh.detach() / self.accum * self.w_sharp
-        self.run_tot = self.run_tot + loss.detach() / self.accum
-        (loss / self.accum).backward()
-        return idx
+        return loss, eq, sh, idx
 
     def optimizer_step(self):
         if self.world > 1:
