@@ -208,6 +208,8 @@ def main():
     ap.add_argument("--res", type=int, default=512)
     ap.add_argument("--upsample-res", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--attn-backend", default="math", choices=["math", "sdpa"],
+                    help="un-captured UNet attention: explicit fp32 GEMM+softmax (math) or torch SDPA")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
                     help="JSON with PMC-derived HBM bytes per launch of the roofline kernel")
     args = ap.parse_args()
@@ -223,7 +225,9 @@ def main():
     torch.cuda.set_device(dev)
 
     from stablekeypoints_amd import ops
+    from stablekeypoints_amd.sd.unet import CrossAttention
     from stablekeypoints_amd.optimize import TokenOptimizer
+    CrossAttention.backend = args.attn_backend
     from stablekeypoints_amd.optimize_token import load_ldm
     from stablekeypoints_amd.datasets import SyntheticDataset
 

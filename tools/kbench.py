@@ -36,7 +36,8 @@ def main():
     g = torch.Generator(device=dev).manual_seed(0)
     zs = {s: torch.randn(H, s * s, N, device=dev, generator=g) * 2 for s in (16, 32)}
     attn = {s: ops.capture_attn(zs[s], s, R) for s in (16, 32)}
-    layers = [attn[16], attn[16], attn[16], attn[32]]
+    # four DISTINCT layers (repeating one tensor would let the 256 MB L3 serve re-reads)
+    layers = [ops.capture_attn(zs[16] * (1 + 0.1 * i), 16, R) for i in range(3)] + [attn[32]]
     dmap = torch.randn(N, R * R, device=dev, generator=g)
     gb = dmap.t().unsqueeze(0).expand(H, R * R, N)
     res = {}

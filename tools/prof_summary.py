@@ -1,0 +1,54 @@
+"""Per-kernel summary of the TIMED region of a bench run from a rocprofv3 kernel trace.
+
+rocprofv3 --stats counts every dispatch, including the warm-up step in which MIOpen's Find
+benchmarks candidate convolution kernels (naive reference kernels among them), so the stats
+CSV over-states conv time.  This tool sorts dispatches by start time, splits them into
+token-opt micro-iterations at the one-per-micro-step `sort_topk_kernel`, keeps the last
+`--micro` micro-iterations (the timed steps × accum) and prints/writes per-kernel totals.
+
+usage: python tools/prof_summary.py TRACE.csv --micro 8 [--out summary.csv]
+"""
+import argparse
+import csv
+import collections
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--micro", type=int, required=True, help="micro-iterations in the timed region")
+    ap.add_argument("--marker", default="sort_topk_kernel")
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--top", type=int, default=30)
+    args = ap.parse_args()
+    rows = list(csv.DictReader(open(args.trace)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    marks = [i for i, r in enumerate(rows) if args.marker in r["Kernel_Name"]]
+    if len(marks) < args.micro + 1:
+        raise SystemExit(f"only {len(marks)} markers for {args.micro} micro-iterations")
+    # the timed region starts right after the marker that ends the last warm-up micro-iteration
+    start = marks[-args.micro - 1] + 1
+    sel = rows[start:]
+    t0 = int(sel[0]["Start_Timestamp"])
+    t1 = int(sel[-1]["End_Timestamp"])
+    agg = collections.defaultdict(lambda: [0, 0])
+    for r in sel:
+        d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        agg[r["Kernel_Name"]][0] += 1
+        agg[r["Kernel_Name"]][1] += d
+    total = sum(v[1] for v in agg.values())
+    items = sorted(agg.items(), key=lambda kv: -kv[1][1])
+    print(f"timed region: {len(sel)} dispatches, span {(t1 - t0) / 1e6:.1f} ms, kernel busy {total / 1e6:.1f} ms, "
+          f"{args.micro} micro-iterations -> {total / 1e6 / args.micro:.2f} ms kernel time per image")
+    for name, (n, d) in items[: args.top]:
+        print(f"{d / 1e6:9.2f} ms {100 * d / total:5.1f}% n={n:6d} avg={d / n / 1e3:9.1f} us  {name[:100]}")
+    if args.out:
+        with open(args.out, "w", newline="") as f:
+            w = csv.writer(f)
+            w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage"])
+            for name, (n, d) in items:
+                w.writerow([name, n, d, d / n, 100 * d / total])
+
+
+if __name__ == "__main__":
+    main()
