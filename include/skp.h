@@ -142,6 +142,19 @@ int skp_bgemm_f32(const float* A, long long sAb, long long sAm, long long sAk, c
                   long long sBk, long long sBn, float* C, long long sCb, long long sCm, long long sCn, int batch,
                   int M, int N, int K, float alpha, int accumulate, void* stream);
 
+/* ---------------------------------------------------------------- UNet-side: GroupNorm (+SiLU)
+ * The token-opt backward runs through the frozen SD-1.5 UNet; its
+ * GroupNorm → SiLU pairs (diffusers-0.8.0 ResnetBlock2D / Transformer2DModel.norm /
+ * VAE encoder) run fused here.  x, y, dx: (B, C, HW) NCHW fp32; act = 1 applies SiLU.
+ * stats (B*G*2 floats) = (mean, rstd) per group, written by fwd and read by bwd.
+ * partial: skp_groupnorm_workspace(B, C, HW, G) doubles.  Parameters are frozen, so the
+ * backward returns dx only.                                                      */
+int skp_groupnorm_workspace(int B, int C, long long HW, int G);
+int skp_groupnorm_fwd(const float* x, const float* gamma, const float* beta, int B, int C, long long HW, int G,
+                      float eps, int act, float* y, float* stats, double* partial, void* stream);
+int skp_groupnorm_bwd(const float* x, const float* dy, const float* gamma, const float* beta, const float* stats,
+                      int B, int C, long long HW, int G, int act, float* dx, double* partial, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,296 @@
+// Fused GroupNorm (+ optional SiLU) forward / input-gradient backward for the frozen SD-1.5
+// UNet / VAE (NCHW fp32) on gfx950.
+//
+// The hot path's backward runs through the UNet into the token embedding,
+// and GroupNorm is the UNet's largest non-GEMM cost (ATen: statistics kernel + separate
+// normalise and SiLU passes).  Here a group is one contiguous run of (C/G)·H·W floats:
+//   pass 1  per-chunk partial (Σx, Σx²) in fp64          (grid = B·G·nsplit blocks)
+//   pass 2  per-chunk: combine the group's partials in fixed order -> mean, rstd;
+//           y = act((x − mean)·rstd·γ + β)                (read x once, write y once)
+// Backward (parameters are frozen, so only dx): with z = x̂γ + β, gz = dy·act'(z),
+//   dx = rstd·(gz·γ − mean(gz·γ) − x̂·mean(gz·γ·x̂))
+//   pass 1  per-chunk partial (Σ gzγ, Σ gzγx̂) in fp64;  pass 2  dx.
+// All reductions have a fixed order, so results are run-to-run deterministic.
+#include "skp_common.h"
+
+using namespace skp;
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kChunk = 16384;   // floats per block (64 KiB)
+
+__device__ __forceinline__ float silu(float z) { return z / (1.0f + __expf(-z)); }
+__device__ __forceinline__ float silu_grad(float z) {
+  const float s = 1.0f / (1.0f + __expf(-z));
+  return s * (1.0f + z * (1.0f - s));
+}
+
+struct GNShape {
+  int B, C, G, cpg, nsplit;
+  long long HW, len;  // len = cpg * HW (floats per group)
+};
+
+__device__ __forceinline__ void block_sum2(double& a, double& b, double* sd) {
+  a = wave_sum(a);
+  b = wave_sum(b);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { sd[2 * wid] = a; sd[2 * wid + 1] = b; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double x = 0.0, y = 0.0;
+    for (int w = 0; w < kThreads / 64; ++w) { x += sd[2 * w]; y += sd[2 * w + 1]; }
+    sd[0] = x;
+    sd[1] = y;
+  }
+  __syncthreads();
+  a = sd[0];
+  b = sd[1];
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(kThreads) void gn_stats_kernel(const float* __restrict__ x, GNShape sh,
+                                                            double* __restrict__ partial) {
+  __shared__ double sd[2 * kThreads / 64];
+  const int grp = blockIdx.x / sh.nsplit, sp = blockIdx.x % sh.nsplit;
+  const float* base = x + (size_t)grp * sh.len;
+  const long long lo = (long long)sp * kChunk, hi = min(sh.len, lo + kChunk);
+  double s1 = 0.0, s2 = 0.0;
+  if (VEC) {
+    for (long long e = lo + 4 * threadIdx.x; e < hi; e += 4 * kThreads) {
+      const float4 v = *reinterpret_cast<const float4*>(base + e);
+      s1 += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
+      s2 += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+    }
+  } else {
+    for (long long e = lo + threadIdx.x; e < hi; e += kThreads) {
+      const double v = base[e];
+      s1 += v;
+      s2 += v * v;
+    }
+  }
+  block_sum2(s1, s2, sd);
+  if (threadIdx.x == 0) {
+    partial[2 * blockIdx.x] = s1;
+    partial[2 * blockIdx.x + 1] = s2;
+  }
+}
+
+// combine one group's partials (fixed order) -> (mean, rstd)
+__device__ __forceinline__ void group_moments(const double* __restrict__ partial, int grp, const GNShape& sh, float eps,
+                                              float& mean, float& rstd) {
+  double s1 = 0.0, s2 = 0.0;
+  for (int k = 0; k < sh.nsplit; ++k) {
+    s1 += partial[2 * (grp * sh.nsplit + k)];
+    s2 += partial[2 * (grp * sh.nsplit + k) + 1];
+  }
+  const double n = (double)sh.len;
+  const double m = s1 / n;
+  double var = s2 / n - m * m;
+  var = var < 0.0 ? 0.0 : var;
+  mean = (float)m;
+  rstd = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+template <bool VEC, bool ACT>
+__global__ __launch_bounds__(kThreads) void gn_apply_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta, GNShape sh, float eps,
+                                                            const double* __restrict__ partial, float* __restrict__ y,
+                                                            float* __restrict__ stats) {
+  __shared__ float sm[2];
+  const int grp = blockIdx.x / sh.nsplit, sp = blockIdx.x % sh.nsplit;
+  if (threadIdx.x == 0) {
+    float mean, rstd;
+    group_moments(partial, grp, sh, eps, mean, rstd);
+    sm[0] = mean;
+    sm[1] = rstd;
+    if (sp == 0 && stats) { stats[2 * grp] = mean; stats[2 * grp + 1] = rstd; }
+  }
+  __syncthreads();
+  const float mean = sm[0], rstd = sm[1];
+  const int g = grp % sh.G;
+  const float* base = x + (size_t)grp * sh.len;
+  float* out = y + (size_t)grp * sh.len;
+  const long long lo = (long long)sp * kChunk, hi = min(sh.len, lo + kChunk);
+  if (VEC) {   // HW % 4 == 0: a float4 never straddles two channels
+    for (long long e = lo + 4 * threadIdx.x; e < hi; e += 4 * kThreads) {
+      const int c = g * sh.cpg + (int)(e / sh.HW);
+      const float ga = gamma[c] * rstd, be = beta[c] - mean * gamma[c] * rstd;
+      float4 v = *reinterpret_cast<const float4*>(base + e);
+      v.x = v.x * ga + be; v.y = v.y * ga + be; v.z = v.z * ga + be; v.w = v.w * ga + be;
+      if (ACT) { v.x = silu(v.x); v.y = silu(v.y); v.z = silu(v.z); v.w = silu(v.w); }
+      *reinterpret_cast<float4*>(out + e) = v;
+    }
+  } else {
+    for (long long e = lo + threadIdx.x; e < hi; e += kThreads) {
+      const int c = g * sh.cpg + (int)(e / sh.HW);
+      float v = (base[e] - mean) * rstd * gamma[c] + beta[c];
+      out[e] = ACT ? silu(v) : v;
+    }
+  }
+}
+
+template <bool VEC, bool ACT>
+__global__ __launch_bounds__(kThreads) void gn_bwd_stats_kernel(const float* __restrict__ x,
+                                                                const float* __restrict__ dy,
+                                                                const float* __restrict__ gamma,
+                                                                const float* __restrict__ beta, GNShape sh,
+                                                                const float* __restrict__ stats,
+                                                                double* __restrict__ partial) {
+  __shared__ double sd[2 * kThreads / 64];
+  const int grp = blockIdx.x / sh.nsplit, sp = blockIdx.x % sh.nsplit;
+  const int g = grp % sh.G;
+  const float mean = stats[2 * grp], rstd = stats[2 * grp + 1];
+  const float* xb = x + (size_t)grp * sh.len;
+  const float* db = dy + (size_t)grp * sh.len;
+  const long long lo = (long long)sp * kChunk, hi = min(sh.len, lo + kChunk);
+  double s1 = 0.0, s2 = 0.0;
+  const long long step = VEC ? 4 : 1;
+  for (long long e0 = lo + step * threadIdx.x; e0 < hi; e0 += step * kThreads) {
+    const int c = g * sh.cpg + (int)(e0 / sh.HW);
+    const float ga = gamma[c], be = beta[c];
+    float xv[4], dv[4];
+    if (VEC) {
+      const float4 a = *reinterpret_cast<const float4*>(xb + e0), b = *reinterpret_cast<const float4*>(db + e0);
+      xv[0] = a.x; xv[1] = a.y; xv[2] = a.z; xv[3] = a.w;
+      dv[0] = b.x; dv[1] = b.y; dv[2] = b.z; dv[3] = b.w;
+    } else {
+      xv[0] = xb[e0];
+      dv[0] = db[e0];
+    }
+#pragma unroll
+    for (int k = 0; k < (VEC ? 4 : 1); ++k) {
+      const float xh = (xv[k] - mean) * rstd;
+      float gz = dv[k];
+      if (ACT) gz *= silu_grad(xh * ga + be);
+      const float gg = gz * ga;
+      s1 += (double)gg;
+      s2 += (double)gg * (double)xh;
+    }
+  }
+  block_sum2(s1, s2, sd);
+  if (threadIdx.x == 0) {
+    partial[2 * blockIdx.x] = s1;
+    partial[2 * blockIdx.x + 1] = s2;
+  }
+}
+
+template <bool VEC, bool ACT>
+__global__ __launch_bounds__(kThreads) void gn_bwd_apply_kernel(const float* __restrict__ x,
+                                                                const float* __restrict__ dy,
+                                                                const float* __restrict__ gamma,
+                                                                const float* __restrict__ beta, GNShape sh,
+                                                                const float* __restrict__ stats,
+                                                                const double* __restrict__ partial,
+                                                                float* __restrict__ dx) {
+  __shared__ float sm[2];
+  const int grp = blockIdx.x / sh.nsplit, sp = blockIdx.x % sh.nsplit;
+  if (threadIdx.x == 0) {
+    double s1 = 0.0, s2 = 0.0;
+    for (int k = 0; k < sh.nsplit; ++k) {
+      s1 += partial[2 * (grp * sh.nsplit + k)];
+      s2 += partial[2 * (grp * sh.nsplit + k) + 1];
+    }
+    sm[0] = (float)(s1 / (double)sh.len);
+    sm[1] = (float)(s2 / (double)sh.len);
+  }
+  __syncthreads();
+  const float ma = sm[0], mb = sm[1];
+  const int g = grp % sh.G;
+  const float mean = stats[2 * grp], rstd = stats[2 * grp + 1];
+  const float* xb = x + (size_t)grp * sh.len;
+  const float* db = dy + (size_t)grp * sh.len;
+  float* ob = dx + (size_t)grp * sh.len;
+  const long long lo = (long long)sp * kChunk, hi = min(sh.len, lo + kChunk);
+  const long long step = VEC ? 4 : 1;
+  for (long long e0 = lo + step * threadIdx.x; e0 < hi; e0 += step * kThreads) {
+    const int c = g * sh.cpg + (int)(e0 / sh.HW);
+    const float ga = gamma[c], be = beta[c];
+    float xv[4], dv[4], r[4];
+    if (VEC) {
+      const float4 a = *reinterpret_cast<const float4*>(xb + e0), b = *reinterpret_cast<const float4*>(db + e0);
+      xv[0] = a.x; xv[1] = a.y; xv[2] = a.z; xv[3] = a.w;
+      dv[0] = b.x; dv[1] = b.y; dv[2] = b.z; dv[3] = b.w;
+    } else {
+      xv[0] = xb[e0];
+      dv[0] = db[e0];
+    }
+#pragma unroll
+    for (int k = 0; k < (VEC ? 4 : 1); ++k) {
+      const float xh = (xv[k] - mean) * rstd;
+      float gz = dv[k];
+      if (ACT) gz *= silu_grad(xh * ga + be);
+      r[k] = rstd * (gz * ga - ma - xh * mb);
+    }
+    if (VEC) *reinterpret_cast<float4*>(ob + e0) = make_float4(r[0], r[1], r[2], r[3]);
+    else ob[e0] = r[0];
+  }
+}
+
+bool make_shape(int B, int C, long long HW, int G, GNShape& sh) {
+  if (B <= 0 || C <= 0 || HW <= 0 || G <= 0 || C % G != 0) return false;
+  sh.B = B; sh.C = C; sh.G = G; sh.cpg = C / G; sh.HW = HW;
+  sh.len = (long long)sh.cpg * HW;
+  sh.nsplit = (int)((sh.len + kChunk - 1) / kChunk);
+  return true;
+}
+
+}  // namespace
+
+extern "C" int skp_groupnorm_workspace(int B, int C, long long HW, int G) {
+  GNShape sh;
+  if (!make_shape(B, C, HW, G, sh)) return -1;
+  return B * G * sh.nsplit * 2;   // doubles
+}
+
+extern "C" int skp_groupnorm_fwd(const float* x, const float* gamma, const float* beta, int B, int C, long long HW,
+                                 int G, float eps, int act, float* y, float* stats, double* partial, void* stream) {
+  SKP_CHECK_ARG(x && gamma && beta && y && partial, "null pointer");
+  GNShape sh;
+  SKP_CHECK_ARG(make_shape(B, C, HW, G, sh), "bad shape (C must be divisible by G)");
+  const bool vec = (HW % 4 == 0) && ((reinterpret_cast<uintptr_t>(x) & 15) == 0) &&
+                   ((reinterpret_cast<uintptr_t>(y) & 15) == 0);
+  hipStream_t st = as_stream(stream);
+  const dim3 grid(B * G * sh.nsplit);
+  if (vec) hipLaunchKernelGGL(gn_stats_kernel<true>, grid, dim3(kThreads), 0, st, x, sh, partial);
+  else hipLaunchKernelGGL(gn_stats_kernel<false>, grid, dim3(kThreads), 0, st, x, sh, partial);
+  SKP_LAUNCH_CHECK();
+#define SKP_GN_APPLY(V, A) \
+  hipLaunchKernelGGL((gn_apply_kernel<V, A>), grid, dim3(kThreads), 0, st, x, gamma, beta, sh, eps, partial, y, stats)
+  if (vec) { if (act) SKP_GN_APPLY(true, true); else SKP_GN_APPLY(true, false); }
+  else { if (act) SKP_GN_APPLY(false, true); else SKP_GN_APPLY(false, false); }
+#undef SKP_GN_APPLY
+  SKP_LAUNCH_CHECK();
+  return SKP_OK;
+}
+
+extern "C" int skp_groupnorm_bwd(const float* x, const float* dy, const float* gamma, const float* beta,
+                                 const float* stats, int B, int C, long long HW, int G, int act, float* dx,
+                                 double* partial, void* stream) {
+  SKP_CHECK_ARG(x && dy && gamma && beta && stats && dx && partial, "null pointer");
+  GNShape sh;
+  SKP_CHECK_ARG(make_shape(B, C, HW, G, sh), "bad shape (C must be divisible by G)");
+  const bool vec = (HW % 4 == 0) && ((reinterpret_cast<uintptr_t>(x) & 15) == 0) &&
+                   ((reinterpret_cast<uintptr_t>(dy) & 15) == 0) && ((reinterpret_cast<uintptr_t>(dx) & 15) == 0);
+  hipStream_t st = as_stream(stream);
+  const dim3 grid(B * G * sh.nsplit);
+#define SKP_GN_B(K, V, A, ...) hipLaunchKernelGGL((K<V, A>), grid, dim3(kThreads), 0, st, __VA_ARGS__)
+  if (vec) {
+    if (act) SKP_GN_B(gn_bwd_stats_kernel, true, true, x, dy, gamma, beta, sh, stats, partial);
+    else SKP_GN_B(gn_bwd_stats_kernel, true, false, x, dy, gamma, beta, sh, stats, partial);
+  } else {
+    if (act) SKP_GN_B(gn_bwd_stats_kernel, false, true, x, dy, gamma, beta, sh, stats, partial);
+    else SKP_GN_B(gn_bwd_stats_kernel, false, false, x, dy, gamma, beta, sh, stats, partial);
+  }
+  SKP_LAUNCH_CHECK();
+  if (vec) {
+    if (act) SKP_GN_B(gn_bwd_apply_kernel, true, true, x, dy, gamma, beta, sh, stats, partial, dx);
+    else SKP_GN_B(gn_bwd_apply_kernel, true, false, x, dy, gamma, beta, sh, stats, partial, dx);
+  } else {
+    if (act) SKP_GN_B(gn_bwd_apply_kernel, false, true, x, dy, gamma, beta, sh, stats, partial, dx);
+    else SKP_GN_B(gn_bwd_apply_kernel, false, false, x, dy, gamma, beta, sh, stats, partial, dx);
+  }
+#undef SKP_GN_B
+  SKP_LAUNCH_CHECK();
+  return SKP_OK;
+}

@@ -439,3 +439,43 @@ def equivariance_loss_single(A, At, theta_inv):
     """mean((A − warp(At, theta_inv))²) with gradients into A and At."""
     _lib.require_device(A, At)
     return EquivarianceLoss.apply(A, At, theta_inv)
+
+
+# --------------------------------------------------------------------------- UNet-side GroupNorm(+SiLU)
+class GroupNormAct(torch.autograd.Function):
+    """y = act(GroupNorm(x)) with frozen affine parameters (dx only) — skp_groupnorm_fwd/bwd."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, groups, eps, act):
+        x = _c(x)
+        B, C = x.shape[:2]
+        HW = x[0, 0].numel()
+        nws = _lib.lib().skp_groupnorm_workspace(B, C, HW, groups)
+        if nws < 0:
+            raise ValueError(f"groupnorm: bad shape {tuple(x.shape)} groups={groups}")
+        part = torch.empty(nws, device=x.device, dtype=torch.float64)
+        stats = torch.empty(B * groups * 2, device=x.device, dtype=F32)
+        y = torch.empty_like(x)
+        g, b = _c(gamma.detach()), _c(beta.detach())
+        call("skp_groupnorm_fwd", ptr(x), ptr(g), ptr(b), B, C, HW, int(groups), float(eps), int(act), ptr(y),
+             ptr(stats), ptr(part), stream(x.device))
+        ctx.save_for_backward(x, g, b, stats)
+        ctx.meta = (B, C, HW, int(groups), int(act), nws)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, g, b, stats = ctx.saved_tensors
+        B, C, HW, G, act, nws = ctx.meta
+        dy = _c(dy)
+        dx = torch.empty_like(x)
+        part = torch.empty(nws, device=x.device, dtype=torch.float64)
+        call("skp_groupnorm_bwd", ptr(x), ptr(dy), ptr(g), ptr(b), ptr(stats), B, C, HW, G, act, ptr(dx), ptr(part),
+             stream(x.device))
+        return dx, None, None, None, None, None
+
+
+def group_norm_act(x, gamma, beta, groups, eps, act):
+    """Fused GroupNorm (+SiLU when act) on the HIP device; frozen gamma/beta."""
+    _lib.require_device(x)
+    return GroupNormAct.apply(x, gamma, beta, int(groups), float(eps), bool(act))

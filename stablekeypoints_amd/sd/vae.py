@@ -9,7 +9,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .unet import ResnetBlock2D, Downsample2D
+from .unet import ResnetBlock2D, Downsample2D, gn_act
 
 
 class AttentionBlock(nn.Module):
@@ -27,7 +27,7 @@ class AttentionBlock(nn.Module):
     def forward(self, x):
         b, c, h, w = x.shape
         res = x
-        t = self.group_norm(x).view(b, c, h * w).transpose(1, 2)
+        t = gn_act(self.group_norm, x, False).view(b, c, h * w).transpose(1, 2)
         q, k, v = self.query(t), self.key(t), self.value(t)
         o = F.scaled_dot_product_attention(q.unsqueeze(1), k.unsqueeze(1), v.unsqueeze(1), scale=1.0 / (c ** 0.5))[:, 0]
         o = self.proj_attn(o).transpose(1, 2).reshape(b, c, h, w)
@@ -83,7 +83,7 @@ class Encoder(nn.Module):
         for blk in self.down_blocks:
             x = blk(x)
         x = self.mid_block(x)
-        return self.conv_out(self.conv_act(self.conv_norm_out(x)))
+        return self.conv_out(gn_act(self.conv_norm_out, x, True))
 
 
 class DiagonalGaussianDistribution:
