@@ -14,6 +14,7 @@
 // horizontal adjoint into per-wave register accumulators (deterministic, no atomics),
 // writes row partials, and a second kernel applies the vertical adjoint.
 #include <algorithm>
+#include <cstdlib>
 
 #include "skp_common.h"
 
@@ -141,22 +142,22 @@ constexpr int kBwdThreads = 512;
 constexpr int kBwdWaves = kBwdThreads / WAVE;
 constexpr int kWin = 8;
 
-template <int NT>  // tokens per thread in the adjoint: N <= 512*NT (wave softmax uses 64-lane chunks)
+template <int NT, int ABL = 0>  // ABL: ablation (diagnostic builds only): 1 = no adjoint, 2 = no softmax
 __global__ __launch_bounds__(kBwdThreads) void capture_bwd_rows_kernel(const float* __restrict__ z, int BH, int s,
                                                                        int N, int R, int CH,
                                                                        const float* __restrict__ g, int group,
-                                                                       long long sb,
-                                                                       long long sp, long long sn, float gscale,
-                                                                       float* __restrict__ ws) {
+                                                                       long long sb, long long sp, long long sn,
+                                                                       float gscale, float* __restrict__ ws) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int Np = NT * kBwdThreads;
+  constexpr int Gp = Np + 1;        // padded G row: the transposed chunk stores hit distinct banks
   constexpr int NCH = Np / WAVE;
   float* V = lds;                   // s × Np      vertical bicubic pass of z_low for row y
   float* dV = V + s * Np;           // s × Np      horizontal adjoint accumulator (thread-owned cells)
-  float* G = dV + s * Np;           // CH × Np     g, then dZ, of the current pixel chunk
-  float* WV = G + CH * Np;          // R × kWin    per-pixel adjoint weights on its chunk's window
+  float* WV = dV + s * Np;          // R × kWin    per-pixel adjoint weights on its chunk's window
   int* TI = reinterpret_cast<int*>(WV + R * kWin);   // R × 4 tap columns (forward recompute)
   float* TW = reinterpret_cast<float*>(TI + R * 4);  // R × 4 tap weights
+  float* G = TW + R * 4;            // CH × Gp     g, then dZ, of the current pixel chunk
   const int b = blockIdx.x % BH;
   const int y = blockIdx.x / BH;
   const Taps4 ty = bicubic_taps(y, s, R);
@@ -175,50 +176,94 @@ __global__ __launch_bounds__(kBwdThreads) void capture_bwd_rows_kernel(const flo
       WV[x * kWin + sl] = w;
     }
   }
-  for (int e = threadIdx.x; e < s * Np; e += kBwdThreads) {
-    const int j = e / Np, n = e - j * Np;
-    float v = 0.0f;
-    if (n < N) {
-      v = ty.w[0] * zb[(size_t)(ty.i[0] * s + j) * N + n];
-      v += ty.w[1] * zb[(size_t)(ty.i[1] * s + j) * N + n];
-      v += ty.w[2] * zb[(size_t)(ty.i[2] * s + j) * N + n];
-      v += ty.w[3] * zb[(size_t)(ty.i[3] * s + j) * N + n];
+  // vertical pass (float4 along tokens when the layout allows) and dV = 0
+  if ((N & 3) == 0 && (reinterpret_cast<uintptr_t>(zb) & 15) == 0) {
+    const int nq = N / 4;
+    constexpr int Npq = Np / 4;
+    const float4* r0 = reinterpret_cast<const float4*>(zb + (size_t)ty.i[0] * s * N);
+    const float4* r1 = reinterpret_cast<const float4*>(zb + (size_t)ty.i[1] * s * N);
+    const float4* r2 = reinterpret_cast<const float4*>(zb + (size_t)ty.i[2] * s * N);
+    const float4* r3 = reinterpret_cast<const float4*>(zb + (size_t)ty.i[3] * s * N);
+    float4* V4 = reinterpret_cast<float4*>(V);
+    float4* dV4 = reinterpret_cast<float4*>(dV);
+    for (int e = threadIdx.x; e < s * Npq; e += kBwdThreads) {
+      const int j = e / Npq, q = e - j * Npq;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (q < nq) {
+        const size_t o = (size_t)j * nq + q;
+        const float4 a0 = r0[o], a1 = r1[o], a2 = r2[o], a3 = r3[o];
+        v.x = ty.w[0] * a0.x + ty.w[1] * a1.x + ty.w[2] * a2.x + ty.w[3] * a3.x;
+        v.y = ty.w[0] * a0.y + ty.w[1] * a1.y + ty.w[2] * a2.y + ty.w[3] * a3.y;
+        v.z = ty.w[0] * a0.z + ty.w[1] * a1.z + ty.w[2] * a2.z + ty.w[3] * a3.z;
+        v.w = ty.w[0] * a0.w + ty.w[1] * a1.w + ty.w[2] * a2.w + ty.w[3] * a3.w;
+      }
+      V4[e] = v;
+      dV4[e] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    V[e] = v;
-    dV[e] = 0.0f;
+  } else {
+    for (int e = threadIdx.x; e < s * Np; e += kBwdThreads) {
+      const int j = e / Np, n = e - j * Np;
+      float v = 0.0f;
+      if (n < N) {
+        v = ty.w[0] * zb[(size_t)(ty.i[0] * s + j) * N + n];
+        v += ty.w[1] * zb[(size_t)(ty.i[1] * s + j) * N + n];
+        v += ty.w[2] * zb[(size_t)(ty.i[2] * s + j) * N + n];
+        v += ty.w[3] * zb[(size_t)(ty.i[3] * s + j) * N + n];
+      }
+      V[e] = v;
+      dV[e] = 0.0f;
+    }
   }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const float* gb = g + (long long)(b / group) * sb + (long long)y * R * sp;
-  // token-major broadcast gradient (sp == 1, e.g. the collect_maps backward): float4 over pixels
-  const bool g4 = (sn != 1) && (sp == 1) && (sn % 4 == 0) && (CH % 4 == 0) &&
-                  ((reinterpret_cast<uintptr_t>(gb) & 15) == 0);
+  // token-major broadcast gradient (sp == 1, e.g. the collect_maps backward): float4 over pixels,
+  // prefetched into registers one chunk ahead so the loads overlap the chunk's compute.
+  const bool g4 = (sn != 1) && (sp == 1) && (sn % 4 == 0) && (CH % 4 == 0) && (R % CH == 0) &&
+                  ((reinterpret_cast<uintptr_t>(gb) & 15) == 0) && (CH * Np / 4) <= 4 * kBwdThreads;
+  constexpr int kPre = 4;   // float4 per thread per chunk (CH*Np/4 <= 4*kBwdThreads)
+  float4 pre[kPre];
+  auto prefetch = [&](int x0) {
+    const int qx = CH / 4;
+#pragma unroll
+    for (int k = 0; k < kPre; ++k) {
+      const int e = threadIdx.x + k * kBwdThreads;
+      const int n = e / qx, xq = e - n * qx;
+      pre[k] = (e < qx * Np && n < N && x0 < R)
+                   ? *reinterpret_cast<const float4*>(gb + (long long)n * sn + x0 + 4 * xq)
+                   : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  if (g4) prefetch(0);
   for (int x0 = 0; x0 < R; x0 += CH) {
     __syncthreads();  // previous chunk's G consumed (and tables/V/dV ready on the first pass)
     const int nx = min(CH, R - x0);
-    if (sn == 1) {
+    if (g4) {
+      const int qx = CH / 4;
+#pragma unroll
+      for (int k = 0; k < kPre; ++k) {
+        const int e = threadIdx.x + k * kBwdThreads;
+        if (e < qx * Np) {
+          const int n = e / qx, xq = e - n * qx;
+          G[(4 * xq + 0) * Gp + n] = pre[k].x * gscale;
+          G[(4 * xq + 1) * Gp + n] = pre[k].y * gscale;
+          G[(4 * xq + 2) * Gp + n] = pre[k].z * gscale;
+          G[(4 * xq + 3) * Gp + n] = pre[k].w * gscale;
+        }
+      }
+      prefetch(x0 + CH);   // next chunk's loads fly while this chunk computes
+    } else if (sn == 1) {
       for (int e = threadIdx.x; e < CH * Np; e += kBwdThreads) {
         const int xx = e / Np, n = e - xx * Np;
-        G[e] = (n < N && xx < nx) ? gb[(long long)(x0 + xx) * sp + n] * gscale : 0.0f;
-      }
-    } else if (g4 && nx == CH) {
-      const int qx = CH / 4;
-      for (int e = threadIdx.x; e < qx * Np; e += kBwdThreads) {
-        const int n = e / qx, xq = e - n * qx;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (n < N) v = *reinterpret_cast<const float4*>(gb + (long long)n * sn + x0 + 4 * xq);
-        G[(4 * xq + 0) * Np + n] = v.x * gscale;
-        G[(4 * xq + 1) * Np + n] = v.y * gscale;
-        G[(4 * xq + 2) * Np + n] = v.z * gscale;
-        G[(4 * xq + 3) * Np + n] = v.w * gscale;
+        G[xx * Gp + n] = (n < N && xx < nx) ? gb[(long long)(x0 + xx) * sp + n] * gscale : 0.0f;
       }
     } else {
       for (int e = threadIdx.x; e < CH * Np; e += kBwdThreads) {
         const int n = e / CH, xx = e - n * CH;
-        G[xx * Np + n] = (n < N && xx < nx) ? gb[(long long)(x0 + xx) * sp + (long long)n * sn] * gscale : 0.0f;
+        G[xx * Gp + n] = (n < N && xx < nx) ? gb[(long long)(x0 + xx) * sp + (long long)n * sn] * gscale : 0.0f;
       }
     }
     __syncthreads();
-    for (int xx = wid; xx < nx; xx += kBwdWaves) {
+    for (int xx = wid; xx < nx && ABL != 2; xx += kBwdWaves) {
       const int x = x0 + xx;
       const int i0 = TI[x * 4], i1 = TI[x * 4 + 1], i2 = TI[x * 4 + 2], i3 = TI[x * 4 + 3];
       const float w0 = TW[x * 4], w1 = TW[x * 4 + 1], w2 = TW[x * 4 + 2], w3 = TW[x * 4 + 3];
@@ -247,13 +292,13 @@ __global__ __launch_bounds__(kBwdThreads) void capture_bwd_rows_kernel(const flo
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
         a[c] *= inv;
-        dot += a[c] * G[xx * Np + c * WAVE + lane];
+        dot += a[c] * G[xx * Gp + c * WAVE + lane];
       }
       dot = wave_sum(dot);
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
         const int n = c * WAVE + lane;
-        G[xx * Np + n] = a[c] * (G[xx * Np + n] - dot);
+        G[xx * Gp + n] = a[c] * (G[xx * Gp + n] - dot);
       }
     }
     __syncthreads();
@@ -264,13 +309,13 @@ __global__ __launch_bounds__(kBwdThreads) void capture_bwd_rows_kernel(const flo
     for (int sl = 0; sl < kWin; ++sl)
 #pragma unroll
       for (int r = 0; r < NT; ++r) acc[sl][r] = 0.0f;
-    for (int xx = 0; xx < nx; ++xx) {
+    for (int xx = 0; xx < nx && ABL != 1; ++xx) {
       const float4 wa = *reinterpret_cast<const float4*>(WV + (x0 + xx) * kWin);
       const float4 wb = *reinterpret_cast<const float4*>(WV + (x0 + xx) * kWin + 4);
       const float wv[kWin] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
 #pragma unroll
       for (int r = 0; r < NT; ++r) {
-        const float gv = G[xx * Np + r * kBwdThreads + threadIdx.x];
+        const float gv = G[xx * Gp + r * kBwdThreads + threadIdx.x];
 #pragma unroll
         for (int sl = 0; sl < kWin; ++sl) acc[sl][r] += wv[sl] * gv;
       }
@@ -471,13 +516,23 @@ template <int NT>
 void launch_bwd_rows(const float* z, int BH, int s, int N, int R, int CH, const float* g, int group, long long sb,
                      long long sp, long long sn, float gscale, float* ws, hipStream_t st) {
   const size_t lds = bwd_rows_lds(s, N, R, CH);
-  hipLaunchKernelGGL((capture_bwd_rows_kernel<NT>), dim3(BH * R), dim3(kBwdThreads), lds, st, z, BH, s, N, R, CH, g,
-                     group, sb, sp, sn, gscale, ws);
+  const char* abl = getenv("SKP_BWD_ABLATION");   // diagnostic only
+  const int a = abl ? atoi(abl) : 0;
+  if (a == 1)
+    hipLaunchKernelGGL((capture_bwd_rows_kernel<NT, 1>), dim3(BH * R), dim3(kBwdThreads), lds, st, z, BH, s, N, R, CH,
+                       g, group, sb, sp, sn, gscale, ws);
+  else if (a == 2)
+    hipLaunchKernelGGL((capture_bwd_rows_kernel<NT, 2>), dim3(BH * R), dim3(kBwdThreads), lds, st, z, BH, s, N, R, CH,
+                       g, group, sb, sp, sn, gscale, ws);
+  else
+    hipLaunchKernelGGL((capture_bwd_rows_kernel<NT>), dim3(BH * R), dim3(kBwdThreads), lds, st, z, BH, s, N, R, CH, g,
+                       group, sb, sp, sn, gscale, ws);
 }
 
 int nt_for(int N);
 size_t bwd_rows_lds(int s, int N, int R, int CH) {
-  return (size_t)(2 * s + CH) * nt_for(N) * kBwdThreads * sizeof(float) + (size_t)R * (kWin + 8) * sizeof(float);
+  const size_t np = (size_t)nt_for(N) * kBwdThreads;
+  return (2 * s * np + (size_t)CH * (np + 1) + (size_t)R * (kWin + 8)) * sizeof(float);
 }
 
 int nq_for(int N) {  // float4 quads per lane for the forward
@@ -502,20 +557,25 @@ void host_taps(int dst, int n_in, int n_out, int& lo, int& hi) {
   hi = std::min(std::max(i0 + 2, 0), n_in - 1);
 }
 
-// largest chunk (<= 16 pixels) whose tap columns always fit the kWin window and whose
-// LDS footprint fits one CU
-int pick_chunk(int s, int N, int R) {
-  for (int ch = 16; ch >= 1; --ch) {
-    if (bwd_rows_lds(s, N, R, ch) > 160 * 1024) continue;
-    bool ok = true;
-    for (int x0 = 0; x0 < R && ok; x0 += ch) {
-      int lo, hi, l2, h2;
-      host_taps(x0, s, R, lo, hi);
-      host_taps(std::min(x0 + ch, R) - 1, s, R, l2, h2);
-      ok = (h2 - lo) < kWin;
-    }
-    if (ok) return ch;
+// chunk of output pixels for the backward: taps of every chunk must fit the kWin window and
+// the LDS footprint one CU; multiples of 4 that divide R come first (they enable the
+// prefetched float4 gradient path), then any size.
+bool chunk_ok(int ch, int s, int N, int R) {
+  if (bwd_rows_lds(s, N, R, ch) > 160 * 1024) return false;
+  for (int x0 = 0; x0 < R; x0 += ch) {
+    int lo, hi, l2, h2;
+    host_taps(x0, s, R, lo, hi);
+    host_taps(std::min(x0 + ch, R) - 1, s, R, l2, h2);
+    if (h2 - lo >= kWin) return false;
   }
+  return true;
+}
+
+int pick_chunk(int s, int N, int R) {
+  for (int ch = 16; ch >= 4; ch -= 4)
+    if (R % ch == 0 && chunk_ok(ch, s, N, R)) return ch;
+  for (int ch = 16; ch >= 1; --ch)
+    if (chunk_ok(ch, s, N, R)) return ch;
   return 1;
 }
 

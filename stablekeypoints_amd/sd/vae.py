@@ -9,7 +9,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .unet import ResnetBlock2D, Downsample2D, gn_act
+from .unet import ResnetBlock2D, Downsample2D, gn_act, attention_core
 
 
 class AttentionBlock(nn.Module):
@@ -29,7 +29,7 @@ class AttentionBlock(nn.Module):
         res = x
         t = gn_act(self.group_norm, x, False).view(b, c, h * w).transpose(1, 2)
         q, k, v = self.query(t), self.key(t), self.value(t)
-        o = F.scaled_dot_product_attention(q.unsqueeze(1), k.unsqueeze(1), v.unsqueeze(1), scale=1.0 / (c ** 0.5))[:, 0]
+        o = attention_core(q, k, v, 1.0 / (c ** 0.5))
         o = self.proj_attn(o).transpose(1, 2).reshape(b, c, h, w)
         return o + res
 
