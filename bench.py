@@ -208,6 +208,7 @@ def main():
     ap.add_argument("--res", type=int, default=512)
     ap.add_argument("--upsample-res", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--conv-benchmark", type=int, default=0, help="torch.backends.cudnn.benchmark (MIOpen exhaustive find)")
     ap.add_argument("--attn-backend", default="math", choices=["math", "sdpa"],
                     help="un-captured UNet attention: explicit fp32 GEMM+softmax (math) or torch SDPA")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
@@ -228,6 +229,7 @@ def main():
     from stablekeypoints_amd.sd.unet import CrossAttention
     from stablekeypoints_amd.optimize import TokenOptimizer
     CrossAttention.backend = args.attn_backend
+    torch.backends.cudnn.benchmark = bool(args.conv_benchmark)
     from stablekeypoints_amd.optimize_token import load_ldm
     from stablekeypoints_amd.datasets import SyntheticDataset
 

@@ -53,6 +53,15 @@ def main():
             res[name] = timed(lambda: ops.capture_bwd(zs[16], 16, R, gb), args.iters)
         elif name == "bwd32":
             res[name] = timed(lambda: ops.capture_bwd(zs[32], 32, R, gb), args.iters)
+        elif name == "sum1g":   # read-bandwidth reference: torch reduction over a fresh 1 GiB tensor
+            big = torch.empty(256 * 1024 * 1024, device=dev).normal_()
+            res[name] = timed(lambda: big.sum(), args.iters)
+            res[name + "_GBs"] = big.numel() * 4 / (res[name] * 1e-3) / 1e9 / 1e3
+        elif name == "copy1g":
+            big = torch.empty(256 * 1024 * 1024, device=dev).normal_()
+            dst = torch.empty_like(big)
+            res[name] = timed(lambda: dst.copy_(big), args.iters)
+            res[name + "_GBs"] = 2 * big.numel() * 4 / (res[name] * 1e-3) / 1e9 / 1e3
         elif name == "bwd16_dense":
             res[name] = timed(lambda: ops.capture_bwd(zs[16], 16, R, attn[16]), args.iters)
     agg_bytes = (4 * H * R * R * N + N * R * R) * 4

@@ -1,0 +1,23 @@
+"""torch.profiler op-level attribution of one token-opt micro-iteration (dev tool)."""
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+from torch.profiler import profile, ProfilerActivity
+from stablekeypoints_amd.optimize import TokenOptimizer
+from stablekeypoints_amd.optimize_token import load_ldm
+from stablekeypoints_amd.datasets import SyntheticDataset
+
+dev = torch.device("cuda:0")
+ldm, ctls, _ = load_ldm(dev, "random", feature_upsample_res=128)
+torch.manual_seed(0)
+ctx = torch.randn(1, 500, 768).to(dev)
+opt = TokenOptimizer(ldm, ctls, ctx, accum=4, device=dev)
+img = SyntheticDataset(n=2, size=512)[0]["img"][None].to(dev)
+for _ in range(3):
+    opt.micro_step(img)
+torch.cuda.synchronize()
+with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+    for _ in range(2):
+        opt.micro_step(img)
+    torch.cuda.synchronize()
+print(prof.key_averages().table(sort_by="self_cuda_time_total", row_limit=45, max_name_column_width=60))
