@@ -62,6 +62,20 @@ def main():
             dst = torch.empty_like(big)
             res[name] = timed(lambda: dst.copy_(big), args.iters)
             res[name + "_GBs"] = 2 * big.numel() * 4 / (res[name] * 1e-3) / 1e9 / 1e3
+        elif name.startswith("gemm"):   # capture logits q kᵀ and its two gradients at s=16/32
+            sz = 16 if name.endswith("16") else 32
+            d = 160 if sz == 16 else 80
+            q = torch.randn(2 * H, sz * sz, d, device=dev, generator=g)
+            k = torch.randn(2 * H, N, d, device=dev, generator=g)
+            dz = torch.randn(2 * H, sz * sz, N, device=dev, generator=g)
+            t_f = timed(lambda: ops.bgemm(q, k.transpose(1, 2), 0.1), args.iters)
+            t_q = timed(lambda: ops.bgemm(dz, k, 0.1), args.iters)
+            t_k = timed(lambda: ops.bgemm(dz.transpose(1, 2), q, 0.1), args.iters)
+            t_ref = timed(lambda: torch.bmm(q, k.transpose(1, 2)), args.iters)
+            fl = 2 * 2 * H * sz * sz * N * d
+            for nm, t in (("fwd", t_f), ("dq", t_q), ("dk", t_k), ("torch_fwd", t_ref)):
+                res[f"{name}_{nm}"] = t
+                res[f"{name}_{nm}_TFs"] = fl / (t * 1e-3) / 1e12 / 1e3
         elif name == "bwd16_dense":
             res[name] = timed(lambda: ops.capture_bwd(zs[16], 16, R, attn[16]), args.iters)
     agg_bytes = (4 * H * R * R * N + N * R * R) * 4
