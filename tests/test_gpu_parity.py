@@ -395,3 +395,29 @@ def test_unet_fused_groupnorm_matches_torch_groupnorm():
     unet_mod.USE_FUSED_GROUPNORM = True
     assert (outs[0][0] - outs[1][0]).abs().max().item() < 1e-4
     assert torch.allclose(outs[0][1], outs[1][1], rtol=1e-3, atol=1e-6)
+
+
+# ----------------------------------------------------------------------------- A16: SDXL shapes
+def test_sdxl_shaped_capture_path():
+    """SURVEY §8 A16 (SDXL, config 5): up_blocks[0] at 32², C=1280, 20 heads × hd 64, context 2048.
+    The reference's SDXL patch is inert (parity unpinned), so the capture path is checked at SDXL
+    shapes against the oracle (N=100 to keep the oracle fast) plus full-N properties."""
+    from stablekeypoints_amd import ops
+    H, s, R, d = 20, 32, 128, 64
+    g = torch.Generator().manual_seed(5)
+    for Nn in (100, 500):
+        q = torch.randn(1 * H, s * s, d, generator=g) * 0.5
+        k = torch.randn(1 * H, Nn, d, generator=g) * 0.5
+        z = ops.capture_logits(q.to(DEV), k.to(DEV), d ** -0.5)
+        zr = (q.double() @ k.double().transpose(1, 2) * d ** -0.5).float()
+        assert torch.allclose(z.cpu(), zr, atol=1e-4)
+        maps = ops.capture_maps([z] * 4, [s] * 4, 1, R)          # (1, N, 128, 128)
+        m = N(maps[0])
+        assert np.allclose(m.sum(0), 1.0, atol=1e-4)
+        if Nn == 100:
+            ref = O.collect_maps([O.capture_fwd(N(z), s, R)] * 4)
+            assert np.abs(m - ref).max() < 1e-6
+            w = recipes.random_logits(3, (Nn, R * R))
+            dz = N(ops.capture_bwd(z, s, R, T(w).t().unsqueeze(0).expand(H, R * R, Nn)))
+            dref = O.capture_bwd(N(z), s, R, np.broadcast_to(w.T[None], (H, R * R, Nn)).astype(np.float32))
+            assert np.abs(dz - dref).max() < 1e-4 * max(1.0, np.abs(dref).max())
