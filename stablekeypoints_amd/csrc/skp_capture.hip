@@ -27,7 +27,7 @@ constexpr int kWaves = kThreads / WAVE;
 // ------------------------------------------------------------------------------------ fwd
 // Lanes own token quads (4 consecutive tokens): V reads are ds_read_b128 and each pixel row
 // of attn leaves as 1 KiB float4 wave stores.  NQ = quads per lane (N <= 256*NQ).
-template <int NQ, bool VEC>
+template <int NQ, bool VEC, bool NTS = false>
 __global__ __launch_bounds__(kThreads) void capture_fwd_kernel(const float* __restrict__ z, int BH, int s, int N,
                                                                int R, float* __restrict__ attn) {
   extern __shared__ __attribute__((aligned(16))) float V[];
@@ -116,7 +116,15 @@ __global__ __launch_bounds__(kThreads) void capture_fwd_kernel(const float* __re
       const int n = 4 * (c * WAVE + lane);
       const float4 v = make_float4(zc[c].x * inv, zc[c].y * inv, zc[c].z * inv, zc[c].w * inv);
       if (VEC) {
-        if (n < N) *reinterpret_cast<float4*>(o + n) = v;
+        if (n < N) {
+          if (NTS) {   // attn is read once, by the aggregate: stream it past the caches
+            typedef float f4v __attribute__((ext_vector_type(4)));
+            f4v w = {v.x, v.y, v.z, v.w};
+            __builtin_nontemporal_store(w, reinterpret_cast<f4v*>(o + n));
+          } else {
+            *reinterpret_cast<float4*>(o + n) = v;
+          }
+        }
       } else {
         if (n < N) o[n] = v.x;
         if (n + 1 < N) o[n + 1] = v.y;
@@ -511,7 +519,13 @@ void launch_fwd(const float* z, int BH, int s, int N, int R, float* attn, hipStr
   const size_t lds = (size_t)s * NQ * 4 * WAVE * sizeof(float);
   const bool vec = (N % 4 == 0) && ((reinterpret_cast<uintptr_t>(z) & 15) == 0) &&
                    ((reinterpret_cast<uintptr_t>(attn) & 15) == 0);
-  if (vec)
+  // Non-temporal stores measured faster at s = 32 (64 KiB LDS, 2 blocks/CU: 96 -> 75-84 us) and
+  // slower at s = 16 (5 blocks/CU: 55 -> 80 us), N = 500, R = 128 (tools/kbench.py).
+  const bool nts = lds > 48 * 1024;
+  if (vec && nts)
+    hipLaunchKernelGGL((capture_fwd_kernel<NQ, true, true>), dim3(BH * R), dim3(kThreads), lds, st, z, BH, s, N, R,
+                       attn);
+  else if (vec)
     hipLaunchKernelGGL((capture_fwd_kernel<NQ, true>), dim3(BH * R), dim3(kThreads), lds, st, z, BH, s, N, R, attn);
   else
     hipLaunchKernelGGL((capture_fwd_kernel<NQ, false>), dim3(BH * R), dim3(kThreads), lds, st, z, BH, s, N, R, attn);
