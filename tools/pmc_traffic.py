@@ -1,0 +1,61 @@
+"""HBM traffic per launch of a kernel from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE).
+
+Both counters are in KB.  On gfx950 FETCH_SIZE reports half of wide coalesced reads, so it is
+doubled (MI355X_MICROARCH.md, HBM/rocprofv3 section); WRITE_SIZE is taken as is.  The median
+over launches is used (the first launch also pays cold TLB misses).
+
+usage: python tools/pmc_traffic.py FETCH.csv WRITE.csv --kernel aggregate_kernel \
+           --algorithmic 1081344000 --out profiles/pmc_traffic.json
+"""
+import argparse
+import csv
+import json
+import statistics
+
+
+def values(path, kernel, counter):
+    out = []
+    for r in csv.DictReader(open(path)):
+        if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            out.append(float(r["Counter_Value"]))
+    if not out:
+        raise SystemExit(f"no {counter} rows for {kernel} in {path}")
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch")
+    ap.add_argument("write")
+    ap.add_argument("--kernel", default="aggregate_kernel")
+    ap.add_argument("--name", default="skp_aggregate")
+    ap.add_argument("--algorithmic", type=int, default=1081344000)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    f = values(args.fetch, args.kernel, "FETCH_SIZE")
+    w = values(args.write, args.kernel, "WRITE_SIZE")
+    fm, wm = statistics.median(f), statistics.median(w)
+    fetch = fm * 1024 * 2
+    write = wm * 1024
+    res = {args.name: {
+        "hbm_bytes_per_launch": fetch + write,
+        "fetch_bytes_corrected": fetch,
+        "write_bytes": write,
+        "fetch_size_kb_raw_median": fm,
+        "write_size_kb_raw_median": wm,
+        "algorithmic_bytes_per_launch": args.algorithmic,
+        "traffic_over_algorithmic": (fetch + write) / args.algorithmic,
+        "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes (tools/gpu_prof.sh) on "
+                  "tools/kbench.py --only agg (N=500, R=128, 4 distinct layers x 8 heads); FETCH_SIZE (KB) x1024 x2 "
+                  "(gfx950: FETCH_SIZE reports half of wide coalesced reads, MI355X_MICROARCH.md HBM section), "
+                  "WRITE_SIZE (KB) x1024; median over launches (tools/pmc_traffic.py)",
+        "launches": min(len(f), len(w)),
+    }}
+    text = json.dumps(res, indent=1)
+    print(text)
+    if args.out:
+        open(args.out, "w").write(text + "\n")
+
+
+if __name__ == "__main__":
+    main()
