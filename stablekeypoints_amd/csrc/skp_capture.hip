@@ -11,8 +11,8 @@
 //   2. per output pixel x (one wave each): Z[n] = Σ_k wx_k · V[ix_k][n], softmax over n
 //      with wave64 shuffle reductions, coalesced store of the (N,) row of attn.
 // The backward recomputes the same rows, forms dZ = a ⊙ (g − Σ a g), applies the
-// horizontal adjoint into per-wave register accumulators (deterministic, no atomics),
-// writes row partials, and a second kernel applies the vertical adjoint.
+// horizontal adjoint into a rolling 4-column register window per token (deterministic, no
+// atomics), streams the row partials out, and a second kernel applies the vertical adjoint.
 #include <algorithm>
 
 #include "skp_common.h"
@@ -137,53 +137,94 @@ __global__ __launch_bounds__(kThreads) void capture_fwd_kernel(const float* __re
 
 // ------------------------------------------------------------------------------------ bwd
 // Phase A: one 512-thread block per (b, y).  Chunks of CH output pixels:
-//   (1) stage g for the chunk in LDS (strided global reads, scaled by gscale),
+//   (1) stage g for the chunk in LDS (float4 loads prefetched one chunk ahead when the
+//       gradient is token-major), scaled by gscale,
 //   (2) one wave per pixel recomputes the softmax row a and overwrites g with
 //       dZ = a ⊙ (g − Σ a g),
-//   (3) thread t owns tokens t, t+512, …: it applies the horizontal bicubic adjoint of the
-//       chunk into a register window of kWin low-res columns (uniform weights), then adds
-//       the window into its own dV[j][n] LDS cells.  Every dV cell has one owner thread and a
-//       fixed order, so the result is deterministic.
-// The host picks CH so that every chunk's taps fit in the window.
+//   (3) thread t owns tokens t, t+512, …: walking the pixels in order it applies the
+//       horizontal bicubic adjoint into a 4-register window over the low-res columns
+//       lo(x) … lo(x)+3 (lo = first tap before clamping).  lo never decreases along x, so
+//       when it advances the window's lowest column is complete and leaves as one coalesced
+//       store of the row partial ws[b][y][j][:]; the virtual columns −2, −1 and s, s+1 fold
+//       into 0 and s−1 exactly as torch's clamped taps do.  Each value has one owner thread
+//       and a fixed order: deterministic, no atomics, no LDS accumulator.
+// LDS = V (s × Np) + G (CH × (Np+1)) + tap tables, so two or three blocks share a CU.
 constexpr int kBwdThreads = 512;
 constexpr int kBwdWaves = kBwdThreads / WAVE;
-constexpr int kWin = 8;
+
+template <int NT>
+struct RowPartialWriter {   // streams finished low-res columns of one (b, y) row partial
+  float* wrow;
+  int N, s, pt;
+  float pend[NT];
+  __device__ __forceinline__ void store(int col, const float* v) const {
+#pragma unroll
+    for (int r = 0; r < NT; ++r) {
+      const int n = r * kBwdThreads + threadIdx.x;
+      if (n < N) wrow[(size_t)col * N + n] = v[r];
+    }
+  }
+  __device__ __forceinline__ void store_zero(int col) const {
+    const float z[NT] = {};
+    store(col, z);
+  }
+  // column c (virtual, −2 … s+1) is complete with value v
+  __device__ __forceinline__ void emit(int c, const float* v) {
+    const int t = min(max(c, 0), s - 1);
+    if (t != pt) {   // block-uniform
+      store(pt, pend);
+      for (int j = pt + 1; j < t; ++j) store_zero(j);
+      pt = t;
+#pragma unroll
+      for (int r = 0; r < NT; ++r) pend[r] = v[r];
+    } else {
+#pragma unroll
+      for (int r = 0; r < NT; ++r) pend[r] += v[r];
+    }
+  }
+  __device__ __forceinline__ void finish() {
+    store(pt, pend);
+    for (int j = pt + 1; j < s; ++j) store_zero(j);
+  }
+};
 
 template <int NT>
 __global__ __launch_bounds__(kBwdThreads) void capture_bwd_rows_kernel(const float* __restrict__ z, int BH, int s,
                                                                        int N, int R, int CH,
                                                                        const float* __restrict__ g, int group,
                                                                        long long sb, long long sp, long long sn,
-                                                                       float gscale, float* __restrict__ ws) {
+                                                                       float gscale, int share,
+                                                                       float* __restrict__ ws) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int Np = NT * kBwdThreads;
   constexpr int Gp = Np + 1;        // padded G row: the transposed chunk stores hit distinct banks
   constexpr int NCH = Np / WAVE;
-  float* V = lds;                   // s × Np      vertical bicubic pass of z_low for row y
-  float* dV = V + s * Np;           // s × Np      horizontal adjoint accumulator (thread-owned cells)
-  float* WV = dV + s * Np;          // R × kWin    per-pixel adjoint weights on its chunk's window
-  int* TI = reinterpret_cast<int*>(WV + R * kWin);   // R × 4 tap columns (forward recompute)
-  float* TW = reinterpret_cast<float*>(TI + R * 4);  // R × 4 tap weights
-  float* G = TW + R * 4;            // CH × Gp     g, then dZ, of the current pixel chunk
-  const int b = blockIdx.x % BH;
-  const int y = blockIdx.x / BH;
+  float* V = lds;                                   // s × Np   vertical bicubic pass of z_low for row y
+  float* TW = V + s * Np;                           // R × 4    tap weights (16-B aligned: Np % 4 == 0)
+  int* TL = reinterpret_cast<int*>(TW + R * 4);     // R        first tap column before clamping
+  float* G = reinterpret_cast<float*>(TL + R);      // CH × Gp  g, then dZ, of the current pixel chunk
+  // block -> (b, y).  When `share` consecutive heads read the same gradient rows (the heads of
+  // one image: group > 1, or a broadcast g), the heads of one (image, y) go to the same XCD back
+  // to back (workgroups are dispatched round-robin over the 8 XCDs), so that XCD's L2 fetches
+  // the g row once instead of once per head.
+  int b, y;
+  if (share > 1 && (R & 7) == 0 && BH % share == 0) {
+    const int xcd = blockIdx.x & 7, k = blockIdx.x >> 3;
+    const int h = k % share, rest = k / share, R8 = R >> 3;
+    y = (rest % R8) * 8 + xcd;
+    b = (rest / R8) * share + h;
+  } else {
+    b = blockIdx.x % BH;
+    y = blockIdx.x / BH;
+  }
   const Taps4 ty = bicubic_taps(y, s, R);
   const float* zb = z + (size_t)b * s * s * N;
-  // per-pixel tables: taps, and the weights of each pixel on its chunk's kWin-column window
   for (int x = threadIdx.x; x < R; x += kBwdThreads) {
     const Taps4 tx = bicubic_taps(x, s, R);
-    const int jlo = bicubic_taps((x / CH) * CH, s, R).i[0];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) { TI[x * 4 + k] = tx.i[k]; TW[x * 4 + k] = tx.w[k]; }
-#pragma unroll
-    for (int sl = 0; sl < kWin; ++sl) {
-      float w = 0.0f;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) w += (tx.i[k] - jlo == sl) ? tx.w[k] : 0.0f;
-      WV[x * kWin + sl] = w;
-    }
+    *reinterpret_cast<float4*>(TW + 4 * x) = make_float4(tx.w[0], tx.w[1], tx.w[2], tx.w[3]);
+    TL[x] = tx.lo;
   }
-  // vertical pass (float4 along tokens when the layout allows) and dV = 0
+  // vertical pass (float4 along tokens when the layout allows)
   if ((N & 3) == 0 && (reinterpret_cast<uintptr_t>(zb) & 15) == 0) {
     const int nq = N / 4;
     constexpr int Npq = Np / 4;
@@ -192,7 +233,6 @@ __global__ __launch_bounds__(kBwdThreads) void capture_bwd_rows_kernel(const flo
     const float4* r2 = reinterpret_cast<const float4*>(zb + (size_t)ty.i[2] * s * N);
     const float4* r3 = reinterpret_cast<const float4*>(zb + (size_t)ty.i[3] * s * N);
     float4* V4 = reinterpret_cast<float4*>(V);
-    float4* dV4 = reinterpret_cast<float4*>(dV);
     for (int e = threadIdx.x; e < s * Npq; e += kBwdThreads) {
       const int j = e / Npq, q = e - j * Npq;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -205,7 +245,6 @@ __global__ __launch_bounds__(kBwdThreads) void capture_bwd_rows_kernel(const flo
         v.w = ty.w[0] * a0.w + ty.w[1] * a1.w + ty.w[2] * a2.w + ty.w[3] * a3.w;
       }
       V4[e] = v;
-      dV4[e] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   } else {
     for (int e = threadIdx.x; e < s * Np; e += kBwdThreads) {
@@ -218,7 +257,6 @@ __global__ __launch_bounds__(kBwdThreads) void capture_bwd_rows_kernel(const flo
         v += ty.w[3] * zb[(size_t)(ty.i[3] * s + j) * N + n];
       }
       V[e] = v;
-      dV[e] = 0.0f;
     }
   }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -241,8 +279,21 @@ __global__ __launch_bounds__(kBwdThreads) void capture_bwd_rows_kernel(const flo
     }
   };
   if (g4) prefetch(0);
+  RowPartialWriter<NT> out;
+  out.wrow = ws + ((size_t)b * R + y) * (size_t)s * N;   // ws layout (BH, R, s, N)
+  out.N = N;
+  out.s = s;
+  out.pt = 0;
+  float acc[4][NT];
+#pragma unroll
+  for (int r = 0; r < NT; ++r) {
+    out.pend[r] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k][r] = 0.0f;
+  }
+  int base = -2;   // virtual column held by acc[0]
   for (int x0 = 0; x0 < R; x0 += CH) {
-    __syncthreads();  // previous chunk's G consumed (and tables/V/dV ready on the first pass)
+    __syncthreads();  // previous chunk's G consumed (and tables/V ready on the first pass)
     const int nx = min(CH, R - x0);
     if (g4) {
       const int qx = CH / 4;
@@ -272,17 +323,19 @@ __global__ __launch_bounds__(kBwdThreads) void capture_bwd_rows_kernel(const flo
     __syncthreads();
     for (int xx = wid; xx < nx; xx += kBwdWaves) {
       const int x = x0 + xx;
-      const int i0 = TI[x * 4], i1 = TI[x * 4 + 1], i2 = TI[x * 4 + 2], i3 = TI[x * 4 + 3];
-      const float w0 = TW[x * 4], w1 = TW[x * 4 + 1], w2 = TW[x * 4 + 2], w3 = TW[x * 4 + 3];
+      const int lo = TL[x];
+      const int i0 = max(lo, 0), i1 = min(max(lo + 1, 0), s - 1);
+      const int i2 = min(lo + 2, s - 1), i3 = min(lo + 3, s - 1);
+      const float4 w = *reinterpret_cast<const float4*>(TW + 4 * x);
       float a[NCH];
       float m = -INFINITY;
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
         const int n = c * WAVE + lane;
-        float v = w0 * V[i0 * Np + n];
-        v += w1 * V[i1 * Np + n];
-        v += w2 * V[i2 * Np + n];
-        v += w3 * V[i3 * Np + n];
+        float v = w.x * V[i0 * Np + n];
+        v += w.y * V[i1 * Np + n];
+        v += w.z * V[i2 * Np + n];
+        v += w.w * V[i3 * Np + n];
         a[c] = n < N ? v : -INFINITY;
         m = fmaxf(m, a[c]);
       }
@@ -295,87 +348,95 @@ __global__ __launch_bounds__(kBwdThreads) void capture_bwd_rows_kernel(const flo
       }
       ssum = wave_sum(ssum);
       const float inv = 1.0f / ssum;
+      float* Gx = G + xx * Gp;
       float dot = 0.0f;
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
         a[c] *= inv;
-        dot += a[c] * G[xx * Gp + c * WAVE + lane];
+        dot += a[c] * Gx[c * WAVE + lane];
       }
       dot = wave_sum(dot);
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
         const int n = c * WAVE + lane;
-        G[xx * Gp + n] = a[c] * (G[xx * Gp + n] - dot);
+        Gx[n] = a[c] * (Gx[n] - dot);
       }
     }
     __syncthreads();
-    // horizontal adjoint of the chunk into a kWin-column register window (weights from WV)
-    const int jlo = TI[x0 * 4];
-    float acc[kWin][NT];
-#pragma unroll
-    for (int sl = 0; sl < kWin; ++sl)
-#pragma unroll
-      for (int r = 0; r < NT; ++r) acc[sl][r] = 0.0f;
+    // horizontal adjoint of the chunk into the rolling 4-column window
     for (int xx = 0; xx < nx; ++xx) {
-      const float4 wa = *reinterpret_cast<const float4*>(WV + (x0 + xx) * kWin);
-      const float4 wb = *reinterpret_cast<const float4*>(WV + (x0 + xx) * kWin + 4);
-      const float wv[kWin] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+      const int x = x0 + xx;
+      const int lo = TL[x];
+      while (base < lo) {   // block-uniform: column `base` is complete
+        out.emit(base, acc[0]);
+#pragma unroll
+        for (int r = 0; r < NT; ++r) {
+          acc[0][r] = acc[1][r];
+          acc[1][r] = acc[2][r];
+          acc[2][r] = acc[3][r];
+          acc[3][r] = 0.0f;
+        }
+        ++base;
+      }
+      const float4 w = *reinterpret_cast<const float4*>(TW + 4 * x);
 #pragma unroll
       for (int r = 0; r < NT; ++r) {
         const float gv = G[xx * Gp + r * kBwdThreads + threadIdx.x];
-#pragma unroll
-        for (int sl = 0; sl < kWin; ++sl) acc[sl][r] += wv[sl] * gv;
-      }
-    }
-#pragma unroll
-    for (int sl = 0; sl < kWin; ++sl) {
-      const int j = jlo + sl;
-      if (j < s) {
-#pragma unroll
-        for (int r = 0; r < NT; ++r) dV[j * Np + r * kBwdThreads + threadIdx.x] += acc[sl][r];
+        acc[0][r] += w.x * gv;
+        acc[1][r] += w.y * gv;
+        acc[2][r] += w.z * gv;
+        acc[3][r] += w.w * gv;
       }
     }
   }
-  __syncthreads();
-  // ws layout (BH, R, s, N): row partials of the vertical adjoint's input
-  float* wrow = ws + ((size_t)b * R + y) * (size_t)s * N;
-  for (int e = threadIdx.x; e < s * N; e += kBwdThreads) {
-    const int j = e / N, n = e - j * N;
-    wrow[e] = dV[j * Np + n];
-  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) out.emit(base + k, acc[k]);
+  out.finish();
 }
 
-// Phase B: dz[b][i·s + j][n] = Σ_y wy(y→i) · ws[b][y][j][n]; block = (b, i, element chunk).
-constexpr int kColChunk = 1024;
+// Phase B: dz[b][i·s + j][n] = Σ_y wy(y→i) · ws[b][y][j][n]; block = (b, kColRows low-res rows,
+// element chunk): every ws row is read once per block for all the rows whose taps it feeds.
+constexpr int kColChunk = 256;
+constexpr int kColRows = 4;
 __global__ __launch_bounds__(kThreads) void capture_bwd_cols_kernel(const float* __restrict__ ws, int BH, int s,
                                                                     int N, int R, float* __restrict__ dz) {
-  __shared__ float wy[1024];
+  __shared__ float wy[kColRows][1024];
   __shared__ int ylo, yhi;
   const int b = blockIdx.x % BH;
-  const int i = blockIdx.x / BH;
+  const int i0 = (blockIdx.x / BH) * kColRows;
   if (threadIdx.x == 0) { ylo = R; yhi = -1; }
   __syncthreads();
-  for (int y = threadIdx.x; y < R; y += kThreads) {   // weight of low-res row i in output row y
+  for (int y = threadIdx.x; y < R; y += kThreads) {   // weight of low-res row i0+r in output row y
     const Taps4 ty = bicubic_taps(y, s, R);
-    float w = 0.0f;
     bool hit = false;
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (ty.i[k] == i) { w += ty.w[k]; hit = true; }
-    wy[y] = w;
+    for (int r = 0; r < kColRows; ++r) {
+      float w = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (ty.i[k] == i0 + r) { w += ty.w[k]; hit = true; }
+      wy[r][y] = w;
+    }
     if (hit) { atomicMin(&ylo, y); atomicMax(&yhi, y); }
   }
   __syncthreads();
   const int y0 = ylo, y1 = yhi;
+  const int nr = min(kColRows, s - i0);
   const size_t plane = (size_t)s * N;
   const float* wb = ws + (size_t)b * R * plane;
-  float* out = dz + ((size_t)b * s * s + (size_t)i * s) * N;
+  float* out = dz + ((size_t)b * s * s + (size_t)i0 * s) * N;
   const int e0 = blockIdx.y * kColChunk;
   const int e1 = min((int)plane, e0 + kColChunk);
   for (int e = e0 + threadIdx.x; e < e1; e += kThreads) {
-    float acc = 0.0f;
-    for (int y = y0; y <= y1; ++y) acc += wy[y] * wb[(size_t)y * plane + e];
-    out[e] = acc;
+    float acc[kColRows] = {};
+    for (int y = y0; y <= y1; ++y) {
+      const float v = wb[(size_t)y * plane + e];
+#pragma unroll
+      for (int r = 0; r < kColRows; ++r) acc[r] += wy[r][y] * v;
+    }
+#pragma unroll
+    for (int r = 0; r < kColRows; ++r)
+      if (r < nr) out[(size_t)r * plane + e] = acc[r];
   }
 }
 
@@ -537,14 +598,15 @@ template <int NT>
 void launch_bwd_rows(const float* z, int BH, int s, int N, int R, int CH, const float* g, int group, long long sb,
                      long long sp, long long sn, float gscale, float* ws, hipStream_t st) {
   const size_t lds = bwd_rows_lds(s, N, R, CH);
+  const int share = sb == 0 ? BH : group;   // heads reading the same gradient rows
   hipLaunchKernelGGL((capture_bwd_rows_kernel<NT>), dim3(BH * R), dim3(kBwdThreads), lds, st, z, BH, s, N, R, CH, g,
-                     group, sb, sp, sn, gscale, ws);
+                     group, sb, sp, sn, gscale, share, ws);
 }
 
 int nt_for(int N);
 size_t bwd_rows_lds(int s, int N, int R, int CH) {
   const size_t np = (size_t)nt_for(N) * kBwdThreads;
-  return (2 * s * np + (size_t)CH * (np + 1) + (size_t)R * (kWin + 8)) * sizeof(float);
+  return (s * np + (size_t)CH * (np + 1) + (size_t)R * 5) * sizeof(float);
 }
 
 int nq_for(int N) {  // float4 quads per lane for the forward
@@ -560,34 +622,16 @@ int nt_for(int N) {  // tokens per thread for the backward
   return -1;
 }
 
-// host mirror of bicubic_taps (first/last tap of a pixel) to size the adjoint chunks
-void host_taps(int dst, int n_in, int n_out, int& lo, int& hi) {
-  const float scale = (float)n_in / (float)n_out;
-  const float src = scale * ((float)dst + 0.5f) - 0.5f;
-  const int i0 = (int)floorf(src);
-  lo = std::min(std::max(i0 - 1, 0), n_in - 1);
-  hi = std::min(std::max(i0 + 2, 0), n_in - 1);
-}
-
-// chunk of output pixels for the backward: taps of every chunk must fit the kWin window and
-// the LDS footprint one CU; multiples of 4 that divide R come first (they enable the
-// prefetched float4 gradient path), then any size.
-bool chunk_ok(int ch, int s, int N, int R) {
-  if (bwd_rows_lds(s, N, R, ch) > 160 * 1024) return false;
-  for (int x0 = 0; x0 < R; x0 += ch) {
-    int lo, hi, l2, h2;
-    host_taps(x0, s, R, lo, hi);
-    host_taps(std::min(x0 + ch, R) - 1, s, R, l2, h2);
-    if (h2 - lo >= kWin) return false;
-  }
-  return true;
-}
-
+// chunk of output pixels for the backward: the largest multiple of 4 dividing R (enables the
+// prefetched float4 gradient path) with which two blocks share a CU, else the largest that
+// fits one CU's LDS.
 int pick_chunk(int s, int N, int R) {
-  for (int ch = 16; ch >= 4; ch -= 4)
-    if (R % ch == 0 && chunk_ok(ch, s, N, R)) return ch;
-  for (int ch = 16; ch >= 1; --ch)
-    if (chunk_ok(ch, s, N, R)) return ch;
+  for (size_t budget : {size_t(80) * 1024, size_t(160) * 1024}) {
+    for (int ch = 16; ch >= 4; ch -= 4)
+      if (R % ch == 0 && bwd_rows_lds(s, N, R, ch) <= budget) return ch;
+    for (int ch = 16; ch >= 1; --ch)
+      if (bwd_rows_lds(s, N, R, ch) <= budget) return ch;
+  }
   return 1;
 }
 
@@ -625,7 +669,7 @@ extern "C" int skp_capture_bwd(const float* z_low, int BH, int s, int N, int R, 
   else launch_bwd_rows<2>(z_low, BH, s, N, R, CH, dattn, group, sb, sp, sn, gscale, workspace, st);
   SKP_LAUNCH_CHECK();
   const int chunks = (s * N + kColChunk - 1) / kColChunk;
-  hipLaunchKernelGGL(capture_bwd_cols_kernel, dim3(BH * s, chunks), dim3(kThreads), 0, st, workspace, BH, s, N, R,
+  hipLaunchKernelGGL(capture_bwd_cols_kernel, dim3(BH * ((s + kColRows - 1) / kColRows), chunks), dim3(kThreads), 0, st, workspace, BH, s, N, R,
                      dz_low);
   SKP_LAUNCH_CHECK();
   return SKP_OK;

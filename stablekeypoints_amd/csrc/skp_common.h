@@ -34,15 +34,32 @@ void set_error(const std::string& msg);
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ------------------------------------------------------------------ wave reductions (64 lanes)
+// Full-wave float reductions without LDS: two quad_perm DPP steps and the half-row / row
+// mirrors reduce each 16-lane row, then v_permlane16_swap / v_permlane32_swap (gfx950) exchange
+// rows.  Every lane ends with the same bits (each step combines the same two partials).
+template <int CTRL>
+__device__ __forceinline__ float dpp_read(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+template <class Op>
+__device__ __forceinline__ float wave_reduce(float v, Op op) {
+  v = op(v, dpp_read<0xB1>(v));    // quad_perm [1,0,3,2]
+  v = op(v, dpp_read<0x4E>(v));    // quad_perm [2,3,0,1]
+  v = op(v, dpp_read<0x141>(v));   // row_half_mirror
+  v = op(v, dpp_read<0x140>(v));   // row_mirror
+  float w = v;
+  // the swaps read registers a VALU just wrote: 2 wait states inside the asm (s_nop 1)
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(v), "+v"(w));
+  v = op(v, w);
+  w = v;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(v), "+v"(w));
+  return op(v, w);
+}
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  return wave_reduce(v, [](float a, float b) { return fmaxf(a, b); });
 }
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  return wave_reduce(v, [](float a, float b) { return a + b; });
 }
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -121,8 +138,9 @@ __device__ __forceinline__ float block_max(float v, float* sf) {
 // torch upsample_bicubic2d, align_corners=False: src = (dst+0.5)·in/out − 0.5 (unclamped),
 // taps floor(src)−1..+2 clamped to [0, in−1], Keys A = −0.75.
 struct Taps4 {
-  int i[4];
+  int i[4];     // tap rows/columns, clamped to [0, n_in - 1]
   float w[4];
+  int lo;       // first tap before clamping (floor(src) - 1, in [-2, n_in - 2])
 };
 
 __device__ __forceinline__ float cubic1(float x) {  // |x| <= 1
@@ -147,6 +165,7 @@ __device__ __forceinline__ Taps4 bicubic_taps(int dst, int n_in, int n_out) {
   r.w[3] = cubic2(2.0f - t);
 #pragma unroll
   for (int k = 0; k < 4; ++k) r.i[k] = min(max(i0 - 1 + k, 0), n_in - 1);
+  r.lo = i0 - 1;
   return r;
 }
 

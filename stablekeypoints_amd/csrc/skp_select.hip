@@ -13,8 +13,26 @@ using namespace skp;
 
 namespace {
 
-constexpr int kThreads = 256;
+constexpr int kThreads = 256;      // elementwise kernels
+constexpr int kRowThreads = 1024;  // one workgroup per map row (16 waves: a 128² row is 4 float4 per thread)
 constexpr int kMaxSubjects = 16;
+
+// Visit a row's elements in increasing index order per thread (16-B loads when aligned).
+template <class F>
+__device__ __forceinline__ void for_row(const float* __restrict__ m, int HW, F&& f) {
+  if ((HW & 3) == 0 && (reinterpret_cast<uintptr_t>(m) & 15) == 0) {
+    const float4* m4 = reinterpret_cast<const float4*>(m);
+    for (int q = threadIdx.x; q < (HW >> 2); q += blockDim.x) {
+      const float4 v = m4[q];
+      f(4 * q, v.x);
+      f(4 * q + 1, v.y);
+      f(4 * q + 2, v.z);
+      f(4 * q + 3, v.w);
+    }
+  } else {
+    for (int e = threadIdx.x; e < HW; e += blockDim.x) f(e, m[e]);
+  }
+}
 
 // Scan one row for its argmax (torch order).  Applies the cumulative radius masks of
 // previously found points (eval.mask_radius multiplies by 0/1, so NaN/inf survive as NaN).
@@ -22,9 +40,7 @@ __device__ void row_argmax_masked(const float* __restrict__ m, int h, int w, con
                                   int nmask, float radius2, float& best, int& bi, float* sv, int* si) {
   best = -INFINITY;
   bi = 0x7fffffff;
-  const int HW = h * w;
-  for (int e = threadIdx.x; e < HW; e += kThreads) {
-    float v = m[e];
+  for_row(m, h * w, [&](int e, float v) {
     if (nmask) {
       const float x = (float)(e % w), y = (float)(e / w);
       for (int q = 0; q < nmask; ++q) {
@@ -33,15 +49,15 @@ __device__ void row_argmax_masked(const float* __restrict__ m, int h, int w, con
       }
     }
     if (argmax_better(v, e, best, bi)) { best = v; bi = e; }
-  }
+  });
   block_argmax(best, bi, sv, si);
 }
 
-__global__ __launch_bounds__(kThreads) void argmax_kernel(const float* __restrict__ maps, int T, int h, int w,
+__global__ __launch_bounds__(kRowThreads) void argmax_kernel(const float* __restrict__ maps, int T, int h, int w,
                                                           const long long* __restrict__ rows, float* __restrict__ pos,
                                                           long long* __restrict__ idx) {
-  __shared__ float sv[kThreads / 64];
-  __shared__ int si[kThreads / 64];
+  __shared__ float sv[kRowThreads / 64];
+  __shared__ int si[kRowThreads / 64];
   const long long row = rows ? rows[blockIdx.x] : blockIdx.x;
   if (row < 0 || row >= T) {  // invalid row id: poison the output instead of reading out of bounds
     if (threadIdx.x == 0) {
@@ -62,11 +78,11 @@ __global__ __launch_bounds__(kThreads) void argmax_kernel(const float* __restric
   }
 }
 
-__global__ __launch_bounds__(kThreads) void kmax_kernel(const float* __restrict__ maps, int T, int h, int w, int num,
+__global__ __launch_bounds__(kRowThreads) void kmax_kernel(const float* __restrict__ maps, int T, int h, int w, int num,
                                                         float radius2, float* __restrict__ pos,
                                                         float* __restrict__ masked) {
-  __shared__ float sv[kThreads / 64];
-  __shared__ int si[kThreads / 64];
+  __shared__ float sv[kRowThreads / 64];
+  __shared__ int si[kRowThreads / 64];
   __shared__ float pr[kMaxSubjects], pc[kMaxSubjects];
   const int row = blockIdx.x;
   const float* m = maps + (size_t)row * h * w;
@@ -84,7 +100,7 @@ __global__ __launch_bounds__(kThreads) void kmax_kernel(const float* __restrict_
   }
   if (masked) {
     const int HW = h * w;
-    for (int e = threadIdx.x; e < HW; e += kThreads) {
+    for (int e = threadIdx.x; e < HW; e += blockDim.x) {
       float v = m[e];
       const float x = (float)(e % w), y = (float)(e / w);
       for (int q = 0; q < num; ++q) {
@@ -106,11 +122,11 @@ __global__ void mask_radius_kernel(const float* __restrict__ maps, int T, int h,
   out[e] = maps[e] * ((dx * dx + dy * dy > radius2) ? 1.0f : 0.0f);
 }
 
-__global__ __launch_bounds__(kThreads) void weighted_avg_kernel(float* __restrict__ maps, int h, int w,
+__global__ __launch_bounds__(kRowThreads) void weighted_avg_kernel(float* __restrict__ maps, int h, int w,
                                                                 float distance, int mutate, float* __restrict__ pos) {
-  __shared__ float sv[kThreads / 64];
-  __shared__ int si[kThreads / 64];
-  __shared__ double sd[kThreads / 64];
+  __shared__ float sv[kRowThreads / 64];
+  __shared__ int si[kRowThreads / 64];
+  __shared__ double sd[kRowThreads / 64];
   float* m = maps + (size_t)blockIdx.x * h * w;
   float best;
   int bi;
@@ -119,7 +135,7 @@ __global__ __launch_bounds__(kThreads) void weighted_avg_kernel(float* __restric
   const bool cut = distance >= 0.0f;
   const int HW = h * w;
   double tot = 0.0;
-  for (int e = threadIdx.x; e < HW; e += kThreads) {
+  for (int e = threadIdx.x; e < HW; e += blockDim.x) {
     const float x = (float)(e / w), y = (float)(e % w);
     const float dx = x - r, dy = y - c;
     const bool drop = cut && (sqrt_rn(dx * dx + dy * dy) > distance);
@@ -133,7 +149,7 @@ __global__ __launch_bounds__(kThreads) void weighted_avg_kernel(float* __restric
   tot = block_sum(tot, sd);
   const float denom = (float)tot + 1e-6f;
   double xs = 0.0, ys = 0.0;
-  for (int e = threadIdx.x; e < HW; e += kThreads) {
+  for (int e = threadIdx.x; e < HW; e += blockDim.x) {
     const float x = (float)(e / w), y = (float)(e % w);
     const float dx = x - r, dy = y - c;
     const bool drop = cut && (sqrt_rn(dx * dx + dy * dy) > distance);
@@ -177,13 +193,13 @@ __global__ void gaussian_target_kernel(const float* __restrict__ pos, int num, i
 }
 
 // KL(target ‖ softmax(map + eps)) per token (ptp_utils.py:97-108)
-__global__ __launch_bounds__(kThreads) void kl_gauss_kernel(const float* __restrict__ maps, int h, int w, int num,
+__global__ __launch_bounds__(kRowThreads) void kl_gauss_kernel(const float* __restrict__ maps, int h, int w, int num,
                                                             float radius2, float two_sig2, float eps,
                                                             double* __restrict__ kl) {
-  __shared__ float sv[kThreads / 64];
-  __shared__ int si[kThreads / 64];
-  __shared__ double sd[kThreads / 64];
-  __shared__ float sf[kThreads / 64];
+  __shared__ float sv[kRowThreads / 64];
+  __shared__ int si[kRowThreads / 64];
+  __shared__ double sd[kRowThreads / 64];
+  __shared__ float sf[kRowThreads / 64];
   __shared__ float pr[kMaxSubjects], pc[kMaxSubjects];
   const float* m = maps + (size_t)blockIdx.x * h * w;
   for (int q = 0; q < num; ++q) {
@@ -204,51 +220,51 @@ __global__ __launch_bounds__(kThreads) void kl_gauss_kernel(const float* __restr
   }
   const int HW = h * w;
   float mx = -INFINITY;
-  for (int e = threadIdx.x; e < HW; e += kThreads) mx = fmaxf(mx, m[e] + eps);
+  for_row(m, HW, [&](int, float v) { mx = fmaxf(mx, v + eps); });
   mx = block_max(mx, sf);
   double se = 0.0, sg = 0.0;
-  for (int e = threadIdx.x; e < HW; e += kThreads) {
-    se += (double)expf((m[e] + eps) - mx);
+  for_row(m, HW, [&](int e, float v) {
+    se += (double)expf((v + eps) - mx);
     sg += (double)(gauss_at(e / w, e % w, p0, p1, num, two_sig2) + eps);
-  }
+  });
   se = block_sum(se, sd);
   sg = block_sum(sg, sd);
   const float sef = (float)se, sgf = (float)sg;
   double acc = 0.0;
-  for (int e = threadIdx.x; e < HW; e += kThreads) {
-    const float P = expf((m[e] + eps) - mx) / sef;
+  for_row(m, HW, [&](int e, float v) {
+    const float P = expf((v + eps) - mx) / sef;
     const float tg = (gauss_at(e / w, e % w, p0, p1, num, two_sig2) + eps) / sgf;
     acc += (double)tg * ((double)logf(tg) - (double)logf(P));
-  }
+  });
   acc = block_sum(acc, sd);
   if (threadIdx.x == 0) kl[blockIdx.x] = acc;
 }
 
 // entropy of softmax(map) (ptp_utils.py:179-182; torch Categorical renormalises and clamps)
-__global__ __launch_bounds__(kThreads) void entropy_kernel(const float* __restrict__ maps, int h, int w,
+__global__ __launch_bounds__(kRowThreads) void entropy_kernel(const float* __restrict__ maps, int h, int w,
                                                            double* __restrict__ ent) {
-  __shared__ double sd[kThreads / 64];
-  __shared__ float sf[kThreads / 64];
+  __shared__ double sd[kRowThreads / 64];
+  __shared__ float sf[kRowThreads / 64];
   const float* m = maps + (size_t)blockIdx.x * h * w;
   const int HW = h * w;
   float mx = -INFINITY;
-  for (int e = threadIdx.x; e < HW; e += kThreads) mx = fmaxf(mx, m[e]);
+  for_row(m, HW, [&](int, float v) { mx = fmaxf(mx, v); });
   mx = block_max(mx, sf);
   double se = 0.0;
-  for (int e = threadIdx.x; e < HW; e += kThreads) se += (double)expf(m[e] - mx);
+  for_row(m, HW, [&](int, float v) { se += (double)expf(v - mx); });
   se = block_sum(se, sd);
   const float sef = (float)se;
   double ps = 0.0;
-  for (int e = threadIdx.x; e < HW; e += kThreads) ps += (double)(expf(m[e] - mx) / sef);
+  for_row(m, HW, [&](int, float v) { ps += (double)(expf(v - mx) / sef); });
   ps = block_sum(ps, sd);
   const float psf = (float)ps;
   const float lo = 1.1920928955078125e-07f, hi = 1.0f - 1.1920928955078125e-07f;
   double acc = 0.0;
-  for (int e = threadIdx.x; e < HW; e += kThreads) {
-    const float p = (expf(m[e] - mx) / sef) / psf;
+  for_row(m, HW, [&](int, float v) {
+    const float p = (expf(v - mx) / sef) / psf;
     const float pcl = fminf(fmaxf(p, lo), hi);
     acc += (double)p * (double)logf(pcl);
-  }
+  });
   acc = block_sum(acc, sd);
   if (threadIdx.x == 0) ent[blockIdx.x] = -acc;
 }
@@ -367,12 +383,12 @@ __global__ __launch_bounds__(64) void fps_kernel(const float* __restrict__ cpos,
 }
 
 // ------------------------------------------------------------------------------------ losses
-__global__ __launch_bounds__(kThreads) void sharpen_fwd_kernel(const float* __restrict__ A, int T, int h, int w,
+__global__ __launch_bounds__(kRowThreads) void sharpen_fwd_kernel(const float* __restrict__ A, int T, int h, int w,
                                                                int num, float radius2, float two_sig2,
                                                                float* __restrict__ pos, double* __restrict__ partial) {
-  __shared__ float sv[kThreads / 64];
-  __shared__ int si[kThreads / 64];
-  __shared__ double sd[kThreads / 64];
+  __shared__ float sv[kRowThreads / 64];
+  __shared__ int si[kRowThreads / 64];
+  __shared__ double sd[kRowThreads / 64];
   __shared__ float pr[kMaxSubjects], pc[kMaxSubjects];
   const int row = blockIdx.x;
   const float* m = A + (size_t)row * h * w;
@@ -395,11 +411,10 @@ __global__ __launch_bounds__(kThreads) void sharpen_fwd_kernel(const float* __re
     p1[q] = (pc[q] / (float)w) * (float)h;
   }
   double acc = 0.0;
-  const int HW = h * w;
-  for (int e = threadIdx.x; e < HW; e += kThreads) {
-    const float d = m[e] - gauss_at(e / w, e % w, p0, p1, num, two_sig2);
+  for_row(m, h * w, [&](int e, float v) {
+    const float d = v - gauss_at(e / w, e % w, p0, p1, num, two_sig2);
     acc += (double)(d * d);
-  }
+  });
   acc = block_sum(acc, sd);
   if (threadIdx.x == 0) partial[row] = acc;
 }
@@ -437,7 +452,7 @@ extern "C" int skp_argmax2d(const float* maps, int T, int h, int w, const long l
   SKP_CHECK_ARG(T > 0 && h > 0 && w > 0, "non-positive shape");
   const int nr = rows ? n_rows : T;
   SKP_CHECK_ARG(nr > 0, "no rows");
-  hipLaunchKernelGGL(argmax_kernel, dim3(nr), dim3(kThreads), 0, as_stream(stream), maps, T, h, w, rows, pos, idx);
+  hipLaunchKernelGGL(argmax_kernel, dim3(nr), dim3(kRowThreads), 0, as_stream(stream), maps, T, h, w, rows, pos, idx);
   SKP_LAUNCH_CHECK();
   return SKP_OK;
 }
@@ -447,7 +462,7 @@ extern "C" int skp_k_max_pixels(const float* maps, int T, int h, int w, int num,
   SKP_CHECK_ARG(maps && pos, "null pointer");
   SKP_CHECK_ARG(T > 0 && h > 0 && w > 0, "non-positive shape");
   SKP_CHECK_ARG(num >= 1 && num <= kMaxSubjects, "num out of range [1, 16]");
-  hipLaunchKernelGGL(kmax_kernel, dim3(T), dim3(kThreads), 0, as_stream(stream), maps, T, h, w, num, radius2, pos,
+  hipLaunchKernelGGL(kmax_kernel, dim3(T), dim3(kRowThreads), 0, as_stream(stream), maps, T, h, w, num, radius2, pos,
                      masked);
   SKP_LAUNCH_CHECK();
   return SKP_OK;
@@ -468,7 +483,7 @@ extern "C" int skp_weighted_avg(float* maps, int T, int h, int w, float distance
                                 void* stream) {
   SKP_CHECK_ARG(maps && pos, "null pointer");
   SKP_CHECK_ARG(T > 0 && h > 0 && w > 0, "non-positive shape");
-  hipLaunchKernelGGL(weighted_avg_kernel, dim3(T), dim3(kThreads), 0, as_stream(stream), maps, h, w, distance, mutate,
+  hipLaunchKernelGGL(weighted_avg_kernel, dim3(T), dim3(kRowThreads), 0, as_stream(stream), maps, h, w, distance, mutate,
                      pos);
   SKP_LAUNCH_CHECK();
   return SKP_OK;
@@ -507,7 +522,7 @@ extern "C" int skp_topk_gaussian(const float* maps, int T, int h, int w, int top
   const float radius2 = (float)(rad * rad);
   const float two_sig2 = (float)(2.0 * (double)sigma * (double)sigma);
   hipStream_t st = as_stream(stream);
-  hipLaunchKernelGGL(kl_gauss_kernel, dim3(T), dim3(kThreads), 0, st, maps, h, w, num_subjects, radius2, two_sig2,
+  hipLaunchKernelGGL(kl_gauss_kernel, dim3(T), dim3(kRowThreads), 0, st, maps, h, w, num_subjects, radius2, two_sig2,
                      epsilon, keys);
   SKP_LAUNCH_CHECK();
   if (top_k == 0) return SKP_OK;
@@ -521,7 +536,7 @@ extern "C" int skp_entropy_sort(const float* maps, int T, int h, int w, int top_
   SKP_CHECK_ARG(top_k >= 0 && top_k <= T, "top_k out of range");
   double* keys = ent ? ent : reinterpret_cast<double*>(workspace);
   hipStream_t st = as_stream(stream);
-  hipLaunchKernelGGL(entropy_kernel, dim3(T), dim3(kThreads), 0, st, maps, h, w, keys);
+  hipLaunchKernelGGL(entropy_kernel, dim3(T), dim3(kRowThreads), 0, st, maps, h, w, keys);
   SKP_LAUNCH_CHECK();
   if (top_k == 0) return SKP_OK;
   return launch_sort(keys, T, top_k, out, st);
@@ -536,7 +551,7 @@ extern "C" int skp_fps(const float* maps, int T, int h, int w, const long long* 
   SKP_CHECK_ARG(top_k >= 2 && top_k <= 1024, "top_k out of range [2, 1024]");
   hipStream_t st = as_stream(stream);
   float* cpos = reinterpret_cast<float*>(workspace);
-  hipLaunchKernelGGL(argmax_kernel, dim3(n_cand), dim3(kThreads), 0, st, maps, T, h, w, cand, cpos,
+  hipLaunchKernelGGL(argmax_kernel, dim3(n_cand), dim3(kRowThreads), 0, st, maps, T, h, w, cand, cpos,
                      (long long*)nullptr);
   SKP_LAUNCH_CHECK();
   const size_t lds = (size_t)n_cand * 8 + (size_t)n_cand * 8 + (size_t)top_k * 8 + (size_t)top_k * 8;
@@ -555,7 +570,7 @@ extern "C" int skp_sharpen_fwd(const float* A, int T, int h, int w, float sigma,
   const float radius2 = (float)(rad * rad);
   const float two_sig2 = (float)(2.0 * (double)sigma * (double)sigma);
   hipStream_t st = as_stream(stream);
-  hipLaunchKernelGGL(sharpen_fwd_kernel, dim3(T), dim3(kThreads), 0, st, A, T, h, w, num_subjects, radius2, two_sig2,
+  hipLaunchKernelGGL(sharpen_fwd_kernel, dim3(T), dim3(kRowThreads), 0, st, A, T, h, w, num_subjects, radius2, two_sig2,
                      pos, partial);
   SKP_LAUNCH_CHECK();
   hipLaunchKernelGGL(finalize_mean_kernel, dim3(1), dim3(kThreads), 0, st, partial, T, (double)T * h * w, loss);

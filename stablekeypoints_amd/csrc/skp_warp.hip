@@ -79,17 +79,18 @@ __global__ void warp_bwd_kernel(const float* __restrict__ gout, int B, int C, in
 }
 
 constexpr int kThreads = 256;
+constexpr int kRowThreads = 1024;   // one workgroup per map row
 
-__global__ __launch_bounds__(kThreads) void equiv_fwd_kernel(const float* __restrict__ A, const float* __restrict__ At,
+__global__ __launch_bounds__(kRowThreads) void equiv_fwd_kernel(const float* __restrict__ A, const float* __restrict__ At,
                                                              int h, int w, const float* __restrict__ th,
                                                              double* __restrict__ partial) {
-  __shared__ double sd[kThreads / 64];
+  __shared__ double sd[kRowThreads / 64];
   const int t = blockIdx.x;
   const size_t HW = (size_t)h * w;
   const float* a = A + t * HW;
   const float* at = At + t * HW;
   double acc = 0.0;
-  for (int p = threadIdx.x; p < (int)HW; p += kThreads) {
+  for (int p = threadIdx.x; p < (int)HW; p += kRowThreads) {
     const float d = a[p] - sample(at, grid_point(th, p / w, p % w, h, w), h, w);
     acc += (double)(d * d);
   }
@@ -152,7 +153,7 @@ extern "C" int skp_equiv_fwd(const float* A, const float* At, int T, int h, int 
   SKP_CHECK_ARG(A && At && theta_inv && partial && loss, "null pointer");
   SKP_CHECK_ARG(T > 0 && h > 0 && w > 0, "non-positive shape");
   hipStream_t st = as_stream(stream);
-  hipLaunchKernelGGL(equiv_fwd_kernel, dim3(T), dim3(kThreads), 0, st, A, At, h, w, theta_inv, partial);
+  hipLaunchKernelGGL(equiv_fwd_kernel, dim3(T), dim3(kRowThreads), 0, st, A, At, h, w, theta_inv, partial);
   SKP_LAUNCH_CHECK();
   hipLaunchKernelGGL(finalize_mean_kernel, dim3(1), dim3(kThreads), 0, st, partial, T, (double)T * h * w, loss);
   SKP_LAUNCH_CHECK();

@@ -40,8 +40,12 @@ def main():
     layers = [ops.capture_attn(zs[16] * (1 + 0.1 * i), 16, R) for i in range(3)] + [attn[32]]
     dmap = torch.randn(N, R * R, device=dev, generator=g)
     gb = dmap.t().unsqueeze(0).expand(H, R * R, N)
+    # the bench's backward: 2 images x H heads, per-image token-major map gradient (CaptureMaps)
+    zb2 = {s: torch.randn(2 * H, s * s, N, device=dev, generator=g) * 2 for s in (16, 32)}
+    gmap = torch.randn(2, N, R, R, device=dev, generator=g)
+    bstr = (N * R * R, 1, R * R)
     res = {}
-    todo = args.only.split(",") if args.only else ["fwd16", "fwd32", "agg", "bwd16", "bwd32", "bwd16_dense"]
+    todo = args.only.split(",") if args.only else ["fwd16", "fwd32", "agg", "bwd16", "bwd32", "bwd16b2", "bwd32b2", "bwd16_dense"]
     for name in todo:
         if name == "fwd16":
             res[name] = timed(lambda: ops.capture_attn(zs[16], 16, R), args.iters)
@@ -53,6 +57,9 @@ def main():
             res[name] = timed(lambda: ops.capture_bwd(zs[16], 16, R, gb), args.iters)
         elif name == "bwd32":
             res[name] = timed(lambda: ops.capture_bwd(zs[32], 32, R, gb), args.iters)
+        elif name in ("bwd16b2", "bwd32b2"):
+            sz = 16 if name == "bwd16b2" else 32
+            res[name] = timed(lambda: ops.capture_bwd(zb2[sz], sz, R, gmap, 0.03125, H, bstr), args.iters)
         elif name == "sum1g":   # read-bandwidth reference: torch reduction over a fresh 1 GiB tensor
             big = torch.empty(256 * 1024 * 1024, device=dev).normal_()
             res[name] = timed(lambda: big.sum(), args.iters)
@@ -76,6 +83,19 @@ def main():
             for nm, t in (("fwd", t_f), ("dq", t_q), ("dk", t_k), ("torch_fwd", t_ref)):
                 res[f"{name}_{nm}"] = t
                 res[f"{name}_{nm}_TFs"] = fl / (t * 1e-3) / 1e12 / 1e3
+        elif name in ("kl", "argmax", "fps", "sharp", "equiv", "entropy"):
+            maps = torch.rand(N, R, R, device=dev, generator=g) ** 8   # peaked, attention-map-like
+            A10 = maps[:10].contiguous()
+            At10 = maps[10:20].contiguous()
+            th = torch.tensor([[0.9, -0.1, 0.05], [0.1, 0.9, -0.02]], device=dev)
+            cand = torch.arange(25, device=dev)
+            fn = {"kl": lambda: ops.find_top_k_gaussian(maps, 25, sigma=2.0),
+                  "entropy": lambda: ops.entropy_sort(maps, 25),
+                  "argmax": lambda: ops.find_max_pixel(maps),
+                  "fps": lambda: ops.furthest_point_sampling(maps, 10, cand),
+                  "sharp": lambda: ops.sharpening_loss(A10, 2.0),
+                  "equiv": lambda: ops.equivariance_loss_single(A10, At10, th)}[name]
+            res[name] = timed(fn, args.iters)
         elif name == "bwd16_dense":
             res[name] = timed(lambda: ops.capture_bwd(zs[16], 16, R, attn[16]), args.iters)
     agg_bytes = (4 * H * R * R * N + N * R * R) * 4
