@@ -3,9 +3,12 @@
 ``find_max_pixel``, ``find_k_max_pixels``, ``mask_radius`` and
 ``pixel_from_weighted_avg`` (``eval.py:39-155``) run as HIP kernels with the
 reference's semantics (first-occurrence argmax, NaN is max, in-place mutation in
-``pixel_from_weighted_avg``).  Dataset metrics (``evaluate``, ``eval.py:374-539``)
-are outside the hot path and not part of this package.
+``pixel_from_weighted_avg``).  ``run_image_with_context_augmented`` (``:197-355``) is the
+test-time-augmentation average on the same kernels; ``evaluate`` (``:374-539``) regresses
+keypoints from it and scores them with the reference's five metrics (``keypoint_error``).
 """
+import os
+
 import torch
 
 from . import ops, ptp_utils
@@ -40,29 +43,135 @@ def run_image_with_context_augmented(ldm, image, context, indices, device="cuda"
                                      controllers=None, num_gpus=1, save_folder="outputs", upscale_size=512):
     """eval.py:197-355 (hot part 221-266, 327-330): TTA-averaged maps of the chosen tokens.
 
-    ``image`` is (3, H, W) in [0, 1].  Each iteration warps ``num_gpus`` copies
-    (on this process: one copy per iteration), captures, gathers ``indices`` and
-    bilinearly upsamples to ``upscale_size`` (collect_maps), inverse-warps maps and
-    ones and accumulates; returns sum / count with NaN -> 0.
+    ``image`` is (3, H, W) in [0, 1] (torch or numpy HWC).  Each of the
+    ``augmentation_iterations // num_gpus`` iterations draws ``num_gpus`` thetas from the CPU
+    generator in the reference's order (one per replica, eval.py:238-242).  Replica r's warped
+    copy is captured (``indices`` gathered, bilinear to ``upscale_size``: collect_maps), then its
+    map and a ones map are inverse-warped and summed.  Returns Σmaps / Σones with NaN → 0.
+
+    Replicas: with torch.distributed initialised and ``num_gpus`` equal to the world size,
+    rank r runs replica r of every iteration and the two (n, S, S) sums are all-reduced (SUM)
+    once at the end; every rank must hold the same CPU RNG state (same seed) so that all draw
+    the same thetas.  In one process, the ``num_gpus`` copies run as one batched capture.
     """
     if visualize:
         raise NotImplementedError("visualisation is outside the hot path")
+    from .optimize import _world
     img = image if torch.is_tensor(image) else torch.as_tensor(image)
     if img.dim() == 3 and img.shape[-1] == 3 and img.shape[0] != 3:
         img = img.permute(2, 0, 1)
     img = img.to(device, torch.float32)
+    world, rank = _world()
+    if world > 1 and num_gpus != world:
+        raise ValueError(f"num_gpus={num_gpus} must equal the world size {world} (one replica per rank)")
     n = len(indices)
     num_samples = torch.zeros(n, upscale_size, upscale_size, device=device)
     sum_samples = torch.zeros(n, upscale_size, upscale_size, device=device)
     T = RandomAffineWithInverse(degrees=augment_degrees, scale=augment_scale, translate=augment_translate)
     for _ in range(augmentation_iterations // num_gpus):
-        aug = T(img[None])
-        maps = ptp_utils.run_and_find_attn(ldm, aug, context, layers=layers, noise_level=noise_level,
-                                           from_where=from_where, upsample_res=upscale_size, device=device,
-                                           controllers=controllers, indices=indices)
-        maps = torch.stack(maps)          # (1, n, S, S) on this rank
+        theta = T.draw_theta(num_gpus)                        # every rank draws all replicas' thetas
+        mine = slice(rank, rank + 1) if world > 1 else slice(0, num_gpus)
+        aug = T(img[None].expand(theta[mine].shape[0], -1, -1, -1), theta=theta[mine])
+        if aug.shape[0] == 1:
+            maps = torch.stack(ptp_utils.run_and_find_attn(
+                ldm, aug, context, layers=layers, noise_level=noise_level, from_where=from_where,
+                upsample_res=upscale_size, device=device, controllers=controllers, indices=indices))
+        else:
+            per = ptp_utils.run_and_find_attn_per_image(ldm, aug, context, noise_level=noise_level, device=device,
+                                                        layers=layers, upsample_res=upscale_size, indices=indices,
+                                                        controllers=controllers)
+            maps = torch.stack([m for ctl_maps in per for m in ctl_maps])
         num_samples += T.inverse(torch.ones_like(maps)).sum(dim=0)
         sum_samples += T.inverse(maps).sum(dim=0)
+    if world > 1:
+        import torch.distributed as dist
+        dist.all_reduce(num_samples)
+        dist.all_reduce(sum_samples)
     attention_maps = sum_samples / num_samples
     attention_maps[attention_maps != attention_maps] = 0
     return attention_maps
+
+
+def swap_points(points):
+    """eval.py:358-370: left/right keypoint permutation of Human3.6M (B, K, D)."""
+    pairs = [(1, 6), (2, 7), (3, 8), (4, 9), (5, 10), (17, 25), (18, 26), (19, 27), (20, 28), (21, 28), (22, 30),
+             (23, 31)]
+    perm = list(range(points.shape[1]))
+    for a, b in pairs:
+        perm[a], perm[b] = b, a
+    return points[:, perm, :]
+
+
+METRICS = ("inter_eye_distance", "visible", "mean_average_error", "pck", "orientation_invariant")
+
+
+def keypoint_error(highest_indices, regressor, gt_kpts, evaluation_method="inter_eye_distance", visible=None):
+    """One image's error (eval.py:467-513): regress (row, col)/512 maxima of the chosen tokens
+    to keypoints, ``((p − 0.5) @ W) + 0.5``, and score them against ``gt_kpts`` (K, 2).
+
+    inter_eye_distance: mean L2 / |gt₀ − gt₁|; visible: Σ L2·v / Σ v; mean_average_error:
+    Σ L2·v at 256 px scale; pck: fraction within 6 px at 256 px scale; orientation_invariant:
+    min over the left/right swap of the mean L2, × 128.
+    """
+    if evaluation_method not in METRICS:
+        raise ValueError(f"evaluation_method must be one of {METRICS}")
+    est = ((highest_indices.reshape(1, -1) - 0.5) @ regressor) + 0.5
+    est = est.reshape(-1, 2)
+    gt = gt_kpts.to(est.device, est.dtype)
+    if evaluation_method in ("mean_average_error", "pck"):
+        est = est * 256
+        gt = gt * 256
+    l2 = (est - gt).norm(dim=-1)
+    if evaluation_method == "inter_eye_distance":
+        eye = torch.sqrt(torch.sum((gt[0] - gt[1]) ** 2, dim=-1))
+        return torch.mean(l2 / eye)
+    if evaluation_method in ("visible", "mean_average_error"):
+        vis = torch.ones_like(l2) if visible is None else visible.to(l2.device, l2.dtype)
+        err = (l2 * vis).sum()
+        return err / vis.sum() if evaluation_method == "visible" else err
+    if evaluation_method == "pck":
+        return (l2 < 6).float().mean()
+    err = l2.mean()
+    swapped = (swap_points(est[None])[0] - gt).norm(dim=-1).mean()
+    return torch.minimum(err, swapped) * 128
+
+
+@torch.no_grad()
+def evaluate(ldm, context, indices, regressor, device="cuda", from_where=("down_cross", "mid_cross", "up_cross"),
+             upsample_res=32, layers=(0, 1, 2, 3, 4, 5), noise_level=-1, num_tokens=1000, augment_degrees=30,
+             augment_scale=(0.9, 1.1), augment_translate=(0.1, 0.1), augmentation_iterations=20, dataset_loc="~",
+             save_folder="outputs", wandb_log=False, visualize=False, dataset_name="celeba_aligned",
+             evaluation_method="inter_eye_distance", controllers=None, num_gpus=1, max_loc_strategy="argmax",
+             validation=False, dataset=None, upscale_size=512):
+    """eval.py:374-539: per test image (shuffled loader, batch 1) the TTA maps of ``indices``,
+    their maxima / 512, the regressed keypoints and ``keypoint_error``; writes
+    ``all_errors.pt`` (per-image errors) to ``save_folder`` and returns the mean error.
+    ``dataset`` (extra) overrides the lookup; ``visualize``/``wandb_log`` are not supported.
+    """
+    from .datasets import make_dataset
+    if evaluation_method not in METRICS:
+        raise ValueError(f"evaluation_method must be one of {METRICS}")
+    if dataset is None:
+        dataset = make_dataset(dataset_name, dataset_loc, validation=validation, split="test")
+    loader = torch.utils.data.DataLoader(dataset, batch_size=1, shuffle=True, drop_last=True)
+    it = iter(loader)
+    regressor = regressor.to(device, torch.float32)
+    values = []
+    for _ in range(len(dataset)):
+        batch = next(it)
+        maps = run_image_with_context_augmented(
+            ldm, batch["img"][0], context, indices.cpu(), device=device, from_where=from_where, layers=layers,
+            noise_level=noise_level, augmentation_iterations=augmentation_iterations, augment_degrees=augment_degrees,
+            augment_scale=augment_scale, augment_translate=augment_translate, controllers=controllers,
+            num_gpus=num_gpus, save_folder=save_folder, upscale_size=upscale_size)
+        if max_loc_strategy == "argmax":
+            highest = find_max_pixel(maps) / 512.0
+        else:
+            highest = pixel_from_weighted_avg(maps) / 512.0
+        vis = batch["visibility"][0] if "visibility" in batch else None
+        values.append(float(keypoint_error(highest, regressor, batch["kpts"][0], evaluation_method, vis)))
+    os.makedirs(save_folder, exist_ok=True)
+    torch.save(torch.tensor(values), os.path.join(save_folder, "all_errors.pt"))
+    mean = float(torch.tensor(values).mean()) if values else float("nan")
+    print(f"mean distance: {mean}", flush=True)
+    return mean

@@ -1,14 +1,39 @@
-"""Token-index selection over a dataset (mirror of reference ``keypoint_regressor.find_best_indices``).
+"""Token-index selection and keypoint precompute over a dataset (mirror of reference
+``keypoint_regressor.py``).
 
-Only ``find_best_indices`` (``keypoint_regressor.py:16-121``) is on the kernels of this
-package: per image a no-grad capture (``upsample_res`` bilinear maps), top-k candidates
-(Gaussian KL / entropy / consistent) and furthest-point sampling, then the most frequent
-token ids.  The regressor fitting and keypoint precompute stages are outside this path.
+``find_best_indices`` (``keypoint_regressor.py:16-121``): per image a no-grad capture
+(``upsample_res`` bilinear maps), top-k candidates (Gaussian KL / entropy / consistent) and
+furthest-point sampling on the HIP kernels, then the most frequent token ids.
+``precompute_all_keypoints`` (``:124-224``): per image the TTA-averaged maps of the chosen
+tokens (``eval.run_image_with_context_augmented``) and their argmax / soft-argmax / 512.
+``return_regressor`` / ``return_regressor_visible`` / ``return_regressor_human36m``
+(``:227-299``): the least-squares keypoint regressor (host numpy/torch, as in the reference).
+
+Multi-GPU: one process per GPU.  The reference's ``num_gpus`` DataParallel replicas become
+ranks: the data order is drawn once (CPU generator; every rank must be seeded alike) and rank
+r takes replica r's image of every batch (find_best_indices, then an all_gather of the index
+lists) or replica r's augmentations of every image (precompute, via the TTA all-reduce).
 """
+import numpy as np
 import torch
 
 from . import ptp_utils
 from .datasets import make_dataset
+from .eval import find_max_pixel, pixel_from_weighted_avg, run_image_with_context_augmented
+
+
+def _loader(dataset, batch_size):
+    """DataLoader(shuffle=True, drop_last=True) as the reference builds it.  Its shuffle seed
+    comes from the CPU generator, so ranks seeded alike draw the same order (no collective)."""
+    return torch.utils.data.DataLoader(dataset, batch_size=batch_size, shuffle=True, drop_last=True)
+
+
+def _next(state):
+    try:
+        return next(state["it"])
+    except StopIteration:   # keypoint_regressor.py:76-80: restart the loader
+        state["it"] = iter(state["loader"])
+        return next(state["it"])
 
 
 @torch.no_grad()
@@ -16,34 +41,118 @@ def find_best_indices(ldm, context, num_steps=100, device="cuda", noise_level=-1
                       layers=(0, 1, 2, 3, 4, 5), from_where=("down_cross", "mid_cross", "up_cross"), num_tokens=1000,
                       top_k=30, dataset_loc="~", dataset_name="celeba_aligned", min_dist=0.05,
                       furthest_point_num_samples=50, controllers=None, num_gpus=1, top_k_strategy="entropy", sigma=3,
-                      validation=False, num_subjects=1, dataset=None, seed=0):
+                      validation=False, num_subjects=1, dataset=None):
+    """keypoint_regressor.py:16-121.  ``dataset`` (extra) overrides the dataset_name lookup."""
+    from .optimize import _world
+    if top_k_strategy not in ("entropy", "gaussian", "consistent"):
+        raise NotImplementedError(top_k_strategy)
     if dataset is None:
         dataset = make_dataset(dataset_name, dataset_loc, validation=validation)
-    g = torch.Generator().manual_seed(seed)
-    order = torch.randperm(len(dataset), generator=g)
+    world, rank = _world()
+    if world > 1 and num_gpus != world:
+        raise ValueError(f"num_gpus={num_gpus} must equal the world size {world} (one replica per rank)")
+    loader = _loader(dataset, num_gpus)
+    state = {"loader": loader, "it": iter(loader)}
     indices_list = []
-    for it in range(num_steps // num_gpus):
-        image = dataset[int(order[it % len(order)])]["img"][None].to(device)
-        attention_maps = ptp_utils.run_and_find_attn(ldm, image, context, layers=layers, noise_level=noise_level,
-                                                     from_where=from_where, upsample_res=upsample_res,
-                                                     controllers=controllers, device=device)
-        for attention_map in attention_maps:
-            if top_k_strategy == "entropy":
-                cand = ptp_utils.entropy_sort(attention_map, furthest_point_num_samples)
-            elif top_k_strategy == "gaussian":
-                cand = ptp_utils.find_top_k_gaussian(attention_map, furthest_point_num_samples, sigma=sigma,
-                                                     num_subjects=num_subjects)
-            elif top_k_strategy == "consistent":
-                cand = torch.arange(furthest_point_num_samples, device=attention_map.device)
-            else:
-                raise NotImplementedError
-            indices_list.append(ptp_utils.furthest_point_sampling(attention_map, top_k, cand).cpu())
+    for _ in range(num_steps // num_gpus):
+        images = _next(state)["img"]
+        mine = images[rank:rank + 1] if world > 1 else images
+        for image in mine:   # one replica = one image (the reference's per-device maps)
+            attention_maps = ptp_utils.run_and_find_attn(ldm, image[None].to(device), context, layers=layers,
+                                                         noise_level=noise_level, from_where=from_where,
+                                                         upsample_res=upsample_res, controllers=controllers,
+                                                         device=device)
+            for attention_map in attention_maps:
+                if top_k_strategy == "entropy":
+                    cand = ptp_utils.entropy_sort(attention_map, furthest_point_num_samples)
+                elif top_k_strategy == "gaussian":
+                    cand = ptp_utils.find_top_k_gaussian(attention_map, furthest_point_num_samples, sigma=sigma,
+                                                         num_subjects=num_subjects)
+                else:
+                    cand = torch.arange(furthest_point_num_samples, device=attention_map.device)
+                indices_list.append(ptp_utils.furthest_point_sampling(attention_map, top_k, cand).cpu())
     indices_list = torch.cat(indices_list)
-    import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        gathered = [None] * dist.get_world_size()
+    if world > 1:
+        import torch.distributed as dist
+        gathered = [None] * world
         dist.all_gather_object(gathered, indices_list)
         indices_list = torch.cat(gathered)
     indices, counts = torch.unique(indices_list, return_counts=True)
     indices = indices[counts.argsort(descending=True)]
     return indices[:top_k]
+
+
+@torch.no_grad()
+def precompute_all_keypoints(ldm, context, top_indices, device="cuda", noise_level=-1, layers=(0, 1, 2, 3, 4, 5),
+                             from_where=("down_cross", "mid_cross", "up_cross"), augment_degrees=30,
+                             augment_scale=(0.9, 1.1), augment_translate=(0.1, 0.1), augmentation_iterations=20,
+                             dataset_loc="~", visualize=False, dataset_name="celeba_aligned", controllers=None,
+                             num_gpus=1, max_num_points=50_000, max_loc_strategy="argmax", save_folder="outputs",
+                             validation=False, dataset=None, upscale_size=512):
+    """keypoint_regressor.py:124-224: (source (P, n, 2), target (P, K, 2), visibility (P, K) or None).
+
+    ``dataset`` (extra) overrides the lookup; its items need "img" and "kpts" (and optionally
+    "visibility"), like the reference's *RegSet readers.
+    """
+    if dataset is None:
+        dataset = make_dataset(dataset_name, dataset_loc, validation=validation)
+    loader = _loader(dataset, 1)
+    it = iter(loader)
+    source, target, visibility = [], [], []
+    for _ in range(min(len(dataset), max_num_points)):
+        mb = next(it)
+        target.append(mb["kpts"][0])
+        if "visibility" in mb:
+            visibility.append(mb["visibility"][0])
+        maps = run_image_with_context_augmented(
+            ldm, mb["img"][0], context, top_indices, device=device, from_where=from_where, layers=layers,
+            noise_level=noise_level, augmentation_iterations=augmentation_iterations, augment_degrees=augment_degrees,
+            augment_scale=augment_scale, augment_translate=augment_translate, controllers=controllers,
+            save_folder=save_folder, num_gpus=num_gpus, upscale_size=upscale_size)
+        if max_loc_strategy == "argmax":
+            source.append(find_max_pixel(maps) / 512.0)
+        else:
+            source.append(pixel_from_weighted_avg(maps) / 512.0)
+    return torch.stack(source), torch.stack(target), (torch.stack(visibility) if visibility else None)
+
+
+def return_regressor(X, Y):
+    """keypoint_regressor.py:246-256: W = pinv(XᵀX) Xᵀ Y on centred coordinates."""
+    X = np.asarray(X) - 0.5
+    Y = np.asarray(Y) - 0.5
+    return np.linalg.pinv(X.T @ X) @ X.T @ Y
+
+
+def return_regressor_visible(X, Y, visible):
+    """keypoint_regressor.py:227-243: one least-squares column per keypoint over the images
+    where that keypoint is visible."""
+    X = np.asarray(X) - 0.5
+    Y = np.asarray(Y) - 0.5
+    visible = np.asarray(visible)
+    W = np.zeros((X.shape[1], Y.shape[1]))
+    for j in range(Y.shape[1]):
+        rows = np.where(visible[:, j] == 1)[0]
+        Xj = X[rows, :]
+        W[:, j] = np.linalg.pinv(Xj.T @ Xj) @ Xj.T @ Y[rows, j]
+    return W
+
+
+def return_regressor_human36m(X, Y):
+    """keypoint_regressor.py:266-299: least squares with left/right label swaps — while more
+    than 10 images sit closer to their swapped labels, swap those and refit."""
+    from .eval import swap_points
+    X = torch.as_tensor(X) - 0.5
+    Y = torch.as_tensor(Y) - 0.5
+    XTXXT = (X.T @ X).inverse() @ X.T
+    while True:
+        W = XTXXT @ Y
+        pred = X @ W
+        dist = (pred - Y).reshape(X.shape[0], -1, 2).norm(dim=2).mean(dim=1)
+        swapped = swap_points(Y.reshape(Y.shape[0], -1, 2)).reshape(Y.shape[0], -1)
+        swapped_dist = (pred - swapped).reshape(X.shape[0], -1, 2).norm(dim=2).mean(dim=1)
+        should = dist > swapped_dist
+        if should.sum() > 10:
+            Y[should] = swapped[should]
+        else:
+            break
+    return W.numpy()

@@ -1,9 +1,11 @@
-"""CLI with the reference's flags (``unsupervised_keypoints/main.py:23-196``).
+"""CLI with the reference's flags and stages (``unsupervised_keypoints/main.py:23-416``).
 
-Stages on this package's path: ``optimize`` (``optimize_embedding`` → ``embedding.pt``) and
-``find_indices`` (``find_best_indices`` → ``indices.pt``).  The later stages (keypoint
-precompute, regressor fitting, visualisation, evaluation) are outside the MI355X hot path.
-Multi-GPU: ``python -m torch.distributed.run --nproc-per-node N -m stablekeypoints_amd.main ...``.
+optimize (``optimize_embedding`` → ``embedding.pt``) → find_indices (``find_best_indices`` →
+``indices.pt``) → precompute (``precompute_all_keypoints`` → ``source_keypoints.pt``,
+``target_keypoints.pt``, ``visible.pt``) → regressor (``regressor.pt``) → evaluate
+(``all_errors.pt``).  ``--start_from_stage`` resumes from the saved files.  Visualisation
+(``visualize_attn_maps``) is not built.  Multi-GPU: ``python -m torch.distributed.run
+--nproc-per-node N -m stablekeypoints_amd.main ...`` (every rank seeded alike: ``--seed``).
 """
 import argparse
 import os
@@ -52,50 +54,95 @@ def build_parser():
     p.add_argument("--visualize", action="store_true")
     p.add_argument("--validation", action="store_true")
     p.add_argument("--top_k", type=int, default=10)
+    p.add_argument("--seed", type=int, default=0, help="CPU/GPU RNG seed, identical on every rank")
     return p
 
 
+def _load(folder, name, device=None):
+    t = torch.load(os.path.join(folder, name), weights_only=True)
+    return t.to(device) if (device is not None and t is not None) else t
+
+
 def main(argv=None):
+    import numpy as np
     args = build_parser().parse_args(argv)
+    from .eval import evaluate
+    from .keypoint_regressor import (find_best_indices, precompute_all_keypoints, return_regressor,
+                                     return_regressor_human36m, return_regressor_visible)
     from .optimize import optimize_embedding
     from .optimize_token import load_ldm
-    from .keypoint_regressor import find_best_indices
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         import torch.distributed as dist
         local = int(os.environ.get("LOCAL_RANK", "0"))
         torch.cuda.set_device(local)
         args.device = f"cuda:{local}"
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.manual_seed(args.seed)
+    torch.cuda.manual_seed(args.seed)
     ldm, controllers, num_gpus = load_ldm(args.device, args.model_type, feature_upsample_res=args.feature_upsample_res)
     os.makedirs(args.save_folder, exist_ok=True)
     rank0 = int(os.environ.get("RANK", "0")) == 0
-    if args.start_from_stage == "optimize":
+    stage = ["optimize", "find_indices", "precompute", "evaluate"].index(args.start_from_stage)
+    common = dict(noise_level=args.noise_level, device=args.device, layers=args.layers, dataset_loc=args.dataset_loc,
+                  dataset_name=args.dataset_name, controllers=controllers, num_gpus=num_gpus,
+                  validation=args.validation)
+    aug = dict(augment_degrees=args.augment_degrees, augment_scale=args.augment_scale,
+               augment_translate=args.augment_translate)
+    if stage <= 0:
         embedding = optimize_embedding(
-            ldm, top_k_strategy=args.top_k_strategy, wandb_log=args.wandb, noise_level=args.noise_level, lr=args.lr,
-            num_steps=int(args.num_steps), num_tokens=args.num_tokens, device=args.device, layers=args.layers,
-            top_k=args.top_k, augment_degrees=args.augment_degrees, augment_scale=args.augment_scale,
-            augment_translate=args.augment_translate, dataset_loc=args.dataset_loc, sigma=args.sigma,
+            ldm, top_k_strategy=args.top_k_strategy, wandb_log=args.wandb, lr=args.lr, num_steps=int(args.num_steps),
+            num_tokens=args.num_tokens, top_k=args.top_k, sigma=args.sigma,
             sharpening_loss_weight=args.sharpening_loss_weight,
             equivariance_attn_loss_weight=args.equivariance_attn_loss_weight, batch_size=args.batch_size,
-            dataset_name=args.dataset_name, max_len=args.max_len,
-            furthest_point_num_samples=args.furthest_point_num_samples, min_dist=args.min_dist,
-            controllers=controllers, num_gpus=num_gpus, validation=args.validation, num_subjects=args.num_subjects)
+            max_len=args.max_len, furthest_point_num_samples=args.furthest_point_num_samples, min_dist=args.min_dist,
+            num_subjects=args.num_subjects, **common, **aug)
         if rank0:
             torch.save(embedding, os.path.join(args.save_folder, "embedding.pt"))
     else:
-        embedding = torch.load(os.path.join(args.save_folder, "embedding.pt"), weights_only=True).to(args.device)
-    if args.start_from_stage in ("optimize", "find_indices"):
+        embedding = _load(args.save_folder, "embedding.pt", args.device).detach()
+    if stage <= 1:
         indices = find_best_indices(
-            ldm, embedding, num_steps=args.num_indices, noise_level=args.noise_level, num_tokens=args.num_tokens,
-            device=args.device, layers=args.layers, top_k=args.top_k, dataset_loc=args.dataset_loc,
-            dataset_name=args.dataset_name, min_dist=args.min_dist, controllers=controllers, num_gpus=num_gpus,
-            top_k_strategy=args.top_k_strategy, furthest_point_num_samples=args.furthest_point_num_samples,
-            sigma=args.sigma, validation=args.validation, num_subjects=args.num_subjects)
+            ldm, embedding, num_steps=args.num_indices, num_tokens=args.num_tokens, top_k=args.top_k,
+            min_dist=args.min_dist, top_k_strategy=args.top_k_strategy,
+            furthest_point_num_samples=args.furthest_point_num_samples, sigma=args.sigma,
+            num_subjects=args.num_subjects, **common)
         if rank0:
             torch.save(indices, os.path.join(args.save_folder, "indices.pt"))
             print("indices:", indices.tolist(), flush=True)
-    if args.start_from_stage in ("precompute", "evaluate"):
-        raise SystemExit("stages 'precompute'/'evaluate' (regressor, metrics) are outside the MI355X hot path")
+    else:
+        indices = _load(args.save_folder, "indices.pt", args.device).detach()
+    if stage <= 2:
+        source, target, visible = precompute_all_keypoints(
+            ldm, embedding, indices, augmentation_iterations=args.augmentation_iterations,
+            max_num_points=args.max_num_points, max_loc_strategy=args.max_loc_strategy,
+            save_folder=args.save_folder, **common, **aug)
+        if rank0:
+            torch.save(source, os.path.join(args.save_folder, "source_keypoints.pt"))
+            torch.save(target, os.path.join(args.save_folder, "target_keypoints.pt"))
+            torch.save(visible, os.path.join(args.save_folder, "visible.pt"))
+    else:
+        source = _load(args.save_folder, "source_keypoints.pt", args.device)
+        target = _load(args.save_folder, "target_keypoints.pt", args.device)
+        visible = _load(args.save_folder, "visible.pt", args.device)
+    # regressor (main.py:334-367)
+    X = source.cpu().numpy().reshape(source.shape[0], -1).astype(np.float64)
+    Y = target.cpu().numpy().reshape(target.shape[0], -1).astype(np.float64)
+    if args.evaluation_method in ("visible", "mean_average_error"):
+        if visible is None:
+            vis = np.ones_like(Y)
+        else:
+            vis = visible.unsqueeze(-1).repeat(1, 1, 2).reshape(visible.shape[0], -1).cpu().numpy().astype(np.float64)
+        regressor = return_regressor_visible(X, Y, vis)
+    elif args.evaluation_method == "orientation_invariant":
+        regressor = return_regressor_human36m(X, Y)
+    else:
+        regressor = return_regressor(X, Y)
+    regressor = torch.tensor(regressor).to(torch.float32)
+    if rank0:
+        torch.save(regressor, os.path.join(args.save_folder, "regressor.pt"))
+    evaluate(ldm, embedding, indices, regressor.to(args.device), num_tokens=args.num_tokens,
+             augmentation_iterations=args.augmentation_iterations, save_folder=args.save_folder,
+             evaluation_method=args.evaluation_method, max_loc_strategy=args.max_loc_strategy, **common, **aug)
 
 
 if __name__ == "__main__":

@@ -36,8 +36,10 @@ def import_reference():
     sys.modules["datasets"] = ds
     sys.path.insert(0, REF)
     from unsupervised_keypoints import ptp_utils, optimize, eval as ref_eval, optimize_token, invertable_transform
+    from unsupervised_keypoints import keypoint_regressor
     return types.SimpleNamespace(ptp_utils=ptp_utils, optimize=optimize, eval=ref_eval,
-                                 optimize_token=optimize_token, invertable_transform=invertable_transform)
+                                 optimize_token=optimize_token, invertable_transform=invertable_transform,
+                                 keypoint_regressor=keypoint_regressor)
 
 
 sys.path.insert(0, HERE)
@@ -296,6 +298,260 @@ def gen_step_tiny():
     np.savez_compressed(os.path.join(HERE, "step_tiny.npz"), **out)
 
 
+class _RecordingVAE:
+    """Wraps vae.encode to record image2latent's latents (ptp_utils.py:300-303)."""
+
+    def __init__(self, parts):
+        self.latents = []
+        enc = parts.vae.encode
+
+        def recording_encode(x, *a, **k):
+            out = enc(x, *a, **k)
+            self.latents.append(out["latent_dist"].mean.detach().clone() * 0.18215)
+            return out
+        parts.vae.encode = recording_encode
+
+
+def _tiny_parts_with_store(R):
+    pu = REFM.ptp_utils
+    from stablekeypoints_amd.sd import build_sd15, TINY_CONFIG
+    parts = build_sd15(seed=0, config=TINY_CONFIG)
+    parts.scheduler = _RecordingScheduler(parts.scheduler)
+    rec = _RecordingVAE(parts)
+    controllers = {torch.device("cpu"): pu.AttentionStore()}
+
+    def hook_fn(module, inp):   # optimize_token.py:59-68
+        pu.register_attention_control(module, controllers[inp[0].device], feature_upsample_res=R)
+    parts.unet.register_forward_pre_hook(hook_fn)
+    return parts, rec, controllers
+
+
+class _cuda_as_cpu:
+    """The reference hard-codes CUDA devices on its CPU-unreachable paths (eval.py:260, 473;
+    keypoint_regressor.py:84 calls run_and_find_attn without a device, default "cuda").  For
+    these CPU runs ``Tensor.to("cuda…")`` maps to "cpu" and ``Tensor.cuda()`` is the identity;
+    nothing else changes."""
+
+    def __enter__(self):
+        self.orig = orig = torch.Tensor.to
+        self.orig_cuda = torch.Tensor.cuda
+
+        def to_cpu(t, *a, **k):
+            if a and isinstance(a[0], str) and a[0].startswith("cuda"):
+                a = ("cpu",) + a[1:]
+            return orig(t, *a, **k)
+        torch.Tensor.to = to_cpu
+        torch.Tensor.cuda = lambda t, *a, **k: t   # eval.py:473 `.cuda()`
+
+    def __exit__(self, *exc):
+        torch.Tensor.to = self.orig
+        torch.Tensor.cuda = self.orig_cuda
+
+
+def gen_eval_tiny():
+    """A15 run_image_with_context_augmented (eval.py:197-355) + find_max_pixel, tiny model, CPU.
+
+    Thetas, VAE latents and noises of every augmentation are recorded so the GPU test can
+    replay identical inputs.
+    """
+    ev, it = REFM.eval, REFM.invertable_transform
+    from stablekeypoints_amd.sd import TINY_IMAGE
+    R, N, S = 32, 16, 64
+    parts, rec, controllers = _tiny_parts_with_store(R)
+    thetas = []
+
+    class RecAffine(it.RandomAffineWithInverse):
+        def __call__(self, img_tensor, theta=None):
+            out = super().__call__(img_tensor, theta)
+            thetas.append(self.last_params["theta"].clone())
+            return out
+    ev.RandomAffineWithInverse = RecAffine
+    img = torch.from_numpy(recipes.uniform(71, (3, TINY_IMAGE, TINY_IMAGE)))
+    ctx = torch.from_numpy(recipes.random_logits(72, (1, N, 32)))
+    indices = torch.tensor([3, 7, 0, 12, 5])
+    with _cuda_as_cpu():
+        torch.manual_seed(200)
+        maps = ev.run_image_with_context_augmented(
+            parts, img, ctx, indices, device="cpu", layers=[0, 1, 2, 3], augmentation_iterations=3, noise_level=-1,
+            augment_degrees=30, augment_scale=(0.9, 1.1), augment_translate=(0.1, 0.1), controllers=controllers,
+            num_gpus=1, upscale_size=S)
+    kp = ev.find_max_pixel(maps.clone()) / float(S)
+    out = {"R": R, "N": N, "S": S, "img_sha": recipes.sha256(_np(img)), "ctx": _np(ctx), "indices": _np(indices),
+           "thetas": np.stack([_np(t) for t in thetas]), "noises": np.stack([_np(n) for n in parts.scheduler.noises]),
+           "latents": np.stack([_np(l) for l in rec.latents]), "maps": _np(maps), "kp": _np(kp)}
+    np.savez_compressed(os.path.join(HERE, "eval_tiny.npz"), **out)
+
+
+def gen_best_indices_tiny():
+    """keypoint_regressor.find_best_indices (keypoint_regressor.py:16-121), tiny model, CPU.
+
+    The reference's "custom" dataset class is replaced by an in-memory one (its torchvision
+    transforms are absent here); the DataLoader shuffle, the per-image capture, top-k, FPS and
+    the unique/count ranking are the reference's own code.  Image order, latents and noises
+    are recorded for the GPU replay.
+    """
+    kr = REFM.keypoint_regressor
+    from stablekeypoints_amd.sd import TINY_IMAGE
+    R, N, S = 32, 16, 32
+    out = {"R": R, "N": N, "S": S}
+    imgs = torch.from_numpy(recipes.uniform(81, (6, 3, TINY_IMAGE, TINY_IMAGE)))
+    out["imgs_sha"] = recipes.sha256(_np(imgs))
+    # The per-image maps are recorded too: the random-init tiny model's maps are flat, so the
+    # argmax behind each Gaussian target (and hence the KL ranking) is decided by near-ties that
+    # a 1e-6 map difference can flip.  The GPU test checks the maps to tolerance and every later
+    # stage bit-exactly on the reference's own maps.  The "entropy" strategy is not pinned:
+    # softmax over [0, 1]-valued maps is near-uniform for ANY input, so its ranking sits at fp32
+    # summation noise (its kernel is checked against the fp64 oracle in test_gpu_parity).
+    ctx = torch.from_numpy(recipes.random_logits(82, (1, N, 32)))
+    out["ctx"] = _np(ctx)
+    for strat in ("gaussian", "consistent"):
+        parts, rec, controllers = _tiny_parts_with_store(R)
+        parts.vae = types.SimpleNamespace(module=parts.vae)   # the device="cuda" branch reads vae.module
+        order = []
+
+        class MemDS(torch.utils.data.Dataset):
+            def __init__(self, data_root=None, image_size=None):
+                pass
+
+            def __getitem__(self, i):
+                order.append(i)
+                return {"img": imgs[i], "kpts": torch.zeros(15, 2), "visibility": torch.zeros(15)}
+
+            def __len__(self):
+                return imgs.shape[0]
+        kr.custom_images.CustomDataset = MemDS
+        cands, picks = [], []
+        pu = REFM.ptp_utils
+        spy_fps, spy_topk = pu.furthest_point_sampling, pu.find_top_k_gaussian
+
+        maps_seen = []
+
+        def fps(maps, top_k, cand):
+            maps_seen.append(maps.clone())
+            cands.append(torch.as_tensor(cand).clone())
+            out = spy_fps(maps, top_k, cand)
+            picks.append(out.clone())
+            return out
+        pu.furthest_point_sampling = fps
+        with _cuda_as_cpu():
+            torch.manual_seed(300)
+            idx = kr.find_best_indices(parts, ctx, num_steps=5, device="cpu", noise_level=-1, upsample_res=S,
+                                       layers=[0, 1, 2, 3], top_k=4, dataset_name="custom",
+                                       furthest_point_num_samples=8, controllers=controllers, num_gpus=1,
+                                       top_k_strategy=strat, sigma=2.0)
+        out[f"{strat}_order"] = np.array(order)
+        out[f"{strat}_latents"] = np.stack([_np(l) for l in rec.latents])
+        out[f"{strat}_noises"] = np.stack([_np(n) for n in parts.scheduler.noises])
+        pu.furthest_point_sampling = spy_fps
+        out[f"{strat}_indices"] = _np(idx)
+        out[f"{strat}_cands"] = np.stack([_np(c) for c in cands])
+        out[f"{strat}_picks"] = np.stack([_np(c) for c in picks])
+        out[f"{strat}_maps"] = np.stack([_np(m) for m in maps_seen])
+    np.savez_compressed(os.path.join(HERE, "best_indices_tiny.npz"), **out)
+
+
+def gen_regressor():
+    """keypoint_regressor.return_regressor / return_regressor_visible (:227-256), numpy."""
+    kr = REFM.keypoint_regressor
+    X = recipes.uniform(101, (40, 20)).astype(np.float64)
+    Y = recipes.uniform(102, (40, 30)).astype(np.float64)
+    vis = (recipes.uniform(103, (40, 30)) > 0.2).astype(np.float64)
+    np.savez_compressed(os.path.join(HERE, "regressor.npz"), X=X, Y=Y, vis=vis, W=kr.return_regressor(X, Y),
+                        Wv=kr.return_regressor_visible(X, Y, vis))
+
+
+def gen_celeba_reader():
+    """datasets/celeba.py:8-150 on a seeded 6-image tree (recipes.write_mini_celeba)."""
+    import tempfile
+    from datasets import celeba
+    out = {}
+    with tempfile.TemporaryDirectory() as root:
+        recipes.write_mini_celeba(root)
+        for align in (True, False):
+            for split in ("train", "test"):
+                ds = celeba.CelebA(split=split, align=align, dataset_loc=root)
+                key = f"{'align' if align else 'wild'}_{split}"
+                out[key + "_len"] = len(ds)
+                out[key + "_img_sha"] = np.array([recipes.sha256(_np(ds[i]["img"])) for i in range(len(ds))])
+                out[key + "_kpts"] = np.stack([_np(ds[i]["kpts"]) for i in range(len(ds))])
+    np.savez_compressed(os.path.join(HERE, "celeba_reader.npz"), **out)
+
+
+def gen_evaluate_tiny():
+    """eval.evaluate (eval.py:374-539) on the tiny model, all five metrics, CPU.
+
+    The test split is an in-memory 3-image set patched in for the CelebA class; per metric the
+    reference's per-image maxima (find_max_pixel output), ground truth, errors (all_errors.pt)
+    and, for inter_eye_distance, the replay inputs (thetas, latents, noises) are recorded.
+    """
+    import tempfile
+    ev, it = REFM.eval, REFM.invertable_transform
+    from stablekeypoints_amd.sd import TINY_IMAGE
+    R, N, K = 32, 16, 32
+    imgs = torch.from_numpy(recipes.uniform(111, (3, 3, TINY_IMAGE, TINY_IMAGE)))
+    kpts = torch.from_numpy(recipes.uniform(112, (3, K, 2)))
+    vis = torch.from_numpy((recipes.uniform(113, (3, K)) > 0.3).astype(np.float32))
+    ctx = torch.from_numpy(recipes.random_logits(114, (1, N, 32)))
+    indices = torch.tensor([2, 9, 14])
+    W = torch.from_numpy(recipes.random_logits(115, (2 * len(indices), 2 * K), scale=0.3))
+    out = {"R": R, "N": N, "imgs_sha": recipes.sha256(_np(imgs)), "kpts": _np(kpts), "vis": _np(vis),
+           "ctx": _np(ctx), "indices": _np(indices), "W": _np(W)}
+    for method in ("inter_eye_distance", "visible", "mean_average_error", "pck", "orientation_invariant"):
+        parts, rec, controllers = _tiny_parts_with_store(R)
+        order, highest, thetas = [], [], []
+
+        class MemDS(torch.utils.data.Dataset):
+            def __init__(self, *a, **k):
+                pass
+
+            def __getitem__(self, i):
+                order.append(i)
+                item = {"img": imgs[i], "kpts": kpts[i]}
+                if method in ("visible", "mean_average_error"):
+                    item["visibility"] = vis[i]
+                return item
+
+            def __len__(self):
+                return imgs.shape[0]
+
+        class RecAffine(it.RandomAffineWithInverse):
+            def __call__(self, img_tensor, theta=None):
+                o = super().__call__(img_tensor, theta)
+                thetas.append(self.last_params["theta"].clone())
+                return o
+        spy_max = REFM.eval.find_max_pixel
+
+        def find_max_pixel(maps):
+            r = spy_max(maps)
+            highest.append(r.clone())
+            return r
+        tta = ev.run_image_with_context_augmented
+
+        def no_vis(*a, **k):   # evaluate plots image 0 (visualize=(i==0), 512² only): a side output
+            k["visualize"] = False
+            return tta(*a, **k)
+        ev.CelebA = MemDS
+        ev.RandomAffineWithInverse = RecAffine
+        ev.find_max_pixel = find_max_pixel
+        ev.run_image_with_context_augmented = no_vis
+        with tempfile.TemporaryDirectory() as d, _cuda_as_cpu():
+            torch.manual_seed(400)
+            ev.evaluate(parts, ctx, indices, W, device="cpu", layers=[0, 1, 2, 3], augmentation_iterations=2,
+                        save_folder=d, dataset_name="celeba_aligned", evaluation_method=method,
+                        controllers=controllers, num_gpus=1)
+            errs = torch.load(os.path.join(d, "all_errors.pt"), weights_only=True)
+        ev.find_max_pixel = spy_max
+        ev.run_image_with_context_augmented = tta
+        out[f"{method}_order"] = np.array(order)
+        out[f"{method}_highest"] = np.stack([_np(h) for h in highest])
+        out[f"{method}_errors"] = _np(errs)
+        if method == "inter_eye_distance":
+            out["thetas"] = np.stack([_np(t) for t in thetas])
+            out["latents"] = np.stack([_np(x) for x in rec.latents])
+            out["noises"] = np.stack([_np(x) for x in parts.scheduler.noises])
+    np.savez_compressed(os.path.join(HERE, "evaluate_tiny.npz"), **out)
+
+
 def gen_interp():
     """Torch interpolation/warp numerics the kernels restate."""
     import torch.nn.functional as F
@@ -315,7 +571,7 @@ if __name__ == "__main__":
     REFM = import_reference()
     torch.set_num_threads(8)
     which = sys.argv[1:] or ["capture_small", "capture_sd15", "argmax", "gaussian", "select", "losses",
-                             "step_tiny", "interp"]
+                             "step_tiny", "interp", "eval_tiny", "best_indices_tiny", "regressor", "celeba_reader", "evaluate_tiny"]
     for w in which:
         print("generating", w, flush=True)
         globals()["gen_" + w]()

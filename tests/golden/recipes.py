@@ -79,3 +79,38 @@ def capture_inputs(seed, shapes, n_tokens, ctx_dim):
     ctx = random_logits(seed * 7 + 99, (1, n_tokens, ctx_dim))
     params = [cross_attention_params(seed, li, c, ctx_dim) for li, (s, c) in enumerate(shapes)]
     return xs, ctx, params
+
+
+def write_mini_celeba(root, seed=0):
+    """A 6-image CelebA tree (datasets/celeba.py layout) with seeded random pixels, sizes,
+    landmarks and face boxes: aligned PNGs and in-the-wild JPEGs, MAFL train/test lists.
+    Images 2 and 5 get face boxes below the wild reader's 30 % area threshold."""
+    import os
+    from PIL import Image
+    rng = np.random.default_rng(seed)
+    n = 6
+    for sub in ("Anno", "MAFL", "Img/img_align_celeba_png", "Img/img_celeba"):
+        os.makedirs(os.path.join(root, sub), exist_ok=True)
+    lm_a, lm_w, bb = [f"{n}\n", "lefteye_x lefteye_y ...\n"], [f"{n}\n", "lefteye_x lefteye_y ...\n"], \
+        [f"{n}\n", "image_id x_1 y_1 width height\n"]
+    for k in range(n):
+        name = f"{k + 1:06d}"
+        ha, wa = int(rng.integers(40, 64)), int(rng.integers(40, 64))
+        Image.fromarray(rng.integers(0, 256, (ha, wa, 3), dtype=np.uint8)).save(
+            os.path.join(root, "Img/img_align_celeba_png", name + ".png"))
+        hw, ww = int(rng.integers(48, 80)), int(rng.integers(48, 80))
+        Image.fromarray(rng.integers(0, 256, (hw, ww, 3), dtype=np.uint8)).save(
+            os.path.join(root, "Img/img_celeba", name + ".jpg"), quality=90)
+        pa = rng.uniform(0, 1, (5, 2)) * [wa, ha]
+        pw = rng.uniform(0, 1, (5, 2)) * [ww, hw]
+        lm_a.append(name + ".jpg " + " ".join(str(int(v)) for v in pa.ravel()) + "\n")
+        lm_w.append(name + ".jpg " + " ".join(str(int(v)) for v in pw.ravel()) + "\n")
+        frac = 0.1 if k in (2, 5) else 0.6
+        bw, bh = int(ww * np.sqrt(frac)), int(hw * np.sqrt(frac))
+        bb.append(f"{name}.jpg 1 2 {bw} {bh}\n")
+    open(os.path.join(root, "Anno/list_landmarks_align_celeba.txt"), "w").writelines(lm_a)
+    open(os.path.join(root, "Anno/list_landmarks_celeba.txt"), "w").writelines(lm_w)
+    open(os.path.join(root, "Anno/list_bbox_celeba.txt"), "w").writelines(bb)
+    open(os.path.join(root, "MAFL/training.txt"), "w").writelines(["000001.jpg\n", "000003.jpg\n", "000004.jpg\n",
+                                                                   "000006.jpg\n"])
+    open(os.path.join(root, "MAFL/testing.txt"), "w").writelines(["000002.jpg\n", "000005.jpg\n"])

@@ -76,7 +76,7 @@ def _worker(rank, world, port, n_img, steps, q):
             for i in range(per_rank):   # rank r takes images r*per_rank ... of each global batch
                 opt.micro_step(imgs[st * n_img + rank * per_rank + i])
             recs.append({k: float(v) for k, v in opt.optimizer_step().items()})
-        q.put((rank, opt.context.detach().clone(), recs))
+        q.put((rank, opt.context.detach().numpy().copy(), recs))   # by value: no fd sharing
     finally:
         dist.destroy_process_group()
 
@@ -95,7 +95,105 @@ def test_two_rank_grad_allreduce_equals_single_rank():
         p.join(timeout=60)
         assert p.exitcode == 0
     for rank, c, recs in out:
+        c = torch.from_numpy(c)
         assert torch.allclose(c, ref_ctx, atol=1e-6, rtol=1e-5), f"rank {rank} context diverged"
         for a, b in zip(recs, ref_recs):
             for k in a:
                 assert abs(a[k] - b[k]) <= 1e-5 * max(1.0, abs(b[k])), (k, a[k], b[k])
+
+
+# ---------------------------------------------------------------------------- eval-side stages
+# find_best_indices / run_image_with_context_augmented on 2 ranks == one process running the
+# reference's num_gpus=2 replicas.  The capture, selection and warp ops are HIP kernels; here
+# they are replaced by CPU stand-ins that depend on the image content and theta, so the test
+# checks the replica ↔ rank mapping, the shared shuffle / theta draws and the collectives.
+def _stub_eval_stages(monkeypatch_like):
+    from stablekeypoints_amd import ptp_utils
+    from stablekeypoints_amd.invertable_transform import RandomAffineWithInverse
+
+    def fake_maps(image, indices=None):
+        img = image.reshape(image.shape[0], -1)
+        base = torch.arange(16.0).reshape(16, 1, 1) * 0.01
+        maps = base + img.mean(dim=1).reshape(-1, 1, 1, 1)[0] * torch.linspace(0, 1, 64).reshape(1, 8, 8)
+        maps = maps * (1 + torch.arange(16.0).reshape(16, 1, 1) * img[0, 0])
+        return maps if indices is None else maps[torch.as_tensor(indices)]
+
+    def run_and_find_attn(ldm, image, context, indices=None, **kw):
+        return [fake_maps(image, indices)]
+
+    def run_and_find_attn_per_image(ldm, images, context, indices=None, **kw):
+        return [[fake_maps(images[b:b + 1], indices) for b in range(images.shape[0])]]
+
+    def topk(maps, k, **kw):
+        return torch.argsort(maps.reshape(maps.shape[0], -1).sum(1), descending=True)[:k]
+
+    def fps(maps, k, cand):
+        return torch.as_tensor(cand)[[0, len(cand) - 1]][:k]
+
+    def warp(self, img, theta=None):
+        if theta is None:
+            theta = self.draw_theta(img.shape[0])
+        self.last_params = {"theta": theta}
+        return img * theta[:, 0, 0].reshape(-1, 1, 1, 1) + theta[:, 0, 2].reshape(-1, 1, 1, 1)
+
+    def inverse(self, x):
+        th = self.last_params["theta"]
+        return (x - th[:, 0, 2].reshape(-1, 1, 1, 1)) * th[:, 1, 1].reshape(-1, 1, 1, 1)
+
+    for obj, name, fn in [(ptp_utils, "run_and_find_attn", run_and_find_attn),
+                          (ptp_utils, "run_and_find_attn_per_image", run_and_find_attn_per_image),
+                          (ptp_utils, "find_top_k_gaussian", topk), (ptp_utils, "entropy_sort", topk),
+                          (ptp_utils, "furthest_point_sampling", fps),
+                          (RandomAffineWithInverse, "__call__", warp), (RandomAffineWithInverse, "inverse", inverse)]:
+        monkeypatch_like(obj, name, fn)
+
+
+class _DS(torch.utils.data.Dataset):
+    def __getitem__(self, i):
+        g = torch.Generator().manual_seed(100 + i)
+        return {"img": torch.rand(3, 8, 8, generator=g), "kpts": torch.zeros(2, 2)}
+
+    def __len__(self):
+        return 6
+
+
+def _eval_stages(num_gpus):
+    from stablekeypoints_amd import keypoint_regressor as kr, eval as ev
+    torch.manual_seed(11)
+    idx = kr.find_best_indices(None, None, num_steps=6, device="cpu", top_k=4, furthest_point_num_samples=8,
+                               controllers={"cpu": None}, num_gpus=num_gpus, top_k_strategy="gaussian",
+                               dataset=_DS())
+    img = _DS()[0]["img"]
+    tta = ev.run_image_with_context_augmented(None, img, None, torch.tensor([1, 3, 5]), device="cpu",
+                                              augmentation_iterations=4, controllers={"cpu": None},
+                                              num_gpus=num_gpus, upscale_size=8)
+    return idx, tta
+
+
+def _eval_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _stub_eval_stages(setattr)
+        q.put((rank,) + tuple(t.numpy().copy() for t in _eval_stages(world)))   # by value
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_eval_stages_equal_two_replicas_in_one_process(monkeypatch):
+    _stub_eval_stages(monkeypatch.setattr)
+    ref_idx, ref_tta = _eval_stages(2)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_eval_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, idx, tta in out:
+        idx, tta = torch.from_numpy(idx), torch.from_numpy(tta)
+        assert torch.equal(idx, ref_idx), (rank, idx, ref_idx)
+        assert torch.allclose(tta, ref_tta, rtol=1e-6, atol=1e-7), rank
