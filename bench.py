@@ -211,6 +211,7 @@ def main():
     ap.add_argument("--conv-benchmark", type=int, default=0, help="torch.backends.cudnn.benchmark (MIOpen exhaustive find)")
     ap.add_argument("--attn-backend", default="math", choices=["math", "sdpa"],
                     help="un-captured UNet attention: explicit fp32 GEMM+softmax (math) or torch SDPA")
+    ap.add_argument("--gc-freeze", type=int, default=1, help="gc.freeze() after the model is built (host overhead)")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
                     help="JSON with PMC-derived HBM bytes per launch of the roofline kernel")
     args = ap.parse_args()
@@ -234,6 +235,10 @@ def main():
     from stablekeypoints_amd.datasets import SyntheticDataset
 
     ldm, controllers, num_gpus = load_ldm(dev, "runwayml/stable-diffusion-v1-5", feature_upsample_res=args.upsample_res)
+    if args.gc_freeze:
+        import gc
+        gc.collect()
+        gc.freeze()   # the model's ~10^5 long-lived objects leave the cyclic collector's scans
     torch.manual_seed(0)
     context = torch.randn(1, args.tokens, 768).to(dev)
     torch.manual_seed(1234 + rank)

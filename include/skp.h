@@ -146,14 +146,22 @@ int skp_bgemm_f32(const float* A, long long sAb, long long sAm, long long sAk, c
  * The token-opt backward runs through the frozen SD-1.5 UNet; its
  * GroupNorm → SiLU pairs (diffusers-0.8.0 ResnetBlock2D / Transformer2DModel.norm /
  * VAE encoder) run fused here.  x, y, dx: (B, C, HW) NCHW fp32; act = 1 applies SiLU.
+ * shift (B*C floats, or NULL) is added to x on load: GroupNorm(x + shift[b, c]) — the
+ * preceding convolution's bias and the resnet's time embedding, never materialised.
  * stats (B*G*2 floats) = (mean, rstd) per group, written by fwd and read by bwd.
  * partial: skp_groupnorm_workspace(B, C, HW, G) doubles.  Parameters are frozen, so the
  * backward returns dx only.                                                      */
 int skp_groupnorm_workspace(int B, int C, long long HW, int G);
-int skp_groupnorm_fwd(const float* x, const float* gamma, const float* beta, int B, int C, long long HW, int G,
-                      float eps, int act, float* y, float* stats, double* partial, void* stream);
-int skp_groupnorm_bwd(const float* x, const float* dy, const float* gamma, const float* beta, const float* stats,
-                      int B, int C, long long HW, int G, int act, float* dx, double* partial, void* stream);
+int skp_groupnorm_fwd(const float* x, const float* gamma, const float* beta, const float* shift, int B, int C,
+                      long long HW, int G, float eps, int act, float* y, float* stats, double* partial,
+                      void* stream);
+int skp_groupnorm_bwd(const float* x, const float* dy, const float* gamma, const float* beta, const float* shift,
+                      const float* stats, int B, int C, long long HW, int G, int act, float* dx, double* partial,
+                      void* stream);
+/* out = a + (h + bias[c]) over (B, C, HW): diffusers ResnetBlock2D `x + conv2(...)` with the
+ * convolution's bias folded into the residual add (same rounding order).         */
+int skp_residual_bias_add(const float* a, const float* h, const float* bias, int B, int C, long long HW,
+                          float* out, void* stream);
 
 #ifdef __cplusplus
 }

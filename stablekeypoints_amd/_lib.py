@@ -38,8 +38,9 @@ _SIGS = {
     "skp_bgemm_f32": [_p, _c_ll, _c_ll, _c_ll, _p, _c_ll, _c_ll, _c_ll, _p, _c_ll, _c_ll, _c_ll, _c_int, _c_int,
                       _c_int, _c_int, _c_float, _c_int, _p],
     "skp_groupnorm_workspace": [_c_int, _c_int, _c_ll, _c_int],
-    "skp_groupnorm_fwd": [_p, _p, _p, _c_int, _c_int, _c_ll, _c_int, _c_float, _c_int, _p, _p, _p, _p],
-    "skp_groupnorm_bwd": [_p, _p, _p, _p, _p, _c_int, _c_int, _c_ll, _c_int, _c_int, _p, _p, _p],
+    "skp_groupnorm_fwd": [_p, _p, _p, _p, _c_int, _c_int, _c_ll, _c_int, _c_float, _c_int, _p, _p, _p, _p],
+    "skp_groupnorm_bwd": [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_ll, _c_int, _c_int, _p, _p, _p],
+    "skp_residual_bias_add": [_p, _p, _p, _c_int, _c_int, _c_ll, _p, _p],
     "skp_version": [],
 }
 

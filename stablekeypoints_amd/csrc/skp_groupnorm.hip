@@ -1,5 +1,7 @@
 // Fused GroupNorm (+ optional SiLU) forward / input-gradient backward for the frozen SD-1.5
-// UNet / VAE (NCHW fp32) on gfx950.
+// UNet / VAE (NCHW fp32) on gfx950.  An optional per-(sample, channel) input shift folds the
+// preceding convolution's bias and the resnet's time-embedding add into the same passes:
+// GroupNorm(x + shift[b, c]) without materialising x + shift.
 //
 // The hot path's backward runs through the UNet into the token embedding,
 // and GroupNorm is the UNet's largest non-GEMM cost (ATen: statistics kernel + separate
@@ -11,6 +13,8 @@
 //   dx = rstd·(gz·γ − mean(gz·γ) − x̂·mean(gz·γ·x̂))
 //   pass 1  per-chunk partial (Σ gzγ, Σ gzγx̂) in fp64;  pass 2  dx.
 // All reductions have a fixed order, so results are run-to-run deterministic.
+#include <algorithm>
+
 #include "skp_common.h"
 
 using namespace skp;
@@ -31,6 +35,11 @@ struct GNShape {
   long long HW, len;  // len = cpg * HW (floats per group)
 };
 
+// shift of channel c of group grp (nullptr: none)
+__device__ __forceinline__ float shift_of(const float* __restrict__ shift, const GNShape& sh, int grp, int c) {
+  return shift ? shift[(grp / sh.G) * sh.C + c] : 0.0f;
+}
+
 __device__ __forceinline__ void block_sum2(double& a, double& b, double* sd) {
   a = wave_sum(a);
   b = wave_sum(b);
@@ -49,22 +58,26 @@ __device__ __forceinline__ void block_sum2(double& a, double& b, double* sd) {
 }
 
 template <bool VEC>
-__global__ __launch_bounds__(kThreads) void gn_stats_kernel(const float* __restrict__ x, GNShape sh,
+__global__ __launch_bounds__(kThreads) void gn_stats_kernel(const float* __restrict__ x,
+                                                            const float* __restrict__ shift, GNShape sh,
                                                             double* __restrict__ partial) {
   __shared__ double sd[2 * kThreads / 64];
   const int grp = blockIdx.x / sh.nsplit, sp = blockIdx.x % sh.nsplit;
+  const int g = grp % sh.G;
   const float* base = x + (size_t)grp * sh.len;
   const long long lo = (long long)sp * kChunk, hi = min(sh.len, lo + kChunk);
   double s1 = 0.0, s2 = 0.0;
   if (VEC) {
     for (long long e = lo + 4 * threadIdx.x; e < hi; e += 4 * kThreads) {
-      const float4 v = *reinterpret_cast<const float4*>(base + e);
+      float4 v = *reinterpret_cast<const float4*>(base + e);
+      const float t = shift_of(shift, sh, grp, g * sh.cpg + (int)(e / sh.HW));
+      v.x += t; v.y += t; v.z += t; v.w += t;
       s1 += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
       s2 += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
     }
   } else {
     for (long long e = lo + threadIdx.x; e < hi; e += kThreads) {
-      const double v = base[e];
+      const double v = base[e] + shift_of(shift, sh, grp, g * sh.cpg + (int)(e / sh.HW));
       s1 += v;
       s2 += v * v;
     }
@@ -94,7 +107,8 @@ __device__ __forceinline__ void group_moments(const double* __restrict__ partial
 
 template <bool VEC, bool ACT>
 __global__ __launch_bounds__(kThreads) void gn_apply_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
-                                                            const float* __restrict__ beta, GNShape sh, float eps,
+                                                            const float* __restrict__ beta,
+                                                            const float* __restrict__ shift, GNShape sh, float eps,
                                                             const double* __restrict__ partial, float* __restrict__ y,
                                                             float* __restrict__ stats) {
   __shared__ float sm[2];
@@ -116,7 +130,9 @@ __global__ __launch_bounds__(kThreads) void gn_apply_kernel(const float* __restr
     for (long long e = lo + 4 * threadIdx.x; e < hi; e += 4 * kThreads) {
       const int c = g * sh.cpg + (int)(e / sh.HW);
       const float ga = gamma[c] * rstd, be = beta[c] - mean * gamma[c] * rstd;
+      const float t = shift_of(shift, sh, grp, c);
       float4 v = *reinterpret_cast<const float4*>(base + e);
+      v.x += t; v.y += t; v.z += t; v.w += t;
       v.x = v.x * ga + be; v.y = v.y * ga + be; v.z = v.z * ga + be; v.w = v.w * ga + be;
       if (ACT) { v.x = silu(v.x); v.y = silu(v.y); v.z = silu(v.z); v.w = silu(v.w); }
       *reinterpret_cast<float4*>(out + e) = v;
@@ -124,7 +140,7 @@ __global__ __launch_bounds__(kThreads) void gn_apply_kernel(const float* __restr
   } else {
     for (long long e = lo + threadIdx.x; e < hi; e += kThreads) {
       const int c = g * sh.cpg + (int)(e / sh.HW);
-      float v = (base[e] - mean) * rstd * gamma[c] + beta[c];
+      float v = ((base[e] + shift_of(shift, sh, grp, c)) - mean) * rstd * gamma[c] + beta[c];
       out[e] = ACT ? silu(v) : v;
     }
   }
@@ -134,7 +150,8 @@ template <bool VEC, bool ACT>
 __global__ __launch_bounds__(kThreads) void gn_bwd_stats_kernel(const float* __restrict__ x,
                                                                 const float* __restrict__ dy,
                                                                 const float* __restrict__ gamma,
-                                                                const float* __restrict__ beta, GNShape sh,
+                                                                const float* __restrict__ beta,
+                                                                const float* __restrict__ shift, GNShape sh,
                                                                 const float* __restrict__ stats,
                                                                 double* __restrict__ partial) {
   __shared__ double sd[2 * kThreads / 64];
@@ -148,7 +165,7 @@ __global__ __launch_bounds__(kThreads) void gn_bwd_stats_kernel(const float* __r
   const long long step = VEC ? 4 : 1;
   for (long long e0 = lo + step * threadIdx.x; e0 < hi; e0 += step * kThreads) {
     const int c = g * sh.cpg + (int)(e0 / sh.HW);
-    const float ga = gamma[c], be = beta[c];
+    const float ga = gamma[c], be = beta[c], t = shift_of(shift, sh, grp, c);
     float xv[4], dv[4];
     if (VEC) {
       const float4 a = *reinterpret_cast<const float4*>(xb + e0), b = *reinterpret_cast<const float4*>(db + e0);
@@ -160,7 +177,7 @@ __global__ __launch_bounds__(kThreads) void gn_bwd_stats_kernel(const float* __r
     }
 #pragma unroll
     for (int k = 0; k < (VEC ? 4 : 1); ++k) {
-      const float xh = (xv[k] - mean) * rstd;
+      const float xh = ((xv[k] + t) - mean) * rstd;
       float gz = dv[k];
       if (ACT) gz *= silu_grad(xh * ga + be);
       const float gg = gz * ga;
@@ -179,7 +196,8 @@ template <bool VEC, bool ACT>
 __global__ __launch_bounds__(kThreads) void gn_bwd_apply_kernel(const float* __restrict__ x,
                                                                 const float* __restrict__ dy,
                                                                 const float* __restrict__ gamma,
-                                                                const float* __restrict__ beta, GNShape sh,
+                                                                const float* __restrict__ beta,
+                                                                const float* __restrict__ shift, GNShape sh,
                                                                 const float* __restrict__ stats,
                                                                 const double* __restrict__ partial,
                                                                 float* __restrict__ dx) {
@@ -205,7 +223,7 @@ __global__ __launch_bounds__(kThreads) void gn_bwd_apply_kernel(const float* __r
   const long long step = VEC ? 4 : 1;
   for (long long e0 = lo + step * threadIdx.x; e0 < hi; e0 += step * kThreads) {
     const int c = g * sh.cpg + (int)(e0 / sh.HW);
-    const float ga = gamma[c], be = beta[c];
+    const float ga = gamma[c], be = beta[c], t = shift_of(shift, sh, grp, c);
     float xv[4], dv[4], r[4];
     if (VEC) {
       const float4 a = *reinterpret_cast<const float4*>(xb + e0), b = *reinterpret_cast<const float4*>(db + e0);
@@ -217,13 +235,33 @@ __global__ __launch_bounds__(kThreads) void gn_bwd_apply_kernel(const float* __r
     }
 #pragma unroll
     for (int k = 0; k < (VEC ? 4 : 1); ++k) {
-      const float xh = (xv[k] - mean) * rstd;
+      const float xh = ((xv[k] + t) - mean) * rstd;
       float gz = dv[k];
       if (ACT) gz *= silu_grad(xh * ga + be);
       r[k] = rstd * (gz * ga - ma - xh * mb);
     }
     if (VEC) *reinterpret_cast<float4*>(ob + e0) = make_float4(r[0], r[1], r[2], r[3]);
     else ob[e0] = r[0];
+  }
+}
+
+// out = a + (h + bias[c]): a convolution's bias add fused into the residual add that
+// consumes it (same fp32 rounding order as the two separate torch adds).
+template <bool VEC>
+__global__ __launch_bounds__(kThreads) void residual_bias_kernel(const float* __restrict__ a,
+                                                                 const float* __restrict__ h,
+                                                                 const float* __restrict__ bias, int C, long long HW,
+                                                                 long long total, float* __restrict__ out) {
+  const long long step = (long long)gridDim.x * kThreads * (VEC ? 4 : 1);
+  for (long long e = ((long long)blockIdx.x * kThreads + threadIdx.x) * (VEC ? 4 : 1); e < total; e += step) {
+    const float b = bias[(e / HW) % C];
+    if (VEC) {
+      const float4 x = *reinterpret_cast<const float4*>(a + e), y = *reinterpret_cast<const float4*>(h + e);
+      *reinterpret_cast<float4*>(out + e) = make_float4(x.x + (y.x + b), x.y + (y.y + b), x.z + (y.z + b),
+                                                        x.w + (y.w + b));
+    } else {
+      out[e] = a[e] + (h[e] + b);
+    }
   }
 }
 
@@ -243,8 +281,9 @@ extern "C" int skp_groupnorm_workspace(int B, int C, long long HW, int G) {
   return B * G * sh.nsplit * 2;   // doubles
 }
 
-extern "C" int skp_groupnorm_fwd(const float* x, const float* gamma, const float* beta, int B, int C, long long HW,
-                                 int G, float eps, int act, float* y, float* stats, double* partial, void* stream) {
+extern "C" int skp_groupnorm_fwd(const float* x, const float* gamma, const float* beta, const float* shift, int B,
+                                 int C, long long HW, int G, float eps, int act, float* y, float* stats,
+                                 double* partial, void* stream) {
   SKP_CHECK_ARG(x && gamma && beta && y && partial, "null pointer");
   GNShape sh;
   SKP_CHECK_ARG(make_shape(B, C, HW, G, sh), "bad shape (C must be divisible by G)");
@@ -252,11 +291,12 @@ extern "C" int skp_groupnorm_fwd(const float* x, const float* gamma, const float
                    ((reinterpret_cast<uintptr_t>(y) & 15) == 0);
   hipStream_t st = as_stream(stream);
   const dim3 grid(B * G * sh.nsplit);
-  if (vec) hipLaunchKernelGGL(gn_stats_kernel<true>, grid, dim3(kThreads), 0, st, x, sh, partial);
-  else hipLaunchKernelGGL(gn_stats_kernel<false>, grid, dim3(kThreads), 0, st, x, sh, partial);
+  if (vec) hipLaunchKernelGGL(gn_stats_kernel<true>, grid, dim3(kThreads), 0, st, x, shift, sh, partial);
+  else hipLaunchKernelGGL(gn_stats_kernel<false>, grid, dim3(kThreads), 0, st, x, shift, sh, partial);
   SKP_LAUNCH_CHECK();
 #define SKP_GN_APPLY(V, A) \
-  hipLaunchKernelGGL((gn_apply_kernel<V, A>), grid, dim3(kThreads), 0, st, x, gamma, beta, sh, eps, partial, y, stats)
+  hipLaunchKernelGGL((gn_apply_kernel<V, A>), grid, dim3(kThreads), 0, st, x, gamma, beta, shift, sh, eps, partial, y, \
+                     stats)
   if (vec) { if (act) SKP_GN_APPLY(true, true); else SKP_GN_APPLY(true, false); }
   else { if (act) SKP_GN_APPLY(false, true); else SKP_GN_APPLY(false, false); }
 #undef SKP_GN_APPLY
@@ -265,8 +305,8 @@ extern "C" int skp_groupnorm_fwd(const float* x, const float* gamma, const float
 }
 
 extern "C" int skp_groupnorm_bwd(const float* x, const float* dy, const float* gamma, const float* beta,
-                                 const float* stats, int B, int C, long long HW, int G, int act, float* dx,
-                                 double* partial, void* stream) {
+                                 const float* shift, const float* stats, int B, int C, long long HW, int G, int act,
+                                 float* dx, double* partial, void* stream) {
   SKP_CHECK_ARG(x && dy && gamma && beta && stats && dx && partial, "null pointer");
   GNShape sh;
   SKP_CHECK_ARG(make_shape(B, C, HW, G, sh), "bad shape (C must be divisible by G)");
@@ -276,21 +316,37 @@ extern "C" int skp_groupnorm_bwd(const float* x, const float* dy, const float* g
   const dim3 grid(B * G * sh.nsplit);
 #define SKP_GN_B(K, V, A, ...) hipLaunchKernelGGL((K<V, A>), grid, dim3(kThreads), 0, st, __VA_ARGS__)
   if (vec) {
-    if (act) SKP_GN_B(gn_bwd_stats_kernel, true, true, x, dy, gamma, beta, sh, stats, partial);
-    else SKP_GN_B(gn_bwd_stats_kernel, true, false, x, dy, gamma, beta, sh, stats, partial);
+    if (act) SKP_GN_B(gn_bwd_stats_kernel, true, true, x, dy, gamma, beta, shift, sh, stats, partial);
+    else SKP_GN_B(gn_bwd_stats_kernel, true, false, x, dy, gamma, beta, shift, sh, stats, partial);
   } else {
-    if (act) SKP_GN_B(gn_bwd_stats_kernel, false, true, x, dy, gamma, beta, sh, stats, partial);
-    else SKP_GN_B(gn_bwd_stats_kernel, false, false, x, dy, gamma, beta, sh, stats, partial);
+    if (act) SKP_GN_B(gn_bwd_stats_kernel, false, true, x, dy, gamma, beta, shift, sh, stats, partial);
+    else SKP_GN_B(gn_bwd_stats_kernel, false, false, x, dy, gamma, beta, shift, sh, stats, partial);
   }
   SKP_LAUNCH_CHECK();
   if (vec) {
-    if (act) SKP_GN_B(gn_bwd_apply_kernel, true, true, x, dy, gamma, beta, sh, stats, partial, dx);
-    else SKP_GN_B(gn_bwd_apply_kernel, true, false, x, dy, gamma, beta, sh, stats, partial, dx);
+    if (act) SKP_GN_B(gn_bwd_apply_kernel, true, true, x, dy, gamma, beta, shift, sh, stats, partial, dx);
+    else SKP_GN_B(gn_bwd_apply_kernel, true, false, x, dy, gamma, beta, shift, sh, stats, partial, dx);
   } else {
-    if (act) SKP_GN_B(gn_bwd_apply_kernel, false, true, x, dy, gamma, beta, sh, stats, partial, dx);
-    else SKP_GN_B(gn_bwd_apply_kernel, false, false, x, dy, gamma, beta, sh, stats, partial, dx);
+    if (act) SKP_GN_B(gn_bwd_apply_kernel, false, true, x, dy, gamma, beta, shift, sh, stats, partial, dx);
+    else SKP_GN_B(gn_bwd_apply_kernel, false, false, x, dy, gamma, beta, shift, sh, stats, partial, dx);
   }
 #undef SKP_GN_B
+  SKP_LAUNCH_CHECK();
+  return SKP_OK;
+}
+
+extern "C" int skp_residual_bias_add(const float* a, const float* h, const float* bias, int B, int C, long long HW,
+                                     float* out, void* stream) {
+  SKP_CHECK_ARG(a && h && bias && out, "null pointer");
+  SKP_CHECK_ARG(B > 0 && C > 0 && HW > 0, "non-positive shape");
+  const long long total = (long long)B * C * HW;
+  const bool vec = (HW % 4 == 0) && ((reinterpret_cast<uintptr_t>(a) & 15) == 0) &&
+                   ((reinterpret_cast<uintptr_t>(h) & 15) == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
+  const long long units = vec ? total / 4 : total;
+  const int blocks = (int)std::min<long long>((units + kThreads - 1) / kThreads, 256LL * 16);
+  hipStream_t st = as_stream(stream);
+  if (vec) hipLaunchKernelGGL(residual_bias_kernel<true>, dim3(blocks), dim3(kThreads), 0, st, a, h, bias, C, HW, total, out);
+  else hipLaunchKernelGGL(residual_bias_kernel<false>, dim3(blocks), dim3(kThreads), 0, st, a, h, bias, C, HW, total, out);
   SKP_LAUNCH_CHECK();
   return SKP_OK;
 }

@@ -443,39 +443,70 @@ def equivariance_loss_single(A, At, theta_inv):
 
 # --------------------------------------------------------------------------- UNet-side GroupNorm(+SiLU)
 class GroupNormAct(torch.autograd.Function):
-    """y = act(GroupNorm(x)) with frozen affine parameters (dx only) — skp_groupnorm_fwd/bwd."""
+    """y = act(GroupNorm(x + shift)) with frozen affine parameters (dx only) — skp_groupnorm_fwd/bwd.
+    ``shift`` (B, C) or None: a per-(sample, channel) input offset (conv bias + time embedding)."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, groups, eps, act):
+    def forward(ctx, x, gamma, beta, groups, eps, act, shift):
         x = _c(x)
         B, C = x.shape[:2]
         HW = x[0, 0].numel()
         nws = _lib.lib().skp_groupnorm_workspace(B, C, HW, groups)
         if nws < 0:
             raise ValueError(f"groupnorm: bad shape {tuple(x.shape)} groups={groups}")
+        if shift is not None:
+            shift = _c(shift.detach().expand(B, C))
         part = torch.empty(nws, device=x.device, dtype=torch.float64)
         stats = torch.empty(B * groups * 2, device=x.device, dtype=F32)
         y = torch.empty_like(x)
         g, b = _c(gamma.detach()), _c(beta.detach())
-        call("skp_groupnorm_fwd", ptr(x), ptr(g), ptr(b), B, C, HW, int(groups), float(eps), int(act), ptr(y),
-             ptr(stats), ptr(part), stream(x.device))
-        ctx.save_for_backward(x, g, b, stats)
+        call("skp_groupnorm_fwd", ptr(x), ptr(g), ptr(b), ptr(shift), B, C, HW, int(groups), float(eps), int(act),
+             ptr(y), ptr(stats), ptr(part), stream(x.device))
+        ctx.save_for_backward(x, g, b, stats, shift)
         ctx.meta = (B, C, HW, int(groups), int(act), nws)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, g, b, stats = ctx.saved_tensors
+        x, g, b, stats, shift = ctx.saved_tensors
         B, C, HW, G, act, nws = ctx.meta
         dy = _c(dy)
         dx = torch.empty_like(x)
         part = torch.empty(nws, device=x.device, dtype=torch.float64)
-        call("skp_groupnorm_bwd", ptr(x), ptr(dy), ptr(g), ptr(b), ptr(stats), B, C, HW, G, act, ptr(dx), ptr(part),
-             stream(x.device))
-        return dx, None, None, None, None, None
+        call("skp_groupnorm_bwd", ptr(x), ptr(dy), ptr(g), ptr(b), ptr(shift), ptr(stats), B, C, HW, G, act, ptr(dx),
+             ptr(part), stream(x.device))
+        return dx, None, None, None, None, None, None
 
 
-def group_norm_act(x, gamma, beta, groups, eps, act):
-    """Fused GroupNorm (+SiLU when act) on the HIP device; frozen gamma/beta."""
+def group_norm_act(x, gamma, beta, groups, eps, act, shift=None):
+    """Fused GroupNorm(x + shift) (+SiLU when act) on the HIP device; frozen gamma/beta.
+    ``shift``: None or a (B, C) / (1, C) / (C,) per-channel input offset without gradient."""
     _lib.require_device(x)
-    return GroupNormAct.apply(x, gamma, beta, int(groups), float(eps), bool(act))
+    if shift is not None:
+        shift = shift.reshape(-1, x.shape[1]).to(x.device, F32)
+    return GroupNormAct.apply(x, gamma, beta, int(groups), float(eps), bool(act), shift)
+
+
+class ResidualBiasAdd(torch.autograd.Function):
+    """out = a + (h + bias[c]) (bias frozen): gradients pass through to a and h."""
+
+    @staticmethod
+    def forward(ctx, a, h, bias):
+        a, h = _c(a), _c(h)
+        B, C = a.shape[:2]
+        out = torch.empty_like(a)
+        call("skp_residual_bias_add", ptr(a), ptr(h), ptr(_c(bias.detach())), B, C, a[0, 0].numel(), ptr(out),
+             stream(a.device))
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, g, None
+
+
+def residual_bias_add(a, h, bias):
+    """a + (h + bias[:, None, None]) for NCHW a, h on the HIP device."""
+    _lib.require_device(a, h)
+    if a.shape != h.shape:
+        raise ValueError(f"residual_bias_add: shapes {tuple(a.shape)} and {tuple(h.shape)} differ")
+    return ResidualBiasAdd.apply(a, h, bias)

@@ -35,12 +35,20 @@ class CaptureComplete(Exception):
 USE_FUSED_GROUPNORM = True
 
 
-def gn_act(norm, x, act):
-    """act(norm(x)) for an nn.GroupNorm ``norm``: on the HIP device the fused libskp kernel
-    (frozen affine parameters, input gradient only); elsewhere plain torch."""
-    if USE_FUSED_GROUPNORM and x.is_cuda and not (norm.weight.requires_grad or norm.bias.requires_grad):
+def _fused(x, *modules):
+    """The libskp UNet-side kernels apply: HIP tensor, frozen parameters."""
+    return USE_FUSED_GROUPNORM and x.is_cuda and not any(p.requires_grad for m in modules for p in m.parameters())
+
+
+def gn_act(norm, x, act, shift=None):
+    """act(norm(x + shift)) for an nn.GroupNorm ``norm`` (``shift``: None or a per-(sample,
+    channel) offset (B or 1, C)): on the HIP device the fused libskp kernel (frozen affine
+    parameters, input gradient only, shift folded into its loads); elsewhere plain torch."""
+    if _fused(x, norm):
         from .. import ops
-        return ops.group_norm_act(x, norm.weight, norm.bias, norm.num_groups, norm.eps, act)
+        return ops.group_norm_act(x, norm.weight, norm.bias, norm.num_groups, norm.eps, act, shift)
+    if shift is not None:
+        x = x + shift.reshape(-1, x.shape[1], 1, 1)
     y = norm(x)
     return F.silu(y) if act else y
 
@@ -174,6 +182,18 @@ class ResnetBlock2D(nn.Module):
         self.conv_shortcut = nn.Conv2d(in_channels, out_channels, 1) if in_channels != out_channels else None
 
     def forward(self, x, temb=None):
+        if _fused(x, self.conv1, self.conv2, self.norm2):
+            # conv1's bias and the time embedding enter norm2 as its input shift, conv2's bias
+            # the residual add: neither is a separate pass over the activations
+            h = F.conv2d(gn_act(self.norm1, x, True), self.conv1.weight, None, 1, 1)
+            shift = self.conv1.bias[None]
+            if temb is not None and self.time_emb_proj is not None:
+                shift = shift + self.time_emb_proj(F.silu(temb))
+            h = F.conv2d(self.dropout(gn_act(self.norm2, h, True, shift)), self.conv2.weight, None, 1, 1)
+            if self.conv_shortcut is not None:
+                x = self.conv_shortcut(x)
+            from .. import ops
+            return ops.residual_bias_add(x, h, self.conv2.bias)
         h = self.conv1(gn_act(self.norm1, x, True))
         if temb is not None and self.time_emb_proj is not None:
             h = h + self.time_emb_proj(F.silu(temb))[:, :, None, None]

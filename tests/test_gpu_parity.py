@@ -357,30 +357,47 @@ def test_batched_captures_match_sequential_tiny():
 
 
 # ----------------------------------------------------------------------------- UNet-side GroupNorm(+SiLU)
-@pytest.mark.parametrize("B,C,H,W,G,act", [(2, 320, 64, 64, 32, True), (2, 1280, 8, 8, 32, False),
-                                           (1, 128, 256, 256, 32, True), (2, 12, 5, 7, 4, True),
-                                           (1, 64, 16, 16, 8, False)])
-def test_groupnorm_act_vs_torch_fp64(B, C, H, W, G, act):
-    """Fused GroupNorm(+SiLU) fwd and input-gradient vs a torch fp64 reference."""
+@pytest.mark.parametrize("B,C,H,W,G,act,shifted", [(2, 320, 64, 64, 32, True, True), (2, 1280, 8, 8, 32, False, False),
+                                                   (1, 128, 256, 256, 32, True, False), (2, 12, 5, 7, 4, True, True),
+                                                   (1, 64, 16, 16, 8, False, True)])
+def test_groupnorm_act_vs_torch_fp64(B, C, H, W, G, act, shifted):
+    """Fused GroupNorm(x + shift)(+SiLU) fwd and input-gradient vs a torch fp64 reference."""
     import torch.nn.functional as F
     from stablekeypoints_amd import ops
     g = torch.Generator().manual_seed(C + H)
     x = (torch.randn(B, C, H, W, generator=g) * 3 + 1).to(DEV).requires_grad_(True)
     gamma = torch.randn(C, generator=g).to(DEV)
     beta = torch.randn(C, generator=g).to(DEV)
-    y = ops.group_norm_act(x, gamma, beta, G, 1e-5, act)
+    shift = (torch.randn(B, C, generator=g) * 2).to(DEV) if shifted else None
+    y = ops.group_norm_act(x, gamma, beta, G, 1e-5, act, shift)
     dy = torch.randn(B, C, H, W, generator=g).to(DEV)
     (y * dy).sum().backward()
     xd = x.detach().double().requires_grad_(True)
-    yr = F.group_norm(xd, G, gamma.double(), beta.double(), 1e-5)
+    xs = xd + shift.double()[:, :, None, None] if shifted else xd
+    yr = F.group_norm(xs, G, gamma.double(), beta.double(), 1e-5)
     yr = F.silu(yr) if act else yr
     (yr * dy.double()).sum().backward()
     assert (y.double() - yr).abs().max().item() < 2e-5
     assert (x.grad.double() - xd.grad).abs().max().item() < 2e-4 * max(1.0, xd.grad.abs().max().item())
 
 
+def test_residual_bias_add_bitexact():
+    """a + (h + bias[c]) equals torch's two adds bit for bit; gradients pass through."""
+    from stablekeypoints_amd import ops
+    g = torch.Generator().manual_seed(9)
+    for shape in ((2, 320, 64, 64), (2, 12, 5, 7)):
+        a = torch.randn(*shape, generator=g).to(DEV).requires_grad_(True)
+        h = torch.randn(*shape, generator=g).to(DEV).requires_grad_(True)
+        b = torch.randn(shape[1], generator=g).to(DEV)
+        out = ops.residual_bias_add(a, h, b)
+        assert torch.equal(out, a + (h + b[:, None, None]))
+        out.sum().backward()
+        assert torch.equal(a.grad, torch.ones_like(a)) and torch.equal(h.grad, torch.ones_like(h))
+
+
 def test_unet_fused_groupnorm_matches_torch_groupnorm():
-    """The SD UNet forward/backward with the fused GroupNorm equals the plain-torch one."""
+    """The SD UNet forward/backward with the fused GroupNorm (+ folded conv biases / time
+    embedding, fused residual+bias) equals the plain-torch one."""
     from stablekeypoints_amd.sd import build_sd15, TINY_CONFIG, unet as unet_mod
     ldm = build_sd15(seed=0, config=TINY_CONFIG, device=DEV)
     lat = torch.randn(2, 4, 16, 16, device=DEV, generator=torch.Generator(device=DEV).manual_seed(0))

@@ -16,8 +16,14 @@ img = SyntheticDataset(n=2, size=512)[0]["img"][None].to(dev)
 for _ in range(3):
     opt.micro_step(img)
 torch.cuda.synchronize()
-with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+import sys as _s
+shapes = "--shapes" in _s.argv
+with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=shapes) as prof:
     for _ in range(2):
         opt.micro_step(img)
     torch.cuda.synchronize()
-print(prof.key_averages().table(sort_by="self_cuda_time_total", row_limit=45, max_name_column_width=60))
+if shapes:
+    print(prof.key_averages(group_by_input_shape=True).table(sort_by="self_cuda_time_total", row_limit=70,
+                                                             max_name_column_width=40, max_shapes_column_width=80))
+else:
+    print(prof.key_averages().table(sort_by="self_cuda_time_total", row_limit=45, max_name_column_width=60))
