@@ -55,8 +55,11 @@ def test_bgemm_layout_identity_asymmetric():
 
 # ----------------------------------------------------------------------------- A1 capture
 @pytest.mark.parametrize("H,s,R,Nn", [(8, 4, 32, 16), (8, 8, 32, 16), (2, 16, 128, 500), (2, 32, 128, 500),
-                                      (3, 5, 13, 70), (1, 16, 128, 1)])
+                                      (3, 5, 13, 70), (1, 16, 128, 1), (1, 16, 256, 40), (1, 8, 32, 1000),
+                                      (2, 1, 8, 20), (1, 32, 16, 9)])
 def test_capture_fwd_vs_oracle(H, s, R, Nn):
+    """Includes R=256 (the reference's default feature_upsample_res), N=1000 (its default token
+    count, two tokens per lane), a 1×1 low-res layer and a downsampling R < s."""
     from stablekeypoints_amd import ops
     z = recipes.random_logits(H * 1000 + s, (H, s * s, Nn), scale=3.0)
     got = N(ops.capture_attn(T(z), s, R))
@@ -66,7 +69,8 @@ def test_capture_fwd_vs_oracle(H, s, R, Nn):
     assert np.allclose(got.sum(-1), 1.0, atol=1e-5)
 
 
-@pytest.mark.parametrize("H,s,R,Nn", [(8, 4, 32, 16), (2, 16, 128, 500), (2, 32, 128, 300), (3, 5, 13, 70)])
+@pytest.mark.parametrize("H,s,R,Nn", [(8, 4, 32, 16), (2, 16, 128, 500), (2, 32, 128, 300), (3, 5, 13, 70),
+                                      (1, 16, 256, 40), (1, 8, 32, 1000), (2, 1, 8, 20), (1, 32, 16, 9)])
 def test_capture_bwd_dense_and_broadcast(H, s, R, Nn):
     from stablekeypoints_amd import ops
     z = recipes.random_logits(7 + s, (H, s * s, Nn), scale=2.0)
