@@ -23,7 +23,13 @@ with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_sh
         opt.micro_step(img)
     torch.cuda.synchronize()
 if shapes:
-    print(prof.key_averages(group_by_input_shape=True).table(sort_by="self_cuda_time_total", row_limit=70,
-                                                             max_name_column_width=40, max_shapes_column_width=80))
+    rows = []
+    for e in prof.key_averages(group_by_input_shape=True):
+        t = getattr(e, "self_device_time_total", 0) or getattr(e, "self_cuda_time_total", 0)
+        if e.key.startswith("aten::") and t > 0:
+            rows.append((t, e.key, e.count, str(e.input_shapes)[:150]))
+    rows.sort(reverse=True)
+    for t, k, n, sh in rows[:120]:
+        print(f"{t / 1e3:8.3f} ms {n:5d} {k:36s} {sh}")
 else:
     print(prof.key_averages().table(sort_by="self_cuda_time_total", row_limit=45, max_name_column_width=60))
