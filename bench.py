@@ -211,6 +211,8 @@ def main():
     ap.add_argument("--conv-benchmark", type=int, default=0, help="torch.backends.cudnn.benchmark (MIOpen exhaustive find)")
     ap.add_argument("--attn-backend", default="math", choices=["math", "sdpa"],
                     help="un-captured UNet attention: explicit fp32 GEMM+softmax (math) or torch SDPA")
+    ap.add_argument("--micro-batch", type=int, default=0,
+                    help="images per VAE/UNet pass (0 = all `accum` images of an optimiser step in one pass)")
     ap.add_argument("--gc-freeze", type=int, default=1, help="gc.freeze() after the model is built (host overhead)")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
                     help="JSON with PMC-derived HBM bytes per launch of the roofline kernel")
@@ -250,10 +252,15 @@ def main():
 
     counter = [0]
 
+    mb = args.micro_batch if args.micro_batch > 0 else args.accum
+
     def step():
-        for _ in range(args.accum):
-            opt.micro_step(imgs[counter[0] % len(imgs)])
-            counter[0] += 1
+        done = 0
+        while done < args.accum:
+            n = min(mb, args.accum - done)
+            opt.micro_steps([imgs[(counter[0] + i) % len(imgs)] for i in range(n)])
+            counter[0] += n
+            done += n
         return opt.optimizer_step()
 
     def barrier():
@@ -314,9 +321,11 @@ def main():
                "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
                "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded torch.rand 512² images, random-init SD-1.5)",
                "config": {"workload": "CelebA-wild-shaped 512², N=500 tokens, SD-1.5 fp32, feature_upsample_res=128, "
-                                      "batch_size 4 per GPU (BASELINE.json configs[1])",
+                                      "batch_size 4 per GPU (BASELINE.json configs[1]); the 4 images and their warps "
+                                      "in one VAE/UNet pass of 8",
                           "global_batch": world * args.accum, "tokens": args.tokens, "image_res": args.res,
-                          "feature_upsample_res": args.upsample_res, "parallelism": f"dp{world} (RCCL grad all-reduce)"},
+                          "feature_upsample_res": args.upsample_res, "micro_batch": mb,
+                          "parallelism": f"dp{world} (RCCL grad all-reduce)"},
                "roofline": roof, "cpu_baseline": cpu, "kernels": extra,
                "last_loss": float(rec["loss"])}
         print(json.dumps(out), flush=True)

@@ -142,11 +142,42 @@ class TokenOptimizer:
     def micro_step(self, image):
         """One reference micro-iteration on ``image`` (1, 3, H, W): loss, backward, running stats."""
         loss, eq, sh, idx = self.image_loss(image)
+        self._account(loss, eq, sh)
+        (loss / self.accum).backward()
+        return idx
+
+    def _account(self, loss, eq, sh):
         self.run_eq = self.run_eq + eq.detach() / self.accum * self.w_eq
         self.run_sh = self.run_sh + sh.detach() / self.accum * self.w_sharp
         self.run_tot = self.run_tot + loss.detach() / self.accum
-        (loss / self.accum).backward()
-        return idx
+
+    def micro_steps(self, images):
+        """``len(images)`` reference micro-iterations in ONE VAE/UNet pass of batch 2·k (every
+        image and its warp) and ONE backward.
+
+        The micro-iterations of an optimiser step are independent given the shared context
+        (optimize.py:362-445 sums their gradients before Adam), so this equals k ``micro_step``
+        calls up to fp32 summation order: the thetas are drawn in the same order from the CPU
+        generator, and the selection and losses stay per image.  A batch of 2·k images fills
+        the 256 CUs far better than k passes of 2 (the UNet's 64²-and-smaller convolutions and
+        GEMMs are too small at batch 2).  Returns the per-image selected token indices.
+        """
+        if not self.batch_captures or len(images) == 1:
+            return [self.micro_step(img) for img in images]
+        k = len(images)
+        batch = torch.cat(list(images))
+        transformed = self.transform(batch)              # draws k thetas, image order
+        maps = ptp_utils.run_and_find_attn_per_image(
+            self.ldm, torch.cat([batch, transformed]), self.context, noise_level=self.kw["noise_level"],
+            device=self.device, layers=self.kw["layers"], controllers=self.controllers)[0]
+        total, out = 0.0, []
+        for i in range(k):
+            loss, eq, sh, idx = self._map_loss(maps[i], maps[k + i], i)
+            self._account(loss, eq, sh)
+            total = total + loss
+            out.append(idx)
+        (total / self.accum).backward()
+        return out
 
     def image_loss(self, image):
         """optimize.py:372-437 for one image: (weighted loss, equivariance, sharpening, indices)."""
@@ -160,6 +191,10 @@ class TokenOptimizer:
             transformed_img = self.transform(image)
             attention_map_transformed = ptp_utils.run_and_find_attn(self.ldm, transformed_img, self.context,
                                                                      **self.kw)[0]
+        return self._map_loss(attn_map, attention_map_transformed, 0)
+
+    def _map_loss(self, attn_map, attention_map_transformed, index):
+        """optimize.py:403-437 for one image's maps; ``index`` selects its theta in ``self.transform``."""
         if self.top_k_strategy == "entropy":
             cand = ptp_utils.entropy_sort(attn_map, self.fps_n)
         elif self.top_k_strategy == "gaussian":
@@ -170,7 +205,8 @@ class TokenOptimizer:
             raise NotImplementedError
         idx = ptp_utils.furthest_point_sampling(attention_map_transformed, self.top_k, cand)
         sh = sharpening_loss(attn_map[idx], device=self.device, sigma=self.sigma, num_subjects=self.num_subjects)
-        eq = equivariance_loss(attn_map[idx], attention_map_transformed[idx][None], self.transform, 0)
+        # a (T, h, w) map: this image's warp is theta ``index`` of self.transform
+        eq = equivariance_loss(attn_map[idx], attention_map_transformed[idx], self.transform, index)
         loss = eq * self.w_eq + sh * self.w_sharp
         return loss, eq, sh, idx
 
@@ -220,14 +256,18 @@ def optimize_embedding(ldm, top_k_strategy="entropy", wandb_log=True, context=No
     sampler_gen = torch.Generator().manual_seed(base + rank)
     order = torch.randperm(len(dataset), generator=sampler_gen)
     pos = 0
-    start = it_start = time.time()
+    start = time.time()
+    it_start = time.time()
+    pending = []
     for iteration in range(n_iter):
         if pos >= len(order):
             order = torch.randperm(len(dataset), generator=sampler_gen)
             pos = 0
-        image = dataset[int(order[pos])]["img"][None].to(device, non_blocking=True)
+        pending.append(dataset[int(order[pos])]["img"][None].to(device, non_blocking=True))
         pos += 1
-        opt.micro_step(image)
+        if (iteration + 1) % accum == 0 or iteration + 1 == n_iter:
+            opt.micro_steps(pending)   # the optimiser step's images in one VAE/UNet pass
+            pending = []
         if (iteration + 1) % accum == 0:
             rec = {k: float(v) for k, v in opt.optimizer_step().items()}
             rec["iteration time"] = time.time() - it_start

@@ -360,6 +360,50 @@ def test_batched_captures_match_sequential_tiny():
     assert np.allclose(res[False][2], res[True][2], rtol=1e-3, atol=1e-8)
 
 
+def test_micro_steps_batch_equals_sequential_micro_steps():
+    """TokenOptimizer.micro_steps (k images + k warps in ONE pass of 2k, one backward) equals k
+    micro_step calls: same indices, loss statistics and context gradient (same noises/thetas)."""
+    from stablekeypoints_amd.optimize import TokenOptimizer
+    from stablekeypoints_amd.optimize_token import load_ldm
+    from stablekeypoints_amd.sd import TINY_CONFIG, TINY_IMAGE
+    k = 3
+    lat = TINY_IMAGE // 8
+    nI = [torch.randn(1, 4, lat, lat, generator=torch.Generator().manual_seed(10 + i)).to(DEV) for i in range(k)]
+    nT = [torch.randn(1, 4, lat, lat, generator=torch.Generator().manual_seed(20 + i)).to(DEV) for i in range(k)]
+    thetas = torch.tensor([[[0.88, -0.14, -0.2], [0.14, 0.88, 0.19]], [[0.95, 0.1, 0.05], [-0.1, 0.95, -0.1]],
+                           [[0.8, 0.0, 0.1], [0.0, 0.8, 0.0]]])
+    imgs = [torch.from_numpy(recipes.uniform(60 + i, (1, 3, TINY_IMAGE, TINY_IMAGE))).to(DEV) for i in range(k)]
+    res = {}
+    for batched in (False, True):
+        ldm, ctls, _ = load_ldm(DEV, "tiny", feature_upsample_res=32, config=TINY_CONFIG)
+        inner = ldm.scheduler
+        cur = {}
+
+        class Sched:
+            timesteps = inner.timesteps
+
+            def add_noise(self, x, noise, t):
+                return inner.add_noise(x, cur["noise"], t)
+        ldm.scheduler = Sched()
+        ctx = torch.from_numpy(recipes.random_logits(52, (1, 16, 32))).to(DEV)
+        opt = TokenOptimizer(ldm, ctls, ctx, top_k=4, furthest_point_num_samples=8, accum=k, device=DEV)
+        if batched:
+            cur["noise"] = torch.cat(nI + nT)
+            opt.transform.draw_theta = lambda batch: thetas[:batch]
+            idx = opt.micro_steps(imgs)
+        else:
+            idx = []
+            for i in range(k):
+                cur["noise"] = torch.cat([nI[i], nT[i]])
+                opt.transform.draw_theta = lambda batch, i=i: thetas[i:i + 1]
+                idx.append(opt.micro_step(imgs[i]))
+        res[batched] = ([N(t) for t in idx], float(opt.run_tot), N(opt.context.grad))
+    for a, b in zip(res[False][0], res[True][0]):
+        assert np.array_equal(a, b)
+    assert abs(res[False][1] - res[True][1]) < 1e-5 * abs(res[False][1])
+    assert np.allclose(res[False][2], res[True][2], rtol=1e-3, atol=1e-8)
+
+
 # ----------------------------------------------------------------------------- UNet-side GroupNorm(+SiLU)
 @pytest.mark.parametrize("B,C,H,W,G,act,shifted", [(2, 320, 64, 64, 32, True, True), (2, 1280, 8, 8, 32, False, False),
                                                    (1, 128, 256, 256, 32, True, False), (2, 12, 5, 7, 4, True, True),
