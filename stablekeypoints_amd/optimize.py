@@ -169,15 +169,22 @@ class TokenOptimizer:
         transformed = self.transform(batch)              # draws k thetas, image order
         maps = ptp_utils.run_and_find_attn_per_image(
             self.ldm, torch.cat([batch, transformed]), self.context, noise_level=self.kw["noise_level"],
-            device=self.device, layers=self.kw["layers"], controllers=self.controllers)[0]
-        total, out = 0.0, []
-        for i in range(k):
-            loss, eq, sh, idx = self._map_loss(maps[i], maps[k + i], i)
+            device=self.device, layers=self.kw["layers"], controllers=self.controllers, stacked=True)[0]
+        sel = [self._select(maps[i], maps[k + i]) for i in range(k)]
+        # one gather of every image's selected rows (its backward is one scatter into the
+        # (2k, N, R, R) map gradient instead of 2k full-size zero-fills and adds)
+        img = torch.cat([torch.full_like(idx, i) for i, idx in enumerate(sel)])
+        tok = torch.cat(sel)
+        A, At = maps[img, tok], maps[img + k, tok]
+        total, off = 0.0, 0
+        for i, idx in enumerate(sel):
+            n = idx.numel()
+            loss, eq, sh = self._losses(A[off:off + n], At[off:off + n], i)
+            off += n
             self._account(loss, eq, sh)
             total = total + loss
-            out.append(idx)
         (total / self.accum).backward()
-        return out
+        return sel
 
     def image_loss(self, image):
         """optimize.py:372-437 for one image: (weighted loss, equivariance, sharpening, indices)."""
@@ -195,6 +202,12 @@ class TokenOptimizer:
 
     def _map_loss(self, attn_map, attention_map_transformed, index):
         """optimize.py:403-437 for one image's maps; ``index`` selects its theta in ``self.transform``."""
+        idx = self._select(attn_map, attention_map_transformed)
+        loss, eq, sh = self._losses(attn_map[idx], attention_map_transformed[idx], index)
+        return loss, eq, sh, idx
+
+    def _select(self, attn_map, attention_map_transformed):
+        """optimize.py:403-424: top-k candidates on the image's map, FPS on its warp's map."""
         if self.top_k_strategy == "entropy":
             cand = ptp_utils.entropy_sort(attn_map, self.fps_n)
         elif self.top_k_strategy == "gaussian":
@@ -203,12 +216,14 @@ class TokenOptimizer:
             cand = torch.arange(self.fps_n, device=attn_map.device)
         else:
             raise NotImplementedError
-        idx = ptp_utils.furthest_point_sampling(attention_map_transformed, self.top_k, cand)
-        sh = sharpening_loss(attn_map[idx], device=self.device, sigma=self.sigma, num_subjects=self.num_subjects)
-        # a (T, h, w) map: this image's warp is theta ``index`` of self.transform
-        eq = equivariance_loss(attn_map[idx], attention_map_transformed[idx], self.transform, index)
+        return ptp_utils.furthest_point_sampling(attention_map_transformed, self.top_k, cand)
+
+    def _losses(self, A, At, index):
+        """optimize.py:425-437 on the selected rows; ``index`` selects the warp's theta."""
+        sh = sharpening_loss(A, device=self.device, sigma=self.sigma, num_subjects=self.num_subjects)
+        eq = equivariance_loss(A, At, self.transform, index)   # (T, h, w): theta ``index``
         loss = eq * self.w_eq + sh * self.w_sharp
-        return loss, eq, sh, idx
+        return loss, eq, sh
 
     def optimizer_step(self):
         if self.world > 1:

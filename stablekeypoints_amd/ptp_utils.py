@@ -253,14 +253,16 @@ def run_and_find_attn(ldm, image, context, noise_level=-1, device="cuda",
 
 
 def run_and_find_attn_per_image(ldm, images, context, noise_level=-1, device="cuda", layers=(0, 1, 2, 3),
-                                upsample_res=-1, indices=None, controllers=None):
+                                upsample_res=-1, indices=None, controllers=None, stacked=False):
     """Batched capture: ONE VAE + UNet pass over B images, maps aggregated PER IMAGE.
 
     Equivalent to B calls of ``run_and_find_attn`` with one image each (every UNet/VAE op is
     per-sample; each image gets its own noise draw), but at batch B on the GPU.  The
     reference's ``collect_maps`` averages over B·heads (optimize.py:75), which would mix
     images at B > 1, so each image's (H, R², N) slice of the stored layers is aggregated
-    separately.  Returns a list (per controller) of lists (per image) of (N', R', R') maps.
+    separately.  Returns a list (per controller) of lists (per image) of (N', R', R') maps;
+    with ``stacked`` (logit store, no ``indices``/``upsample_res``) one (B, N, R, R) tensor per
+    controller instead, so callers can gather rows of several images in one autograd op.
     """
     find_pred_noise(ldm, images, context, noise_level=noise_level, device=device)
     B = images.shape[0]
@@ -269,6 +271,10 @@ def run_and_find_attn_per_image(ldm, images, context, noise_level=-1, device="cu
         ctl = controllers[key]
         if getattr(ctl, "stores_logits", False):
             maps = ctl.maps_per_image(B, ldm.feature_upsample_res, layers)
+            if stacked and indices is None and upsample_res in (-1, maps.shape[-1]):
+                out.append(maps)
+                ctl.reset()
+                continue
             res = []
             for b in range(B):
                 m = maps[b]

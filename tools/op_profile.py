@@ -12,15 +12,14 @@ ldm, ctls, _ = load_ldm(dev, "random", feature_upsample_res=128)
 torch.manual_seed(0)
 ctx = torch.randn(1, 500, 768).to(dev)
 opt = TokenOptimizer(ldm, ctls, ctx, accum=4, device=dev)
-img = SyntheticDataset(n=2, size=512)[0]["img"][None].to(dev)
-for _ in range(3):
-    opt.micro_step(img)
+imgs = [SyntheticDataset(n=4, size=512)[i]["img"][None].to(dev) for i in range(4)]
+for _ in range(2):
+    opt.micro_steps(imgs)
 torch.cuda.synchronize()
 import sys as _s
 shapes = "--shapes" in _s.argv
 with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=shapes) as prof:
-    for _ in range(2):
-        opt.micro_step(img)
+    opt.micro_steps(imgs)   # one optimiser step's 4 images in one batch-8 pass
     torch.cuda.synchronize()
 if shapes:
     rows = []
