@@ -25,17 +25,18 @@ def main():
     ap.add_argument("--benchmark", action="store_true")
     ap.add_argument("--channels-last", action="store_true")
     ap.add_argument("--bwd", action="store_true")
+    ap.add_argument("--batch", type=int, default=2)
     args = ap.parse_args()
     torch.backends.cudnn.benchmark = args.benchmark
     dev = "cuda:0"
     for (hw, c) in [(64, 320), (32, 640), (16, 1280), (64, 640), (128, 512), (256, 256)]:
-        x = torch.randn(2, c, hw, hw, device=dev)
+        x = torch.randn(args.batch, c, hw, hw, device=dev)
         w = torch.randn(c, c, 3, 3, device=dev) * 0.02
         bias = torch.randn(c, device=dev)
         if args.channels_last:
             x = x.contiguous(memory_format=torch.channels_last)
             w = w.contiguous(memory_format=torch.channels_last)
-        fl = 2 * 2 * hw * hw * c * c * 9
+        fl = 2 * args.batch * hw * hw * c * c * 9
         t = timed(lambda: F.conv2d(x, w, bias, padding=1))
         line = f"fwd {hw:4d}^2 c={c:5d}: {t * 1e3:8.1f} us  {fl / (t * 1e-3) / 1e12:6.1f} TF/s"
         if args.bwd:

@@ -7,6 +7,9 @@ token-opt micro-iterations at the one-per-micro-step `sort_topk_kernel`, keeps t
 `--micro` micro-iterations (the timed steps × accum) and prints/writes per-kernel totals.
 
 usage: python tools/prof_summary.py TRACE.csv --micro 8 [--out summary.csv]
+       python tools/prof_summary.py TRACE.csv --steps 2 --accum 4   # split at the Adam kernels
+(with batched micro-steps the per-image marker no longer bounds the timed region; the
+optimiser step's multi_tensor_apply kernels do)
 """
 import argparse
 import csv
@@ -16,18 +19,33 @@ import collections
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
-    ap.add_argument("--micro", type=int, required=True, help="micro-iterations in the timed region")
+    ap.add_argument("--micro", type=int, default=0, help="micro-iterations in the timed region")
+    ap.add_argument("--steps", type=int, default=0, help="optimiser steps in the timed region (Adam marker)")
+    ap.add_argument("--accum", type=int, default=4, help="images per optimiser step (with --steps)")
     ap.add_argument("--marker", default="sort_topk_kernel")
     ap.add_argument("--out", default=None)
     ap.add_argument("--top", type=int, default=30)
     args = ap.parse_args()
     rows = list(csv.DictReader(open(args.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    marks = [i for i, r in enumerate(rows) if args.marker in r["Kernel_Name"]]
-    if len(marks) < args.micro + 1:
-        raise SystemExit(f"only {len(marks)} markers for {args.micro} micro-iterations")
-    # the timed region starts right after the marker that ends the last warm-up micro-iteration
-    start = marks[-args.micro - 1] + 1
+    if args.steps:
+        adam = [i for i, r in enumerate(rows) if "multi_tensor_apply" in r["Kernel_Name"]]
+        groups = []   # consecutive Adam kernels of one optimiser step
+        for i in adam:
+            if groups and i - groups[-1][-1] <= 16:
+                groups[-1].append(i)
+            else:
+                groups.append([i])
+        if len(groups) < args.steps + 1:
+            raise SystemExit(f"only {len(groups)} optimiser steps for {args.steps}")
+        start = groups[-args.steps - 1][-1] + 1
+        args.micro = args.steps * args.accum
+    else:
+        marks = [i for i, r in enumerate(rows) if args.marker in r["Kernel_Name"]]
+        if len(marks) < args.micro + 1:
+            raise SystemExit(f"only {len(marks)} markers for {args.micro} micro-iterations")
+        # the timed region starts right after the marker that ends the last warm-up micro-iteration
+        start = marks[-args.micro - 1] + 1
     sel = rows[start:]
     t0 = int(sel[0]["Start_Timestamp"])
     t1 = int(sel[-1]["End_Timestamp"])
