@@ -69,17 +69,17 @@ def main():
             dst = torch.empty_like(big)
             res[name] = timed(lambda: dst.copy_(big), args.iters)
             res[name + "_GBs"] = 2 * big.numel() * 4 / (res[name] * 1e-3) / 1e9 / 1e3
-        elif name.startswith("gemm"):   # capture logits q kᵀ and its two gradients at s=16/32
+        elif name.startswith("gemm"):   # capture logits q kᵀ and its two gradients at s=16/32, bench batch 8
             sz = 16 if name.endswith("16") else 32
             d = 160 if sz == 16 else 80
-            q = torch.randn(2 * H, sz * sz, d, device=dev, generator=g)
-            k = torch.randn(2 * H, N, d, device=dev, generator=g)
-            dz = torch.randn(2 * H, sz * sz, N, device=dev, generator=g)
+            q = torch.randn(8 * H, sz * sz, d, device=dev, generator=g)
+            k = torch.randn(8 * H, N, d, device=dev, generator=g)
+            dz = torch.randn(8 * H, sz * sz, N, device=dev, generator=g)
             t_f = timed(lambda: ops.bgemm(q, k.transpose(1, 2), 0.1), args.iters)
             t_q = timed(lambda: ops.bgemm(dz, k, 0.1), args.iters)
             t_k = timed(lambda: ops.bgemm(dz.transpose(1, 2), q, 0.1), args.iters)
             t_ref = timed(lambda: torch.bmm(q, k.transpose(1, 2)), args.iters)
-            fl = 2 * 2 * H * sz * sz * N * d
+            fl = 2 * 8 * H * sz * sz * N * d
             for nm, t in (("fwd", t_f), ("dq", t_q), ("dk", t_k), ("torch_fwd", t_ref)):
                 res[f"{name}_{nm}"] = t
                 res[f"{name}_{nm}_TFs"] = fl / (t * 1e-3) / 1e12 / 1e3
