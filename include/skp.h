@@ -158,6 +158,10 @@ int skp_groupnorm_fwd(const float* x, const float* gamma, const float* beta, con
 int skp_groupnorm_bwd(const float* x, const float* dy, const float* gamma, const float* beta, const float* shift,
                       const float* stats, int B, int C, long long HW, int G, int act, float* dx, double* partial,
                       void* stream);
+/* Softmax backward of the UNet's math attention (diffusers-0.8.0 CrossAttention,
+ * softmax(q kᵀ·scale) v): per row of P (rows × cols), dS = alpha·P ⊙ (dP − Σ P ⊙ dP),
+ * written over dP (alpha = the logits' scale, baddbmm's backward folded in).  cols ≤ 16384. */
+int skp_softmax_bwd(const float* P, float* dP, long long rows, int cols, float alpha, void* stream);
 /* out = a + (h + bias[c]) over (B, C, HW): diffusers ResnetBlock2D `x + conv2(...)` with the
  * convolution's bias folded into the residual add (same rounding order).         */
 int skp_residual_bias_add(const float* a, const float* h, const float* bias, int B, int C, long long HW,

@@ -41,6 +41,7 @@ _SIGS = {
     "skp_groupnorm_fwd": [_p, _p, _p, _p, _c_int, _c_int, _c_ll, _c_int, _c_float, _c_int, _p, _p, _p, _p],
     "skp_groupnorm_bwd": [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_ll, _c_int, _c_int, _p, _p, _p],
     "skp_residual_bias_add": [_p, _p, _p, _c_int, _c_int, _c_ll, _p, _p],
+    "skp_softmax_bwd": [_p, _p, _c_ll, _c_int, _c_float, _p],
     "skp_version": [],
 }
 

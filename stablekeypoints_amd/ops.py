@@ -510,3 +510,39 @@ def residual_bias_add(a, h, bias):
     if a.shape != h.shape:
         raise ValueError(f"residual_bias_add: shapes {tuple(a.shape)} and {tuple(h.shape)} differ")
     return ResidualBiasAdd.apply(a, h, bias)
+
+
+class MathAttention(torch.autograd.Function):
+    """softmax(q kᵀ·scale) v over (B·H, S, D) (diffusers-0.8.0 math path): hipBLASLt GEMMs and
+    torch softmax forward; the backward's softmax gradient (with baddbmm's scale folded in) is
+    one skp_softmax_bwd pass written over dP."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, scale):
+        sim = torch.baddbmm(torch.empty(q.shape[0], q.shape[1], k.shape[1], dtype=q.dtype, device=q.device),
+                            q, k.transpose(1, 2), beta=0, alpha=scale)
+        p = sim.softmax(dim=-1)
+        del sim
+        ctx.save_for_backward(q, k, v, p)
+        ctx.scale = scale
+        return torch.bmm(p, v)
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, k, v, p = ctx.saved_tensors
+        dout = dout.contiguous()
+        dv = torch.bmm(p.transpose(1, 2), dout) if ctx.needs_input_grad[2] else None
+        dq = dk = None
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+            ds = torch.bmm(dout, v.transpose(1, 2))                 # dP, overwritten by scale·dS
+            call("skp_softmax_bwd", ptr(p), ptr(ds), p.shape[0] * p.shape[1], p.shape[2], float(ctx.scale),
+                 stream(p.device))
+            dq = torch.bmm(ds, k) if ctx.needs_input_grad[0] else None
+            dk = torch.bmm(ds.transpose(1, 2), q) if ctx.needs_input_grad[1] else None
+        return dq, dk, dv, None
+
+
+def math_attention(q, k, v, scale):
+    """softmax(q kᵀ·scale) v with the fused softmax backward (HIP device)."""
+    _lib.require_device(q, k, v)
+    return MathAttention.apply(q, k, v, float(scale))

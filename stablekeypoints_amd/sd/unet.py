@@ -31,7 +31,10 @@ class CaptureComplete(Exception):
     """
 
 
-# --------------------------------------------------------------------------- fused GroupNorm(+SiLU)
+# --------------------------------------------------------------------------- libskp UNet-side kernels
+# GroupNorm(+SiLU) with folded conv bias / time embedding, residual + bias, and the attention's
+# fused softmax backward run on libskp when True (HIP tensors, frozen parameters); False is the
+# plain-torch model (the tests compare the two).
 USE_FUSED_GROUPNORM = True
 
 
@@ -96,6 +99,10 @@ def attention_core(q, k, v, scale, mask=None, heads=1):
     """softmax(q kᵀ · scale) v over (B·H, S, D) tensors (diffusers-0.8.0 semantics)."""
     if mask is None and CrossAttention.backend == "sdpa":
         return F.scaled_dot_product_attention(q.unsqueeze(0), k.unsqueeze(0), v.unsqueeze(0), scale=scale)[0]
+    if mask is None and USE_FUSED_GROUPNORM and q.is_cuda and torch.is_grad_enabled() and \
+            (q.requires_grad or k.requires_grad or v.requires_grad):
+        from .. import ops   # same forward; one fused pass for the softmax backward
+        return ops.math_attention(q, k, v, scale)
     sim = torch.baddbmm(torch.empty(q.shape[0], q.shape[1], k.shape[1], dtype=q.dtype, device=q.device),
                         q, k.transpose(1, 2), beta=0, alpha=scale)
     if mask is not None:

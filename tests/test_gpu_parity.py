@@ -429,6 +429,27 @@ def test_groupnorm_act_vs_torch_fp64(B, C, H, W, G, act, shifted):
     assert (x.grad.double() - xd.grad).abs().max().item() < 2e-4 * max(1.0, xd.grad.abs().max().item())
 
 
+@pytest.mark.parametrize("BH,S,L,D", [(16, 256, 256, 40), (4, 1024, 1024, 80), (8, 256, 500, 160), (3, 64, 77, 40),
+                                      (2, 4096, 4096, 40)])
+def test_math_attention_fused_softmax_backward_vs_fp64(BH, S, L, D):
+    """ops.math_attention: forward and (q, k, v) gradients vs torch fp64 autograd."""
+    from stablekeypoints_amd import ops
+    g = torch.Generator().manual_seed(S + L)
+    q = (torch.randn(BH, S, D, generator=g)).to(DEV).requires_grad_(True)
+    k = (torch.randn(BH, L, D, generator=g)).to(DEV).requires_grad_(True)
+    v = (torch.randn(BH, L, D, generator=g)).to(DEV).requires_grad_(True)
+    scale = D ** -0.5
+    out = ops.math_attention(q, k, v, scale)
+    dout = torch.randn(BH, S, D, generator=g).to(DEV)
+    (out * dout).sum().backward()
+    qd, kd, vd = (t.detach().double().requires_grad_(True) for t in (q, k, v))
+    ref = torch.softmax(qd @ kd.transpose(1, 2) * scale, -1) @ vd
+    (ref * dout.double()).sum().backward()
+    assert (out.double() - ref).abs().max().item() < 1e-5
+    for a, b in ((q.grad, qd.grad), (k.grad, kd.grad), (v.grad, vd.grad)):
+        assert (a.double() - b).abs().max().item() < 1e-4 * max(1.0, b.abs().max().item())
+
+
 def test_residual_bias_add_bitexact():
     """a + (h + bias[c]) equals torch's two adds bit for bit; gradients pass through."""
     from stablekeypoints_amd import ops
