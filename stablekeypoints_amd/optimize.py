@@ -257,7 +257,8 @@ def optimize_embedding(ldm, top_k_strategy="entropy", wandb_log=True, context=No
     if dataset is None:
         dataset = _make_dataset(dataset_name, dataset_loc, max_len, validation)
     if context is None:
-        context = ptp_utils.init_random_noise(device, num_words=num_tokens)
+        context = ptp_utils.init_random_noise(device, num_words=num_tokens,
+                                              dim=getattr(ldm.unet, "cross_attention_dim", 768))
     accum = batch_size // num_gpus
     opt = TokenOptimizer(ldm, controllers, context, lr=lr, top_k_strategy=top_k_strategy, top_k=top_k,
                          furthest_point_num_samples=furthest_point_num_samples, sigma=sigma,

@@ -32,6 +32,9 @@ def load_ldm(device, type="CompVis/stable-diffusion-v1-4", feature_upsample_res=
     capture (the reference discards that output; DESIGN.md §UNet early exit).
     """
     weights = type if (isinstance(type, str) and os.path.isdir(type)) else None
+    if type == "tiny" and config is None:   # toy-width SD-1.5 (tests, CLI smoke runs)
+        from .sd import TINY_CONFIG
+        config = TINY_CONFIG
     if weights is None and str(device) != "cpu":
         pass  # hub names cannot be fetched offline: random-init SD-1.5 (seeded) instead
     ldm = build_sd15(seed=seed, device=device, weights=weights, config=config)

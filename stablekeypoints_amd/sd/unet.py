@@ -356,6 +356,7 @@ class UNet2DConditionModel(nn.Module):
     def __init__(self, in_channels=4, out_channels=4, block_out_channels=(320, 640, 1280, 1280),
                  cross_attention_dim=768, attention_head_dim=8, norm_num_groups=32):
         super().__init__()
+        self.cross_attention_dim = cross_attention_dim
         ch0 = block_out_channels[0]
         temb = ch0 * 4
         heads = attention_head_dim

@@ -255,3 +255,24 @@ def test_evaluate_tiny_vs_reference(monkeypatch, tmp_path):
             agree += 1
             assert abs(errs[p] - g["inter_eye_distance_errors"][p]) < 1e-5
     assert agree >= 1
+
+
+def test_cli_all_stages_tiny(tmp_path):
+    """main.py end to end (optimize → find_indices → precompute → regressor → evaluate) on the
+    tiny model and synthetic images: every stage runs on the HIP path and writes the
+    reference's files with the reference's shapes."""
+    from stablekeypoints_amd import main as cli
+    out = tmp_path / "run"
+    cli.main(["--model_type", "tiny", "--dataset_name", "synthetic", "--max_len", "4", "--num_steps", "2",
+              "--batch_size", "2", "--num_tokens", "16", "--feature_upsample_res", "32", "--num_indices", "2",
+              "--top_k", "4", "--furthest_point_num_samples", "8", "--augmentation_iterations", "2",
+              "--max_num_points", "2", "--evaluation_method", "mean_average_error", "--save_folder", str(out),
+              "--device", DEV])
+    load = lambda n: torch.load(out / n, weights_only=True)   # noqa: E731
+    assert load("embedding.pt").shape == (1, 16, 32)
+    idx = load("indices.pt")
+    assert idx.dtype == torch.int64 and 1 <= idx.numel() <= 4
+    src, tgt = load("source_keypoints.pt"), load("target_keypoints.pt")
+    assert src.shape == (2, idx.numel(), 2) and tgt.shape == (2, 15, 2)
+    assert load("regressor.pt").shape == (2 * idx.numel(), 30)
+    assert torch.isfinite(load("all_errors.pt")).all()
