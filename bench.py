@@ -201,6 +201,8 @@ def cpu_baseline(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--model", default="sd15", choices=["sd15", "sdxl"],
+                    help="sdxl = BASELINE.json configs[4] (SDXL UNet, 1024², context width 2048; not the headline)")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--accum", type=int, default=4, help="images per rank per optimiser step (batch_size/num_gpus)")
@@ -236,13 +238,16 @@ def main():
     from stablekeypoints_amd.optimize_token import load_ldm
     from stablekeypoints_amd.datasets import SyntheticDataset
 
-    ldm, controllers, num_gpus = load_ldm(dev, "runwayml/stable-diffusion-v1-5", feature_upsample_res=args.upsample_res)
+    if args.model == "sdxl" and args.res == 512:
+        args.res = 1024
+    name = "stabilityai/stable-diffusion-xl-base-1.0" if args.model == "sdxl" else "runwayml/stable-diffusion-v1-5"
+    ldm, controllers, num_gpus = load_ldm(dev, name, feature_upsample_res=args.upsample_res)
     if args.gc_freeze:
         import gc
         gc.collect()
         gc.freeze()   # the model's ~10^5 long-lived objects leave the cyclic collector's scans
     torch.manual_seed(0)
-    context = torch.randn(1, args.tokens, 768).to(dev)
+    context = torch.randn(1, args.tokens, ldm.unet.cross_attention_dim).to(dev)
     torch.manual_seed(1234 + rank)
     opt = TokenOptimizer(ldm, controllers, context, accum=args.accum, device=dev)
     data = SyntheticDataset(n=16, size=args.res, seed=rank)
@@ -295,7 +300,10 @@ def main():
         traffic = None
         if os.path.exists(args.traffic):
             try:
-                traffic = json.load(open(args.traffic)).get("skp_aggregate", {}).get("hbm_bytes_per_launch")
+                rec_t = json.load(open(args.traffic)).get("skp_aggregate", {})
+                # PMC bytes apply only to the workload they were measured on
+                if rec_t.get("algorithmic_bytes_per_launch") == agg["bytes_per_launch"]:
+                    traffic = rec_t.get("hbm_bytes_per_launch")
             except (OSError, ValueError):
                 traffic = None
         roof = {"kernel": "skp_aggregate", "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
@@ -311,18 +319,27 @@ def main():
                         "GB/s_algorithmic": s["bytes_per_launch"] / (s["avg_ms"] * 1e-3) / 1e9}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.model == "sd15":
         ops.set_kernel_timer(None)
         cpu = cpu_baseline(args)
 
     if rank == 0:
-        out = {"metric": "images/sec (token-opt step, 512², N=500 tokens)", "value": value, "unit": "images/sec",
+        if args.model == "sdxl":
+            metric = f"images/sec (token-opt step, {args.res}², N={args.tokens} tokens, SDXL)"
+            workload = (f"SDXL-shaped {args.res}², N={args.tokens} tokens, SDXL UNet fp32 (20 heads x 64 at the 32² "
+                        f"capture layers, context width 2048), feature_upsample_res={args.upsample_res} "
+                        "(BASELINE.json configs[4])")
+        else:
+            metric = "images/sec (token-opt step, 512², N=500 tokens)"
+            workload = ("CelebA-wild-shaped 512², N=500 tokens, SD-1.5 fp32, feature_upsample_res=128, "
+                        "batch_size 4 per GPU (BASELINE.json configs[1]); the 4 images and their warps "
+                        "in one VAE/UNet pass of 8")
+        out = {"metric": metric, "value": value, "unit": "images/sec",
                "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-               "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded torch.rand 512² images, random-init SD-1.5)",
-               "config": {"workload": "CelebA-wild-shaped 512², N=500 tokens, SD-1.5 fp32, feature_upsample_res=128, "
-                                      "batch_size 4 per GPU (BASELINE.json configs[1]); the 4 images and their warps "
-                                      "in one VAE/UNet pass of 8",
+               "vs_baseline": None, "dtype": "f32",
+               "data": f"synthetic (seeded torch.rand {args.res}² images, random-init {args.model.upper()})",
+               "config": {"workload": workload,
                           "global_batch": world * args.accum, "tokens": args.tokens, "image_res": args.res,
                           "feature_upsample_res": args.upsample_res, "micro_batch": mb,
                           "parallelism": f"dp{world} (RCCL grad all-reduce)"},

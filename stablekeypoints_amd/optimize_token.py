@@ -14,7 +14,7 @@ import os
 import torch
 
 from . import ops, ptp_utils
-from .sd import build_sd15
+from .sd import build_sd15, build_sdxl
 
 
 def _world():
@@ -32,12 +32,16 @@ def load_ldm(device, type="CompVis/stable-diffusion-v1-4", feature_upsample_res=
     capture (the reference discards that output; DESIGN.md §UNet early exit).
     """
     weights = type if (isinstance(type, str) and os.path.isdir(type)) else None
+    xl = isinstance(type, str) and ("xl" in type.lower())   # SDXL (SURVEY §8 A16, config 5)
     if type == "tiny" and config is None:   # toy-width SD-1.5 (tests, CLI smoke runs)
         from .sd import TINY_CONFIG
         config = TINY_CONFIG
+    if type == "tiny-xl" and config is None:
+        from .sd import TINY_SDXL_CONFIG
+        config = TINY_SDXL_CONFIG
     if weights is None and str(device) != "cpu":
         pass  # hub names cannot be fetched offline: random-init SD-1.5 (seeded) instead
-    ldm = build_sd15(seed=seed, device=device, weights=weights, config=config)
+    ldm = (build_sdxl if xl else build_sd15)(seed=seed, device=device, weights=weights, config=config)
     dev = torch.device(device)
     if dev.type == "cuda" and dev.index is None:
         dev = torch.device("cuda", torch.cuda.current_device())

@@ -1,5 +1,6 @@
-"""Frozen SD-1.5 UNet / VAE-encoder / DDIM scheduler (PyTorch-ROCm side of the path)."""
+"""Frozen SD-1.5 / SDXL UNet, VAE-encoder and DDIM scheduler (PyTorch-ROCm side of the path)."""
 from .unet import UNet2DConditionModel, CrossAttention, CaptureComplete
+from .sdxl import SDXLUNet, SDXL_CONFIG
 from .vae import AutoencoderKL
 from .scheduler import DDIMScheduler
 
@@ -30,7 +31,14 @@ TINY_CONFIG = dict(unet=dict(block_out_channels=(32, 64, 64, 64), cross_attentio
 TINY_IMAGE = 128
 
 
-def build_sd15(seed=0, device="cpu", weights=None, config=None):
+# Toy SDXL (same structure: no attention at the top level, depth-2/-N transformers, linear
+# projections, text_time conditioning) for tests.
+TINY_SDXL_CONFIG = dict(unet=dict(block_out_channels=(32, 64, 64), transformer_depth=(0, 1, 2), head_dim=16,
+                                  cross_attention_dim=32, addition_time_embed_dim=8, pooled_dim=32, norm_num_groups=8),
+                        vae=dict(block_out_channels=(32, 32, 64, 64), norm_num_groups=8))
+
+
+def build_sd15(seed=0, device="cpu", weights=None, config=None, unet_cls=None):
     """Random-init SD-1.5 parts (seeded), or load a local diffusers-0.8.0 state dict.
 
     ``weights`` may be a directory holding ``unet.safetensors``/``vae.safetensors`` or
@@ -44,7 +52,7 @@ def build_sd15(seed=0, device="cpu", weights=None, config=None):
     with g:
         torch.manual_seed(seed)
         cfg = config or {}
-        unet = UNet2DConditionModel(**cfg.get("unet", {}))
+        unet = (unet_cls or UNet2DConditionModel)(**cfg.get("unet", {}))
         vae = AutoencoderKL(**cfg.get("vae", {}))
     if weights:
         for name, mod in (("unet", unet), ("vae", vae)):
@@ -68,3 +76,9 @@ def build_sd15(seed=0, device="cpu", weights=None, config=None):
         for p in m.parameters():
             p.requires_grad = False
     return StableDiffusionParts(unet, vae, sched).to(device)
+
+
+def build_sdxl(seed=0, device="cpu", weights=None, config=None):
+    """Random-init (seeded) or local-weights SDXL UNet + VAE encoder + DDIM (scaled_linear
+    0.00085 → 0.012, as SD-1.5; SDXL's scheduler config uses the same betas)."""
+    return build_sd15(seed=seed, device=device, weights=weights, config=config, unet_cls=SDXLUNet)

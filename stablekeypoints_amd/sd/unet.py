@@ -152,25 +152,36 @@ class BasicTransformerBlock(nn.Module):
 
 
 class Transformer2DModel(nn.Module):
-    """SD-1.x spatial transformer (conv proj_in/proj_out, one BasicTransformerBlock)."""
+    """Spatial transformer: SD-1.x (conv proj_in/proj_out, one BasicTransformerBlock) or, with
+    ``linear_proj`` and ``depth`` > 1, SDXL's (Linear projections on the (B, HW, C) tokens,
+    ``depth`` BasicTransformerBlocks)."""
 
-    def __init__(self, num_attention_heads, attention_head_dim, in_channels, cross_attention_dim, norm_num_groups=32):
+    def __init__(self, num_attention_heads, attention_head_dim, in_channels, cross_attention_dim, norm_num_groups=32,
+                 depth=1, linear_proj=False):
         super().__init__()
         inner = num_attention_heads * attention_head_dim
+        self.linear_proj = linear_proj
         self.norm = nn.GroupNorm(norm_num_groups, in_channels, eps=1e-6, affine=True)
-        self.proj_in = nn.Conv2d(in_channels, inner, 1)
+        self.proj_in = nn.Linear(in_channels, inner) if linear_proj else nn.Conv2d(in_channels, inner, 1)
         self.transformer_blocks = nn.ModuleList(
-            [BasicTransformerBlock(inner, num_attention_heads, attention_head_dim, cross_attention_dim)])
-        self.proj_out = nn.Conv2d(inner, in_channels, 1)
+            [BasicTransformerBlock(inner, num_attention_heads, attention_head_dim, cross_attention_dim)
+             for _ in range(depth)])
+        self.proj_out = nn.Linear(inner, in_channels) if linear_proj else nn.Conv2d(inner, in_channels, 1)
 
     def forward(self, x, encoder_hidden_states=None):
         b, c, hh, ww = x.shape
         res = x
-        x = self.proj_in(gn_act(self.norm, x, False))
-        inner = x.shape[1]
-        x = x.permute(0, 2, 3, 1).reshape(b, hh * ww, inner)
+        x = gn_act(self.norm, x, False)
+        if self.linear_proj:
+            x = self.proj_in(x.permute(0, 2, 3, 1).reshape(b, hh * ww, c))
+        else:
+            x = self.proj_in(x)
+            x = x.permute(0, 2, 3, 1).reshape(b, hh * ww, x.shape[1])
+        inner = x.shape[-1]
         for blk in self.transformer_blocks:
             x = blk(x, context=encoder_hidden_states)
+        if self.linear_proj:
+            return self.proj_out(x).reshape(b, hh, ww, c).permute(0, 3, 1, 2) + res
         x = x.reshape(b, hh, ww, inner).permute(0, 3, 1, 2)
         return self.proj_out(x) + res
 
@@ -237,11 +248,11 @@ class Upsample2D(nn.Module):
 
 # --------------------------------------------------------------------------- blocks
 class CrossAttnDownBlock2D(nn.Module):
-    def __init__(self, in_ch, out_ch, temb, heads, ctx_dim, add_downsample, groups=32):
+    def __init__(self, in_ch, out_ch, temb, heads, ctx_dim, add_downsample, groups=32, depth=1, linear_proj=False):
         super().__init__()
         self.resnets = nn.ModuleList([ResnetBlock2D(in_ch if i == 0 else out_ch, out_ch, temb, groups) for i in range(2)])
-        self.attentions = nn.ModuleList([Transformer2DModel(heads, out_ch // heads, out_ch, ctx_dim, groups)
-                                         for _ in range(2)])
+        self.attentions = nn.ModuleList([Transformer2DModel(heads, out_ch // heads, out_ch, ctx_dim, groups, depth,
+                                                            linear_proj) for _ in range(2)])
         self.downsamplers = nn.ModuleList([Downsample2D(out_ch)]) if add_downsample else None
 
     def forward(self, h, temb, context):
@@ -283,11 +294,12 @@ class _UpBase(nn.Module):
 
 
 class CrossAttnUpBlock2D(_UpBase):
-    def __init__(self, in_ch, out_ch, prev_ch, temb, heads, ctx_dim, add_upsample, groups=32):
+    def __init__(self, in_ch, out_ch, prev_ch, temb, heads, ctx_dim, add_upsample, groups=32, depth=1,
+                 linear_proj=False):
         super().__init__()
         self.resnets = self._make_resnets(in_ch, out_ch, prev_ch, temb, groups)
-        self.attentions = nn.ModuleList([Transformer2DModel(heads, out_ch // heads, out_ch, ctx_dim, groups)
-                                         for _ in range(3)])
+        self.attentions = nn.ModuleList([Transformer2DModel(heads, out_ch // heads, out_ch, ctx_dim, groups, depth,
+                                                            linear_proj) for _ in range(3)])
         self.upsamplers = nn.ModuleList([Upsample2D(out_ch)]) if add_upsample else None
 
     def forward(self, h, res_tuple, temb, context, upsample_size=None):
@@ -318,10 +330,11 @@ class UpBlock2D(_UpBase):
 
 
 class UNetMidBlock2DCrossAttn(nn.Module):
-    def __init__(self, ch, temb, heads, ctx_dim, groups=32):
+    def __init__(self, ch, temb, heads, ctx_dim, groups=32, depth=1, linear_proj=False):
         super().__init__()
         self.resnets = nn.ModuleList([ResnetBlock2D(ch, ch, temb, groups) for _ in range(2)])
-        self.attentions = nn.ModuleList([Transformer2DModel(heads, ch // heads, ch, ctx_dim, groups)])
+        self.attentions = nn.ModuleList([Transformer2DModel(heads, ch // heads, ch, ctx_dim, groups, depth,
+                                                            linear_proj)])
 
     def forward(self, h, temb, context):
         h = self.resnets[0](h, temb)
