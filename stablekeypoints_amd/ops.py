@@ -546,3 +546,57 @@ def math_attention(q, k, v, scale):
     """softmax(q kᵀ·scale) v with the fused softmax backward (HIP device)."""
     _lib.require_device(q, k, v)
     return MathAttention.apply(q, k, v, float(scale))
+
+
+# --------------------------------------------------------------------------- UNet-side: token projections
+class TokensProjIn(torch.autograd.Function):
+    """Transformer2DModel.proj_in (1×1 conv) + NCHW→(B, HW, C') as ONE strided batched GEMM:
+    h[b] = x[b]ᵀ Wᵀ + bias, x (B, C, HW) read through a transposed view (no permute copy, no
+    NHWC conversion); the input gradient comes back in NCHW the same way (W frozen)."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias):
+        B, C, HW = x.shape
+        h = torch.bmm(x.transpose(1, 2), w.t().expand(B, C, w.shape[0]))
+        if bias is not None:
+            h.add_(bias)
+        ctx.save_for_backward(w)
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        (w,) = ctx.saved_tensors
+        B = dh.shape[0]
+        dx = torch.bmm(w.t().expand(B, w.shape[1], w.shape[0]), dh.transpose(1, 2))   # (B, C, HW)
+        return dx, None, None
+
+
+class TokensProjOut(torch.autograd.Function):
+    """Transformer2DModel.proj_out (1×1 conv) on (B, HW, C') tokens back to NCHW as one strided
+    batched GEMM, y[b] = W h[b]ᵀ; the bias and the residual follow in one residual_bias_add."""
+
+    @staticmethod
+    def forward(ctx, h, w):
+        B = h.shape[0]
+        ctx.save_for_backward(w)
+        return torch.bmm(w.expand(B, *w.shape), h.transpose(1, 2))                     # (B, C, HW)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (w,) = ctx.saved_tensors
+        B = dy.shape[0]
+        return torch.bmm(dy.transpose(1, 2), w.expand(B, *w.shape)), None             # (B, HW, C')
+
+
+def tokens_proj_in(x, weight, bias):
+    """(B, C, H, W) → (B, HW, C') = 1×1 conv (weight (C', C, 1, 1)) + bias, flattened to tokens."""
+    B, C = x.shape[:2]
+    return TokensProjIn.apply(x.reshape(B, C, -1), weight.detach().reshape(weight.shape[0], C),
+                              None if bias is None else bias.detach())
+
+
+def tokens_proj_out(h, weight, bias, residual):
+    """(B, HW, C') → residual + 1×1 conv(h) + bias in NCHW (residual's shape)."""
+    B, C = residual.shape[:2]
+    y = TokensProjOut.apply(h, weight.detach().reshape(C, h.shape[-1]))
+    return residual_bias_add(residual, y.view(residual.shape), bias)

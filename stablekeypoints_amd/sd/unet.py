@@ -172,6 +172,13 @@ class Transformer2DModel(nn.Module):
         b, c, hh, ww = x.shape
         res = x
         x = gn_act(self.norm, x, False)
+        if not self.linear_proj and _fused(x, self.proj_in, self.proj_out):
+            # 1×1 projections as strided batched GEMMs straight between NCHW and (B, HW, C')
+            from .. import ops
+            x = ops.tokens_proj_in(x, self.proj_in.weight, self.proj_in.bias)
+            for blk in self.transformer_blocks:
+                x = blk(x, context=encoder_hidden_states)
+            return ops.tokens_proj_out(x, self.proj_out.weight, self.proj_out.bias, res)
         if self.linear_proj:
             x = self.proj_in(x.permute(0, 2, 3, 1).reshape(b, hh * ww, c))
         else:
