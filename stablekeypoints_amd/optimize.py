@@ -104,7 +104,8 @@ class TokenOptimizer:
                  from_where=("down_cross", "mid_cross", "up_cross"), augment_degrees=15, augment_scale=(0.8, 1.0),
                  augment_translate=(0.25, 0.25), device="cuda", batch_captures=True):
         self.ldm, self.controllers, self.device = ldm, controllers, device
-        # batch_captures: run the image and its warp through ONE B=2 VAE/UNet pass
+        # batch_captures: run each image with its warp in one VAE/UNet pass (micro_steps: all
+        # of an optimiser step's images in one pass)
         # (run_and_find_attn_per_image); False = the reference's two sequential passes.
         self.batch_captures = batch_captures
         self._orig_controllers = controllers

@@ -1,4 +1,4 @@
-"""Dev tool: time the SD-1.5 UNet 3x3 convolutions (B=2) under MIOpen settings.
+"""Dev tool: time the SD-1.5 UNet/VAE 3x3 convolutions (--batch, default 2) under MIOpen settings.
 
 usage: python tools/conv_probe.py [--benchmark] [--channels-last]
 (set MIOPEN_FIND_MODE etc. in the environment to compare find modes)
