@@ -215,6 +215,10 @@ def main():
                     help="un-captured UNet attention: explicit fp32 GEMM+softmax (math) or torch SDPA")
     ap.add_argument("--micro-batch", type=int, default=0,
                     help="images per VAE/UNet pass (0 = all `accum` images of an optimiser step in one pass)")
+    ap.add_argument("--prefetch", type=int, default=1,
+                    help="VAE-encode the next optimiser step's images on a side stream (TokenOptimizer.prefetch); "
+                         "steady state: every timed step runs one UNet pass and one VAE pass, the warm-up's "
+                         "prefetch is balanced by the last timed step's")
     ap.add_argument("--gc-freeze", type=int, default=1, help="gc.freeze() after the model is built (host overhead)")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
                     help="JSON with PMC-derived HBM bytes per launch of the roofline kernel")
@@ -259,11 +263,18 @@ def main():
 
     mb = args.micro_batch if args.micro_batch > 0 else args.accum
 
+    def batch_at(c, n):
+        return [imgs[(c + i) % len(imgs)] for i in range(n)]
+
     def step():
         done = 0
         while done < args.accum:
             n = min(mb, args.accum - done)
-            opt.micro_steps([imgs[(counter[0] + i) % len(imgs)] for i in range(n)])
+            cur = batch_at(counter[0], n)
+            if args.prefetch:
+                opt.prefetch(cur)                                   # no-op when already prefetched
+                opt.prefetch(batch_at(counter[0] + n, min(mb, args.accum)))   # overlaps this pass
+            opt.micro_steps(cur)
             counter[0] += n
             done += n
         return opt.optimizer_step()

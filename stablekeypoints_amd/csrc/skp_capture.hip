@@ -394,50 +394,70 @@ __global__ __launch_bounds__(kBwdThreads) void capture_bwd_rows_kernel(const flo
   out.finish();
 }
 
-// Phase B: dz[b][i·s + j][n] = Σ_y wy(y→i) · ws[b][y][j][n]; block = (b, kColRows low-res rows,
-// element chunk): every ws row is read once per block for all the rows whose taps it feeds.
-constexpr int kColChunk = 256;
-constexpr int kColRows = 4;
-__global__ __launch_bounds__(kThreads) void capture_bwd_cols_kernel(const float* __restrict__ ws, int BH, int s,
-                                                                    int N, int R, float* __restrict__ dz) {
-  __shared__ float wy[kColRows][1024];
-  __shared__ int ylo, yhi;
-  const int b = blockIdx.x % BH;
-  const int i0 = (blockIdx.x / BH) * kColRows;
-  if (threadIdx.x == 0) { ylo = R; yhi = -1; }
-  __syncthreads();
-  for (int y = threadIdx.x; y < R; y += kThreads) {   // weight of low-res row i0+r in output row y
+// Phase B: dz[b][i·s + j][n] = Σ_y wy(y→i) · ws[b][y][j][n].  Thread = one (j, n) element of one
+// b; it streams the R row partials in order (each read exactly once, coalesced across the
+// block) through the same rolling 4-row window as the horizontal adjoint: low-res row i is
+// complete once lo(y) passes it and leaves as one coalesced store (edge rows folded as torch's
+// clamped taps do).  Deterministic, no atomics.
+constexpr int kColThreads = 256;
+constexpr int kColBatch = 8;   // row partials loaded ahead per thread
+__global__ __launch_bounds__(kColThreads) void capture_bwd_cols_kernel(const float* __restrict__ ws, int BH, int s,
+                                                                       int N, int R, float* __restrict__ dz) {
+  __shared__ __attribute__((aligned(16))) float TW[1024 * 4];
+  __shared__ int TL[1024];
+  const int b = blockIdx.y;
+  const long long plane = (long long)s * N;
+  const long long e = (long long)blockIdx.x * kColThreads + threadIdx.x;
+  for (int y = threadIdx.x; y < R; y += kColThreads) {
     const Taps4 ty = bicubic_taps(y, s, R);
-    bool hit = false;
-#pragma unroll
-    for (int r = 0; r < kColRows; ++r) {
-      float w = 0.0f;
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (ty.i[k] == i0 + r) { w += ty.w[k]; hit = true; }
-      wy[r][y] = w;
-    }
-    if (hit) { atomicMin(&ylo, y); atomicMax(&yhi, y); }
+    *reinterpret_cast<float4*>(TW + 4 * y) = make_float4(ty.w[0], ty.w[1], ty.w[2], ty.w[3]);
+    TL[y] = ty.lo;
   }
   __syncthreads();
-  const int y0 = ylo, y1 = yhi;
-  const int nr = min(kColRows, s - i0);
-  const size_t plane = (size_t)s * N;
-  const float* wb = ws + (size_t)b * R * plane;
-  float* out = dz + ((size_t)b * s * s + (size_t)i0 * s) * N;
-  const int e0 = blockIdx.y * kColChunk;
-  const int e1 = min((int)plane, e0 + kColChunk);
-  for (int e = e0 + threadIdx.x; e < e1; e += kThreads) {
-    float acc[kColRows] = {};
-    for (int y = y0; y <= y1; ++y) {
-      const float v = wb[(size_t)y * plane + e];
-#pragma unroll
-      for (int r = 0; r < kColRows; ++r) acc[r] += wy[r][y] * v;
+  if (e >= plane) return;
+  const float* src = ws + (size_t)b * R * plane + e;
+  float* out = dz + (size_t)b * s * plane + e;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f, pend = 0.f;
+  int base = -2, pt = 0;
+  auto emit = [&](int c, float v) {   // virtual low-res row c (−2 … s+1) is complete
+    const int t = min(max(c, 0), s - 1);
+    if (t != pt) {
+      out[(size_t)pt * plane] = pend;
+      for (int j = pt + 1; j < t; ++j) out[(size_t)j * plane] = 0.0f;
+      pt = t;
+      pend = v;
+    } else {
+      pend += v;
     }
+  };
+  for (int y0 = 0; y0 < R; y0 += kColBatch) {
+    float v[kColBatch];
 #pragma unroll
-    for (int r = 0; r < kColRows; ++r)
-      if (r < nr) out[(size_t)r * plane + e] = acc[r];
+    for (int u = 0; u < kColBatch; ++u) v[u] = (y0 + u < R) ? src[(size_t)(y0 + u) * plane] : 0.0f;
+#pragma unroll
+    for (int u = 0; u < kColBatch; ++u) {
+      const int y = y0 + u;
+      if (y < R) {
+        const int lo = TL[y];
+        while (base < lo) {   // uniform across the block
+          emit(base, a0);
+          a0 = a1; a1 = a2; a2 = a3; a3 = 0.0f;
+          ++base;
+        }
+        const float4 w = *reinterpret_cast<const float4*>(TW + 4 * y);
+        a0 += w.x * v[u];
+        a1 += w.y * v[u];
+        a2 += w.z * v[u];
+        a3 += w.w * v[u];
+      }
+    }
   }
+  emit(base, a0);
+  emit(base + 1, a1);
+  emit(base + 2, a2);
+  emit(base + 3, a3);
+  out[(size_t)pt * plane] = pend;
+  for (int j = pt + 1; j < s; ++j) out[(size_t)j * plane] = 0.0f;
 }
 
 // ------------------------------------------------------------------------------------ aggregate
@@ -660,6 +680,7 @@ extern "C" int skp_capture_bwd(const float* z_low, int BH, int s, int N, int R, 
   SKP_CHECK_ARG(group >= 1, "group must be >= 1");
   SKP_CHECK_ARG(BH > 0 && s > 0 && R > 0 && N > 0, "non-positive shape");
   SKP_CHECK_ARG(R <= 1024, "R > 1024 is not supported");
+  SKP_CHECK_ARG(BH <= 65535, "BH > 65535");
   const int nt = nt_for(N);
   SKP_CHECK_ARG(nt > 0, "N > 1024 tokens is not supported");
   const int CH = pick_chunk(s, N, R);
@@ -668,8 +689,8 @@ extern "C" int skp_capture_bwd(const float* z_low, int BH, int s, int N, int R, 
   if (nt == 1) launch_bwd_rows<1>(z_low, BH, s, N, R, CH, dattn, group, sb, sp, sn, gscale, workspace, st);
   else launch_bwd_rows<2>(z_low, BH, s, N, R, CH, dattn, group, sb, sp, sn, gscale, workspace, st);
   SKP_LAUNCH_CHECK();
-  const int chunks = (s * N + kColChunk - 1) / kColChunk;
-  hipLaunchKernelGGL(capture_bwd_cols_kernel, dim3(BH * ((s + kColRows - 1) / kColRows), chunks), dim3(kThreads), 0, st, workspace, BH, s, N, R,
+  const int chunks = (int)(((long long)s * N + kColThreads - 1) / kColThreads);
+  hipLaunchKernelGGL(capture_bwd_cols_kernel, dim3(chunks, BH), dim3(kColThreads), 0, st, workspace, BH, s, N, R,
                      dz_low);
   SKP_LAUNCH_CHECK();
   return SKP_OK;

@@ -128,7 +128,42 @@ class TokenOptimizer:
         self.transform = RandomAffineWithInverse(degrees=augment_degrees, scale=augment_scale,
                                                  translate=augment_translate)
         self.world, self.rank = _world()
+        self._prefetched = []      # FIFO of (key, thetas, latents, event) from prefetch()
+        self._side = None
         self.reset_running()
+
+    def prefetch(self, images):
+        """Warp and VAE-encode an optimiser step's images (and draw their thetas) ahead of time
+        on a side stream, so the VAE encoder — a third of the step, independent of the
+        context — overlaps the previous step's UNet backward.  The thetas are drawn here, in the
+        same order as ``micro_steps`` would draw them; ``micro_steps(images)`` then consumes
+        the record.  A no-op for images already prefetched or without ``batch_captures``."""
+        key = tuple(id(t) for t in images)
+        if not self.batch_captures or any(r[0] == key for r in self._prefetched):
+            return
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        batch = torch.cat(list(images))
+        thetas = self.transform.draw_theta(len(images))
+        main = torch.cuda.current_stream(self.device)
+        self._side.wait_stream(main)
+        with torch.cuda.stream(self._side), torch.no_grad():
+            batch.record_stream(self._side)
+            transformed = ops.affine_warp(batch, thetas.to(self.device, torch.float32))
+            lat = ptp_utils.image2latent(self.ldm, torch.cat([batch, transformed]), self.device)
+            ev = torch.cuda.Event()
+            ev.record(self._side)
+        self._prefetched.append((key, thetas, lat, ev))
+
+    def _take_prefetched(self, images):
+        key = tuple(id(t) for t in images)
+        if self._prefetched and self._prefetched[0][0] == key:
+            _, thetas, lat, ev = self._prefetched.pop(0)
+            main = torch.cuda.current_stream(self.device)
+            main.wait_event(ev)
+            lat.record_stream(main)
+            return thetas, lat
+        return None
 
     def restore_hooks(self):
         """Point the patched attention back at the caller's controllers."""
@@ -166,11 +201,18 @@ class TokenOptimizer:
         if not self.batch_captures or len(images) == 1:
             return [self.micro_step(img) for img in images]
         k = len(images)
-        batch = torch.cat(list(images))
-        transformed = self.transform(batch)              # draws k thetas, image order
+        pre = self._take_prefetched(images)
+        if pre is not None:                              # latents of images + warps (prefetch)
+            thetas, inputs = pre
+            self.transform.last_params = {"theta": thetas.detach().cpu().float()}
+        else:
+            batch = torch.cat(list(images))
+            transformed = self.transform(batch)          # draws k thetas, image order
+            inputs = torch.cat([batch, transformed])
         maps = ptp_utils.run_and_find_attn_per_image(
-            self.ldm, torch.cat([batch, transformed]), self.context, noise_level=self.kw["noise_level"],
+            self.ldm, inputs, self.context, noise_level=self.kw["noise_level"],
             device=self.device, layers=self.kw["layers"], controllers=self.controllers, stacked=True)[0]
+        th_inv = self.transform.theta_inverse().to(self.device)   # all k warps, one upload
         sel = [self._select(maps[i], maps[k + i]) for i in range(k)]
         # one gather of every image's selected rows (its backward is one scatter into the
         # (2k, N, R, R) map gradient instead of 2k full-size zero-fills and adds)
@@ -180,7 +222,7 @@ class TokenOptimizer:
         total, off = 0.0, 0
         for i, idx in enumerate(sel):
             n = idx.numel()
-            loss, eq, sh = self._losses(A[off:off + n], At[off:off + n], i)
+            loss, eq, sh = self._losses(A[off:off + n], At[off:off + n], i, th_inv[i])
             off += n
             self._account(loss, eq, sh)
             total = total + loss
@@ -219,10 +261,14 @@ class TokenOptimizer:
             raise NotImplementedError
         return ptp_utils.furthest_point_sampling(attention_map_transformed, self.top_k, cand)
 
-    def _losses(self, A, At, index):
-        """optimize.py:425-437 on the selected rows; ``index`` selects the warp's theta."""
+    def _losses(self, A, At, index, theta_inv=None):
+        """optimize.py:425-437 on the selected rows; ``index`` selects the warp's theta
+        (``theta_inv``: that theta's inverse already on the device)."""
         sh = sharpening_loss(A, device=self.device, sigma=self.sigma, num_subjects=self.num_subjects)
-        eq = equivariance_loss(A, At, self.transform, index)   # (T, h, w): theta ``index``
+        if theta_inv is not None:
+            eq = ops.equivariance_loss_single(A, At, theta_inv)
+        else:
+            eq = equivariance_loss(A, At, self.transform, index)   # (T, h, w): theta ``index``
         loss = eq * self.w_eq + sh * self.w_sharp
         return loss, eq, sh
 

@@ -404,6 +404,42 @@ def test_micro_steps_batch_equals_sequential_micro_steps():
     assert np.allclose(res[False][2], res[True][2], rtol=1e-3, atol=1e-8)
 
 
+def test_prefetched_vae_pass_equals_inline():
+    """TokenOptimizer.prefetch (warp + VAE on a side stream, thetas drawn ahead) then
+    micro_steps gives the same indices, loss and gradient as micro_steps alone."""
+    from stablekeypoints_amd.optimize import TokenOptimizer
+    from stablekeypoints_amd.optimize_token import load_ldm
+    from stablekeypoints_amd.sd import TINY_CONFIG, TINY_IMAGE
+    lat = TINY_IMAGE // 8
+    noise = torch.randn(4, 4, lat, lat, generator=torch.Generator().manual_seed(3)).to(DEV)
+    thetas = torch.tensor([[[0.9, -0.1, 0.1], [0.1, 0.9, -0.05]], [[0.85, 0.05, -0.1], [-0.05, 0.85, 0.2]]])
+    imgs = [torch.from_numpy(recipes.uniform(80 + i, (1, 3, TINY_IMAGE, TINY_IMAGE))).to(DEV) for i in range(2)]
+    res = {}
+    for pre in (False, True):
+        ldm, ctls, _ = load_ldm(DEV, "tiny", feature_upsample_res=32, config=TINY_CONFIG)
+        inner = ldm.scheduler
+
+        class Sched:
+            timesteps = inner.timesteps
+
+            def add_noise(self, x, n, t):
+                return inner.add_noise(x, noise, t)
+        ldm.scheduler = Sched()
+        ctx = torch.from_numpy(recipes.random_logits(52, (1, 16, 32))).to(DEV)
+        opt = TokenOptimizer(ldm, ctls, ctx, top_k=4, furthest_point_num_samples=8, accum=2, device=DEV)
+        opt.transform.draw_theta = lambda batch: thetas[:batch]
+        if pre:
+            opt.prefetch(imgs)
+        idx = opt.micro_steps(imgs)
+        assert not opt._prefetched
+        res[pre] = ([N(t) for t in idx], float(opt.run_tot), N(opt.context.grad))
+    for a, b in zip(res[False][0], res[True][0]):
+        assert np.array_equal(a, b)
+    assert abs(res[False][1] - res[True][1]) <= 1e-6 * abs(res[False][1])
+    # the equivariance adjoint scatters with atomics, so two identical runs differ at ~1e-6
+    assert np.allclose(res[False][2], res[True][2], rtol=1e-4, atol=1e-8)
+
+
 # ----------------------------------------------------------------------------- UNet-side GroupNorm(+SiLU)
 @pytest.mark.parametrize("B,C,H,W,G,act,shifted", [(2, 320, 64, 64, 32, True, True), (2, 1280, 8, 8, 32, False, False),
                                                    (1, 128, 256, 256, 32, True, False), (2, 12, 5, 7, 4, True, True),
