@@ -318,20 +318,32 @@ def optimize_embedding(ldm, top_k_strategy="entropy", wandb_log=True, context=No
     base = seed if seed is not None else int(torch.randint(0, 2 ** 31 - 1, (1,)))
     sampler_gen = torch.Generator().manual_seed(base + rank)
     order = torch.randperm(len(dataset), generator=sampler_gen)
-    pos = 0
+    state = {"order": order, "pos": 0}
+
+    def next_image():
+        if state["pos"] >= len(state["order"]):
+            state["order"] = torch.randperm(len(dataset), generator=sampler_gen)
+            state["pos"] = 0
+        img = dataset[int(state["order"][state["pos"]])]["img"][None].to(device, non_blocking=True)
+        state["pos"] += 1
+        return img
+
+    def next_batch(n):
+        return [next_image() for _ in range(n)]
+
     start = time.time()
     it_start = time.time()
-    pending = []
-    for iteration in range(n_iter):
-        if pos >= len(order):
-            order = torch.randperm(len(dataset), generator=sampler_gen)
-            pos = 0
-        pending.append(dataset[int(order[pos])]["img"][None].to(device, non_blocking=True))
-        pos += 1
-        if (iteration + 1) % accum == 0 or iteration + 1 == n_iter:
-            opt.micro_steps(pending)   # the optimiser step's images in one VAE/UNet pass
-            pending = []
-        if (iteration + 1) % accum == 0:
+    done = 0
+    cur = next_batch(min(accum, n_iter)) if n_iter > 0 else []
+    while done < n_iter:
+        n = len(cur)
+        nxt = next_batch(min(accum, n_iter - done - n)) if done + n < n_iter else []
+        opt.prefetch(cur)                 # no-op when already prefetched
+        if nxt:
+            opt.prefetch(nxt)             # the next step's VAE pass overlaps this step's UNet pass
+        opt.micro_steps(cur)              # the optimiser step's images in one VAE/UNet pass
+        done += n
+        if done % accum == 0:
             rec = {k: float(v) for k, v in opt.optimizer_step().items()}
             rec["iteration time"] = time.time() - it_start
             if log is not None:
@@ -342,6 +354,7 @@ def optimize_embedding(ldm, top_k_strategy="entropy", wandb_log=True, context=No
                       f"sharpening_loss: {rec['running_sharpening_loss']}, iteration time: {rec['iteration time']}",
                       flush=True)
             it_start = time.time()
+        cur = nxt
     opt.restore_hooks()
     if rank == 0 and log is None:
         print(f"optimization took {time.time() - start} seconds", flush=True)
