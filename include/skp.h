@@ -166,6 +166,18 @@ int skp_softmax_bwd(const float* P, float* dP, long long rows, int cols, float a
  * convolution's bias folded into the residual add (same rounding order).         */
 int skp_residual_bias_add(const float* a, const float* h, const float* bias, int B, int C, long long HW,
                           float* out, void* stream);
+/* 3×3 / stride-1 / pad-1 convolution of the frozen VAE encoder and UNet (diffusers Conv2d in
+ * Encoder / ResnetBlock2D / Upsample2D, run by ptp_utils.py:289-304 image2latent and the UNet
+ * forward/backward of optimize.py:173-190) as Winograd F(4×4, 3×3) on the fp32 matrix cores.
+ * skp_wino_weights: transformed weights U (K·C·36 floats, layout [K/32][C][32][36]) from
+ *   w (K, C, 3, 3) (flip 0), or, for the input gradient, from the forward weight w (C, K, 3, 3)
+ *   rotated 180° and transposed (flip 1).  K % 32 == 0.
+ * skp_conv3x3_wino: y (B, K, H, W) = conv(x (B, C, H, W), w) + bias[k] (bias may be NULL)
+ *   + residual (B, K, H, W) (may be NULL).  C % 4 == 0, K % 32 == 0, H % 4 == W % 4 == 0,
+ *   16-byte aligned tensors.                                                   */
+int skp_wino_weights(const float* w, int K, int C, int flip, float* U, void* stream);
+int skp_conv3x3_wino(const float* x, const float* U, const float* bias, const float* residual, float* y, int B, int C,
+                     int K, int H, int W, void* stream);
 
 #ifdef __cplusplus
 }

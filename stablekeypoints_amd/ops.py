@@ -600,3 +600,100 @@ def tokens_proj_out(h, weight, bias, residual):
     B, C = residual.shape[:2]
     y = TokensProjOut.apply(h, weight.detach().reshape(C, h.shape[-1]))
     return residual_bias_add(residual, y.view(residual.shape), bias)
+
+
+# --------------------------------------------------------------------------- 3×3 convolution
+# Transformed weights per frozen weight tensor: {weight: {flip: (version, U)}} (U = G g Gᵀ,
+# K·C·36 floats; built once, on first use, on the weight's device and stream).
+import weakref as _weakref
+
+_WINO_U = {}   # id(weight) -> (weakref(weight), {flip: (version, U)})
+# Below this many (64-tile × 32-channel) workgroups the Winograd kernel leaves most of the
+# 256 CUs idle and MIOpen's split-K kernels are faster (tools/conv_probe.py --wino at batch 8:
+# 160 workgroups (640 channels at 32²) still win, 80 (1280 at 16²) lose).
+WINO_MIN_WORKGROUPS = 128
+
+
+def _wino_u(weight, flip):
+    ent = _WINO_U.get(id(weight))
+    if ent is None or ent[0]() is not weight:
+        key = id(weight)
+        ent = (_weakref.ref(weight, lambda _r, key=key: _WINO_U.pop(key, None)), {})
+        _WINO_U[key] = ent
+    per = ent[1]
+    hit = per.get(flip)
+    if hit is not None and hit[0] == weight._version:
+        return hit[1]
+    w = _c(weight.detach())
+    K, C = (w.shape[0], w.shape[1]) if not flip else (w.shape[1], w.shape[0])
+    U = torch.empty(K * C * 36, device=w.device, dtype=F32)
+    call("skp_wino_weights", ptr(w), K, C, int(flip), ptr(U), stream(w.device))
+    per[flip] = (weight._version, U)
+    return U
+
+
+def wino_eligible(B, C, K, H, W, min_workgroups=None):
+    """Whether skp_conv3x3_wino takes a (B, C, H, W) → (B, K, H, W) 3×3 convolution."""
+    if C % 4 or K % 32 or H % 4 or W % 4:
+        return False
+    wgs = -(-(B * (H // 4) * (W // 4)) // 64) * (K // 32)
+    return wgs >= (WINO_MIN_WORKGROUPS if min_workgroups is None else min_workgroups)
+
+
+def _wino_launch(x, U, bias, residual, K):
+    B, C, H, W = x.shape
+    y = torch.empty(B, K, H, W, device=x.device, dtype=F32)
+    with _timed("skp_conv3x3_wino", 0):
+        call("skp_conv3x3_wino", ptr(x), ptr(U), ptr(bias) if bias is not None else None,
+             ptr(residual) if residual is not None else None, ptr(y), B, C, K, H, W, stream(x.device))
+    return y
+
+
+class Conv3x3(torch.autograd.Function):
+    """y = conv2d(x, w, bias, padding=1) (+ residual) with a frozen 3×3 weight; the input
+    gradient is the same Winograd kernel on the flipped weight (MIOpen when its shape is not
+    eligible).  Gradients: x and residual only."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual):
+        x = _c(x)
+        K = weight.shape[0]
+        y = _wino_launch(x, _wino_u(weight, False), None if bias is None else _c(bias.detach()),
+                         None if residual is None else _c(residual), K)
+        ctx.weight = weight
+        ctx.xshape = x.shape
+        ctx.has_res = residual is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        w = ctx.weight
+        B, C, H, W = ctx.xshape
+        K = w.shape[0]
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dy = _c(dy)
+            if wino_eligible(B, K, C, H, W):
+                dx = _wino_launch(dy, _wino_u(w, True), None, None, C)
+            else:
+                dx = torch.nn.grad.conv2d_input(ctx.xshape, w.detach(), dy, padding=1)
+        return dx, None, None, (dy if ctx.has_res else None)
+
+
+def conv3x3(x, weight, bias=None, residual=None):
+    """3×3 / stride 1 / pad 1 convolution (+ bias, + residual) of NCHW fp32 ``x`` with a frozen
+    ``weight`` (K, C, 3, 3): the Winograd F(4×4, 3×3) kernel when the shape is eligible, else
+    MIOpen (F.conv2d) with the bias and residual added after."""
+    _lib.require_device(x)
+    if weight.requires_grad:
+        raise ValueError("conv3x3: the weight must be frozen (requires_grad=False)")
+    B, C, H, W = x.shape
+    K = weight.shape[0]
+    if tuple(weight.shape[1:]) != (C, 3, 3):
+        raise ValueError(f"conv3x3: weight {tuple(weight.shape)} does not fit input {tuple(x.shape)}")
+    if residual is not None and tuple(residual.shape) != (B, K, H, W):
+        raise ValueError(f"conv3x3: residual {tuple(residual.shape)} is not ({B}, {K}, {H}, {W})")
+    if x.dtype != F32 or not wino_eligible(B, C, K, H, W):
+        y = torch.nn.functional.conv2d(x, weight, bias, 1, 1)
+        return y if residual is None else residual + y
+    return Conv3x3.apply(x, weight, bias, residual)

@@ -210,15 +210,15 @@ class ResnetBlock2D(nn.Module):
         if _fused(x, self.conv1, self.conv2, self.norm2):
             # conv1's bias and the time embedding enter norm2 as its input shift, conv2's bias
             # the residual add: neither is a separate pass over the activations
-            h = F.conv2d(gn_act(self.norm1, x, True), self.conv1.weight, None, 1, 1)
+            # (3×3 convolutions: Winograd F(4×4, 3×3) where the shape fills the chip, else MIOpen)
+            from .. import ops
+            h = ops.conv3x3(gn_act(self.norm1, x, True), self.conv1.weight)
             shift = self.conv1.bias[None]
             if temb is not None and self.time_emb_proj is not None:
                 shift = shift + self.time_emb_proj(F.silu(temb))
-            h = F.conv2d(self.dropout(gn_act(self.norm2, h, True, shift)), self.conv2.weight, None, 1, 1)
             if self.conv_shortcut is not None:
                 x = self.conv_shortcut(x)
-            from .. import ops
-            return ops.residual_bias_add(x, h, self.conv2.bias)
+            return ops.conv3x3(self.dropout(gn_act(self.norm2, h, True, shift)), self.conv2.weight, self.conv2.bias, x)
         h = self.conv1(gn_act(self.norm1, x, True))
         if temb is not None and self.time_emb_proj is not None:
             h = h + self.time_emb_proj(F.silu(temb))[:, :, None, None]
@@ -250,6 +250,9 @@ class Upsample2D(nn.Module):
             x = F.interpolate(x, scale_factor=2.0, mode="nearest")
         else:
             x = F.interpolate(x, size=output_size, mode="nearest")
+        if _fused(x, self.conv):
+            from .. import ops
+            return ops.conv3x3(x, self.conv.weight, self.conv.bias)
         return self.conv(x)
 
 

@@ -1,0 +1,116 @@
+"""skp_conv3x3_wino (Winograd F(4×4, 3×3) on the fp32 matrix cores) vs torch fp64.
+
+The VAE encoder and UNet 3×3 convolutions run through ops.conv3x3.  Tolerance: the max
+error relative to the output's max magnitude stays below 3e-5 (a direct fp32 sum of the same
+length sits near 1e-6; F(4×4) with the points (0, ±1, 1/2, -2) measured ≈3× that on CPU, the
+bound leaves room for accumulation order).  Input gradients are checked the same way.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+@pytest.fixture
+def all_shapes(monkeypatch):
+    from stablekeypoints_amd import ops
+    monkeypatch.setattr(ops, "WINO_MIN_WORKGROUPS", 1)
+    return ops
+
+
+def _rel(a, b):
+    return ((a.double() - b).abs().max() / b.abs().max()).item()
+
+
+@pytest.mark.parametrize("B,C,K,H,W", [(2, 64, 64, 32, 32), (2, 4, 32, 20, 20), (1, 32, 96, 12, 28),
+                                       (3, 128, 64, 16, 8), (1, 512, 64, 8, 8), (2, 36, 32, 4, 4)])
+@pytest.mark.parametrize("bias,res", [(False, False), (True, False), (True, True)])
+def test_conv3x3_forward_vs_fp64(all_shapes, B, C, K, H, W, bias, res):
+    ops = all_shapes
+    g = torch.Generator().manual_seed(B * 1000 + C + K + H)
+    x = torch.randn(B, C, H, W, generator=g)
+    w = torch.randn(K, C, 3, 3, generator=g) / (3 * C ** 0.5)
+    b = torch.randn(K, generator=g) if bias else None
+    r = torch.randn(B, K, H, W, generator=g) if res else None
+    y = ops.conv3x3(x.to(DEV), w.to(DEV), None if b is None else b.to(DEV), None if r is None else r.to(DEV))
+    ref = F.conv2d(x.double(), w.double(), None if b is None else b.double(), 1, 1)
+    if r is not None:
+        ref = ref + r.double()
+    assert y.shape == ref.shape
+    assert _rel(y.cpu(), ref) < 3e-5
+
+
+@pytest.mark.parametrize("B,C,K,H,W", [(2, 64, 32, 16, 16), (1, 32, 64, 12, 20), (2, 320, 320, 8, 8)])
+def test_conv3x3_input_gradient_vs_fp64(all_shapes, B, C, K, H, W):
+    ops = all_shapes
+    g = torch.Generator().manual_seed(K + H)
+    x = torch.randn(B, C, H, W, generator=g)
+    w = torch.randn(K, C, 3, 3, generator=g) / (3 * C ** 0.5)
+    r = torch.randn(B, K, H, W, generator=g)
+    dy = torch.randn(B, K, H, W, generator=g)
+    xd, rd = x.to(DEV).requires_grad_(True), r.to(DEV).requires_grad_(True)
+    y = ops.conv3x3(xd, w.to(DEV), None, rd)
+    (y * dy.to(DEV)).sum().backward()
+    x64 = x.double().requires_grad_(True)
+    (F.conv2d(x64, w.double(), None, 1, 1) * dy.double()).sum().backward()
+    assert _rel(xd.grad.cpu(), x64.grad) < 3e-5
+    assert torch.equal(rd.grad.cpu(), dy)
+
+
+def test_conv3x3_vae_shape_and_weight_cache(all_shapes):
+    """A full-size VAE layer (128 channels at 512², batch 1) and the transformed-weight cache:
+    an in-place weight update invalidates it."""
+    ops = all_shapes
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x = torch.randn(1, 128, 512, 512, device=DEV, generator=g)
+    w = torch.randn(128, 128, 3, 3, device=DEV, generator=g) / 34
+    b = torch.randn(128, device=DEV, generator=g)
+    y = ops.conv3x3(x, w, b)
+    ref = F.conv2d(x.double(), w.double(), b.double(), 1, 1)
+    assert _rel(y, ref) < 3e-5
+    with torch.no_grad():
+        w.mul_(-2.0)
+    y2 = ops.conv3x3(x, w, b)
+    ref2 = F.conv2d(x.double(), w.double(), b.double(), 1, 1)
+    assert _rel(y2, ref2) < 3e-5
+
+
+def test_conv3x3_falls_back_to_miopen_for_ineligible_shapes():
+    """conv_in (3 channels) / conv_out (8 channels) shapes go to MIOpen, not the Winograd kernel."""
+    from stablekeypoints_amd import ops
+    x = torch.randn(1, 3, 16, 16, device=DEV)
+    w = torch.randn(32, 3, 3, 3, device=DEV)
+    assert not ops.wino_eligible(1, 3, 32, 16, 16, min_workgroups=1)
+    assert torch.allclose(ops.conv3x3(x, w), F.conv2d(x, w, None, 1, 1), atol=1e-5)
+
+
+def test_sd_models_winograd_vs_miopen(monkeypatch):
+    """The tiny SD UNet (forward + context gradient) and VAE encoder with every eligible 3×3
+    convolution on the Winograd kernel equal the same models on MIOpen (within 1e-4)."""
+    from stablekeypoints_amd import ops
+    from stablekeypoints_amd.sd import build_sd15, TINY_CONFIG
+    ldm = build_sd15(seed=0, config=TINY_CONFIG, device=DEV)
+    gen = torch.Generator(device=DEV).manual_seed(0)
+    img = torch.rand(2, 3, 128, 128, device=DEV, generator=gen) * 2 - 1
+    lat = torch.randn(2, 4, 16, 16, device=DEV, generator=gen)
+    ctx0 = torch.randn(1, 16, 32, device=DEV, generator=gen)
+    outs = []
+    for thresh in (10 ** 9, 1):
+        monkeypatch.setattr(ops, "WINO_MIN_WORKGROUPS", thresh)
+        with torch.no_grad():
+            z = ldm.vae.encode(img)["latent_dist"].mean
+        ctx = ctx0.clone().requires_grad_(True)
+        out = ldm.unet(lat, torch.tensor(0, device=DEV).repeat(2), ctx.repeat(2, 1, 1))["sample"]
+        out.square().mean().backward()
+        outs.append((z, out.detach(), ctx.grad.detach()))
+    for a, b in zip(outs[0], outs[1]):
+        assert _rel(b, a.double()) < 1e-4
