@@ -211,6 +211,8 @@ def main():
     ap.add_argument("--upsample-res", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--conv-benchmark", type=int, default=0, help="torch.backends.cudnn.benchmark (MIOpen exhaustive find)")
+    ap.add_argument("--conv", default="wino", choices=["wino", "miopen"],
+                    help="3x3 stride-1 convolutions: skp_conv3x3_wino where eligible, or MIOpen throughout")
     ap.add_argument("--attn-backend", default="math", choices=["math", "sdpa"],
                     help="un-captured UNet attention: explicit fp32 GEMM+softmax (math) or torch SDPA")
     ap.add_argument("--micro-batch", type=int, default=0,
@@ -239,6 +241,8 @@ def main():
     from stablekeypoints_amd.optimize import TokenOptimizer
     CrossAttention.backend = args.attn_backend
     torch.backends.cudnn.benchmark = bool(args.conv_benchmark)
+    if args.conv == "miopen":
+        ops.WINO_MIN_WORKGROUPS = 1 << 30
     from stablekeypoints_amd.optimize_token import load_ldm
     from stablekeypoints_amd.datasets import SyntheticDataset
 
