@@ -174,10 +174,20 @@ int skp_residual_bias_add(const float* a, const float* h, const float* bias, int
  *   rotated 180° and transposed (flip 1).  K % 32 == 0.
  * skp_conv3x3_wino: y (B, K, H, W) = conv(x (B, C, H, W), w) + bias[k] (bias may be NULL)
  *   + residual (B, K, H, W) (may be NULL).  C % 4 == 0, K % 32 == 0, H % 4 == W % 4 == 0,
- *   16-byte aligned tensors.                                                   */
+ *   16-byte aligned tensors.  nsplit > 1 splits the input channels over nsplit workgroup sets
+ *   (C % (4·nsplit) == 0) for grids too small to fill the chip: partial sums go to ws
+ *   (nsplit·B·K·H·W floats) and one pass adds them (in split order), the bias and the
+ *   residual into y.  nsplit == 1: ws unused (may be NULL).                     */
 int skp_wino_weights(const float* w, int K, int C, int flip, float* U, void* stream);
 int skp_conv3x3_wino(const float* x, const float* U, const float* bias, const float* residual, float* y, int B, int C,
-                     int K, int H, int W, void* stream);
+                     int K, int H, int W, int nsplit, float* ws, void* stream);
+/* The same convolution for H % 32 == W % 32 == 0 (workgroup = 32×32 output pixels × 32
+ * channels, three stages of input region and weights in flight, transforms straight into the
+ * MFMA operands).  skp_wino2_weights writes U as [K/32][C][32][40] (positions 0..17 at 0..17,
+ * 18..35 at 20..37, zero pads); flip as above.                                              */
+int skp_wino2_weights(const float* w, int K, int C, int flip, float* U, void* stream);
+int skp_conv3x3_wino2(const float* x, const float* U, const float* bias, const float* residual, float* y, int B,
+                      int C, int K, int H, int W, int nsplit, float* ws, void* stream);
 
 #ifdef __cplusplus
 }

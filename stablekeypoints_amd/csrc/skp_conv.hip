@@ -159,17 +159,21 @@ template <int EPI>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void wino_f4_kernel(
     const float* __restrict__ x, const float* __restrict__ U, const float* __restrict__ bias,
     const float* __restrict__ res, float* __restrict__ y, int nimg, int C, int K, int H, int W, int tw, int tpi,
-    int ntiles, int ntb, int nkb, int kb_major, int dbg) {
+    int ntiles, int ntb, int nkb, int kb_major, int csplit, int dbg) {
   // separate LDS objects per buffer, so the compiler can tell a DMA into one buffer from a
   // ds_read of another and does not wait for the DMA before every LDS read
   __shared__ __attribute__((aligned(16))) float V0[kVs], V1[kVs];   // [kCK][kMT][kP]
   __shared__ __attribute__((aligned(16))) float U0[kUs], U1[kUs];   // [kCK][kNC][kP]
   __shared__ __attribute__((aligned(16))) char Raw[4 * kRawWave];   // [4 waves][6 rows][mid | left | right]
 
-  // workgroup → (tile block, channel block); consecutive logical ids share one XCD
+  // workgroup → (input-channel split, tile block, channel block); consecutive logical ids share
+  // one XCD.  With csplit < C the workgroup sums input channels [sp·csplit, (sp+1)·csplit) only
+  // and writes its partial to slab sp of y (the caller's workspace).
   const int G = gridDim.x;
   const int g = blockIdx.x;
-  const int L = (G % 8 == 0) ? (g % 8) * (G / 8) + g / 8 : g;
+  const int Lg = (G % 8 == 0) ? (g % 8) * (G / 8) + g / 8 : g;
+  const int sp = Lg / (ntb * nkb);
+  const int L = Lg - sp * (ntb * nkb);
   int tb, kb;
   if (kb_major) {
     kb = L / ntb;
@@ -178,6 +182,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
     tb = L / nkb;
     kb = L - tb * nkb;
   }
+  const int c0 = sp * csplit;
+  y += (size_t)sp * nimg * K * H * W;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -207,14 +213,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
       pa.row[r] = (base + (unsigned)(yc * W + px0)) * 4u;
     }
   }
-  const float* Ub = U + (size_t)kb * C * kNC * kP;
-  const int nst = C / kCK;
+  const float* Ub = U + ((size_t)kb * C + c0) * kNC * kP;
+  const int nst = csplit / kCK;
   const size_t xfloats = (size_t)nimg * C * plane;
   char* raw = Raw + (wv & 3) * kRawWave;
   const int vrow = ((wv & 3) * kMT + lane) * kP;   // this patcher lane's V row
   // per-stage descriptors: x from the stage's first channel plane, U from the stage's slice
   auto xrsrc = [&](int s) {
-    const size_t off = (size_t)s * kCK * plane;
+    const size_t off = ((size_t)c0 + (size_t)s * kCK) * plane;
     return __builtin_amdgcn_make_buffer_rsrc((void*)(x + off), (short)0, (dbg & 1) ? 0 : (int)((xfloats - off) * 4), 0x00020000);
   };
   auto dma_u = [&](int s, float* ubuf) {
@@ -250,7 +256,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
   auto phase = [&](int s, const float* vc, const float* uc, float* vn, float* un) {
     if (s + 1 < nst) {
       if (patcher) {
-        transform_patch(raw, pa.mask, lane, vn + vrow);
+        if (!(dbg & 4)) transform_patch(raw, pa.mask, lane, vn + vrow);
         if (s + 2 < nst) dma_patches(xrsrc(s + 2), pa, raw);
       } else {
         dma_u(s + 1, un);
@@ -260,6 +266,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
     const float* ub = uc + boff;
 #pragma unroll
     for (int q = 0; q < 9; ++q) {
+      if (dbg & 8) break;
       const float4 a = *reinterpret_cast<const float4*>(va + 4 * q);
       const float4 b = *reinterpret_cast<const float4*>(ub + 4 * q);
       acc[4 * q + 0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc[4 * q + 0], 0, 0, 0);
@@ -345,31 +352,80 @@ extern "C" int skp_wino_weights(const float* w, int K, int C, int flip, float* U
   return SKP_OK;
 }
 
+namespace {
+
+// y = Σ_s ws[s] + bias[k] + residual over (B, K, HW), float4 lanes (HW % 4 == 0)
+__global__ void splitk_reduce_kernel(const float4* __restrict__ ws, int nsplit, long long n4, int K, int hw4,
+                                     const float* __restrict__ bias, const float4* __restrict__ res,
+                                     float4* __restrict__ y) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  float4 v = ws[i];
+  for (int s = 1; s < nsplit; ++s) {
+    const float4 p = ws[(long long)s * n4 + i];
+    v.x += p.x;
+    v.y += p.y;
+    v.z += p.z;
+    v.w += p.w;
+  }
+  if (bias) {
+    const float b = bias[(i / hw4) % K];
+    v.x += b;
+    v.y += b;
+    v.z += b;
+    v.w += b;
+  }
+  if (res) {
+    const float4 r = res[i];
+    v.x += r.x;
+    v.y += r.y;
+    v.z += r.z;
+    v.w += r.w;
+  }
+  y[i] = v;
+}
+
+int splitk_reduce(const float* ws, int nsplit, int B, int K, int HW, const float* bias, const float* residual,
+                  float* y, hipStream_t st) {
+  const long long n4 = (long long)B * K * HW / 4;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st,
+                     reinterpret_cast<const float4*>(ws), nsplit, n4, K, HW / 4, bias,
+                     reinterpret_cast<const float4*>(residual), reinterpret_cast<float4*>(y));
+  SKP_LAUNCH_CHECK();
+  return SKP_OK;
+}
+
+}  // namespace
+
 extern "C" int skp_conv3x3_wino(const float* x, const float* U, const float* bias, const float* residual, float* y,
-                                int B, int C, int K, int H, int W, void* stream) {
+                                int B, int C, int K, int H, int W, int nsplit, float* ws, void* stream) {
   SKP_CHECK_ARG(x && U && y, "null pointer");
   SKP_CHECK_ARG(B > 0 && C > 0 && K > 0 && H > 0 && W > 0, "non-positive shape");
   SKP_CHECK_ARG(C % kCK == 0, "input channels must be a multiple of 4");
   SKP_CHECK_ARG(K % kNC == 0, "output channels must be a multiple of 32");
   SKP_CHECK_ARG(H % 4 == 0 && W % 4 == 0, "H and W must be multiples of 4");
-  SKP_CHECK_ARG(aligned16(x) && aligned16(U) && aligned16(y) && (!residual || aligned16(residual)),
+  SKP_CHECK_ARG(nsplit >= 1 && C % (kCK * nsplit) == 0, "nsplit must divide C into multiples of 4");
+  SKP_CHECK_ARG(nsplit == 1 || ws, "split-K needs a workspace of nsplit·B·K·H·W floats");
+  SKP_CHECK_ARG(aligned16(x) && aligned16(U) && aligned16(y) && (!residual || aligned16(residual)) &&
+                    (!ws || aligned16(ws)),
                 "tensors must be 16-byte aligned");
   const int tw = W / 4, tpi = (H / 4) * tw;
   const long long ntiles = (long long)B * tpi;
   SKP_CHECK_ARG(ntiles <= 0x7fffffffLL - kMT, "too many tiles");
   SKP_CHECK_ARG((long long)B * C * H * W * 4 < 0x7fffffffLL, "input larger than 2 GiB (32-bit buffer offsets)");
   const int ntb = (int)((ntiles + kMT - 1) / kMT), nkb = K / kNC;
-  SKP_CHECK_ARG((long long)ntb * nkb <= 0x7fffffffLL, "grid too large");
+  SKP_CHECK_ARG((long long)ntb * nkb * nsplit <= 0x7fffffffLL, "grid too large");
   // one channel block's U slice is C·32·36·4 B; keep all of U on an L2 slice when it fits
   const long long ubytes = (long long)K * C * kP * 4;
   const int kb_major = ubytes > (2LL << 20);
-  const int epi = (bias ? 1 : 0) | (residual ? 2 : 0);
-  static const int dbg = getenv("SKP_WINO_DEBUG") ? atoi(getenv("SKP_WINO_DEBUG")) : 0;   // dev: 1 drop x loads, 2 drop U loads
+  const int epi = nsplit > 1 ? 0 : (bias ? 1 : 0) | (residual ? 2 : 0);
+  float* out = nsplit > 1 ? ws : y;
+  static const int dbg = getenv("SKP_WINO_DEBUG") ? atoi(getenv("SKP_WINO_DEBUG")) : 0;   // dev: 1 drop x loads, 2 drop U loads, 4 skip transforms, 8 skip MFMAs
   hipStream_t st = as_stream(stream);
-  const dim3 grid((unsigned)(ntb * nkb));
-#define SKP_WG(E)                                                                                                 \
-  hipLaunchKernelGGL((wino_f4_kernel<E>), grid, dim3(kThreads), 0, st, x, U, bias, residual, y, B, C, K, H, W, \
-                     tw, tpi, (int)ntiles, ntb, nkb, kb_major, dbg)
+  const dim3 grid((unsigned)(ntb * nkb * nsplit));
+#define SKP_WG(E)                                                                                                   \
+  hipLaunchKernelGGL((wino_f4_kernel<E>), grid, dim3(kThreads), 0, st, x, U, bias, residual, out, B, C, K, H, W, \
+                     tw, tpi, (int)ntiles, ntb, nkb, kb_major, C / nsplit, dbg)
   switch (epi) {
     case 0: SKP_WG(0); break;
     case 1: SKP_WG(1); break;
@@ -378,5 +434,453 @@ extern "C" int skp_conv3x3_wino(const float* x, const float* U, const float* bia
   }
 #undef SKP_WG
   SKP_LAUNCH_CHECK();
+  if (nsplit > 1) return splitk_reduce(ws, nsplit, B, K, H * W, bias, residual, y, st);
+  return SKP_OK;
+}
+
+// ================================================================================================
+// Winograd F(4×4, 3×3), region-staged version for H and W multiples of 32 (every VAE-encoder
+// layer at 512² input and the UNet's 64² / 32² layers).
+//
+// The kernel above is bound by its one-deep pipeline: every stage waits for LDS-DMA it issued
+// in the same stage (≈1 µs under load, about one stage of MFMA work), and with neither
+// transforms nor MFMAs it still takes half its time.  This one keeps three stages in flight:
+//   - a workgroup owns an 8×8 block of output tiles (32×32 pixels) × 32 output channels; per
+//     stage of 4 input channels it DMAs the block's 34×34-pixel input region as rows of ten
+//     16-byte chunks (columns x0-4 … x0+35; rows and chunks outside the image load as zeros —
+//     out-of-range buffer offsets — so the zero padding costs no masking) and the stage's U
+//     slice, into 3-slot LDS rings, two stages ahead of use;
+//   - the transformed input never goes through LDS: lane (tile, channel) of a wave reads its
+//     own 6×6 patch (three ds_read_b128 per row) and computes the V values that are exactly its
+//     MFMA A operand.  The two waves of a SIMD (w, w+4) share the 16 tiles and split the 36
+//     positions by transform rows (0-2 / 3-5), so no transform work is repeated: each runs half
+//     of the column pass and half of the row pass;
+//   - a wave owns 16 tiles × 32 channels × 18 positions (2 MFMA blocks, 144 accumulators) and
+//     transforms stage s+1 while its MFMAs run on stage s (the A operands are double-buffered
+//     in registers);
+//   - one barrier per stage; the epilogue applies the output transform to each half's rows and
+//     the partner waves exchange the half-sums through LDS (two rounds of 8 KB per wave).
+// ================================================================================================
+namespace {
+namespace w2 {
+
+constexpr int kNC = 32;                    // output channels per workgroup
+constexpr int kCK = 4;                     // input channels per stage
+constexpr int kRowF = 40;                  // floats per region row (ten 16-B chunks)
+constexpr int kChF = 1408;                 // floats per channel's region (34 rows + pad; ≡ 0 mod 64)
+constexpr int kRawF = kCK * kChF;          // 5632 floats = 22 KB per raw slot
+constexpr int kRawInstr = kRawF / 256;     // 22 1-KB DMA chunks
+constexpr int kUP = 40;                    // floats per (input, output channel) U row
+constexpr int kUF = kCK * kNC * kUP;       // 5120 floats = 20 KB per U slot
+constexpr int kUInstr = kUF / 256;         // 20
+constexpr int kInstr = kRawInstr + kUInstr;   // 42 per stage, ≤ 6 per wave
+constexpr int kThreads = 512;
+constexpr unsigned kOOB = 0x80000000u;     // buffer offset past any num_records (< 2 GiB): loads 0
+static_assert(kRawF % 256 == 0 && kUF % 256 == 0, "whole 1-KB chunks");
+static_assert(3 * (kRawF + kUF) * 4 <= 160 * 1024, "LDS");
+static_assert(2 * 8 * 1024 <= kUF * 4, "epilogue exchange: two waves' 8 KB per ring buffer");
+
+// Bᵀ (rows i = transform row, columns a = patch row) for the points (0, 1, -1, 1/2, -2, ∞)
+__device__ constexpr float kBt[6][6] = {{1.f, -1.5f, -2.f, 1.5f, 1.f, 0.f},  {0.f, -1.f, 0.5f, 2.5f, 1.f, 0.f},
+                                        {0.f, 1.f, -2.5f, 0.5f, 1.f, 0.f},  {0.f, -2.f, -1.f, 2.f, 1.f, 0.f},
+                                        {0.f, 0.5f, -1.f, -0.5f, 1.f, 0.f}, {0.f, 1.f, -1.5f, -2.f, 1.5f, 1.f}};
+// Aᵀ (4 outputs × 6 positions)
+__device__ constexpr float kAt[4][6] = {{1.f, 1.f, 1.f, 1.f, 1.f, 0.f},
+                                        {0.f, 1.f, -1.f, 0.5f, -2.f, 0.f},
+                                        {0.f, 1.f, 1.f, 0.25f, 4.f, 0.f},
+                                        {0.f, 1.f, -1.f, 0.125f, -8.f, 1.f}};
+
+// s_waitcnt vmcnt(n) with expcnt / lgkmcnt left alone (gfx9 encoding)
+#define W2_VMCNT(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (((n) >> 4) << 14) | (7 << 4) | (15 << 8))
+
+// Transform rows 3H..3H+2 of V = Bᵀ d B for this lane's patch (region rows at `raw`, the
+// patch's first row; columns: .w of chunk 0, chunk 1, .x of chunk 2) → a[18] = V[3H+ii][j].
+template <int H>
+__device__ __forceinline__ void half_transform(const float* raw, float* a) {
+  float t[3][6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    const float4 c0 = *reinterpret_cast<const float4*>(raw + r * kRowF);
+    const float4 c1 = *reinterpret_cast<const float4*>(raw + r * kRowF + 4);
+    const float4 c2 = *reinterpret_cast<const float4*>(raw + r * kRowF + 8);
+    const float d[6] = {c0.w, c1.x, c1.y, c1.z, c1.w, c2.x};
+#pragma unroll
+    for (int ii = 0; ii < 3; ++ii) {
+      const float c = kBt[3 * H + ii][r];
+      if (c == 0.0f) continue;
+      bool first = true;   // the first nonzero coefficient of row 3H+ii (compile time)
+#pragma unroll
+      for (int rp = 0; rp < r; ++rp)
+        if (kBt[3 * H + ii][rp] != 0.0f) first = false;
+#pragma unroll
+      for (int b = 0; b < 6; ++b)
+        t[ii][b] = first ? ((c == 1.0f) ? d[b] : c * d[b]) : ((c == 1.0f) ? t[ii][b] + d[b] : fmaf(c, d[b], t[ii][b]));
+    }
+  }
+#pragma unroll
+  for (int ii = 0; ii < 3; ++ii) bt6(t[ii][0], t[ii][1], t[ii][2], t[ii][3], t[ii][4], t[ii][5], a + 6 * ii, 1);
+}
+
+// partial output tile of rows 3H..3H+2 of M (m[18] = M[3H+ii][j]) → y[16] (row-major 4×4)
+template <int H>
+__device__ __forceinline__ void half_output(const float* m, float* y) {
+  float s[3][4];
+#pragma unroll
+  for (int ii = 0; ii < 3; ++ii) at6(m[6 * ii], m[6 * ii + 1], m[6 * ii + 2], m[6 * ii + 3], m[6 * ii + 4], m[6 * ii + 5], s[ii], 1);
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float v = 0.0f;
+      bool first = true;
+#pragma unroll
+      for (int ii = 0; ii < 3; ++ii) {
+        const float a = kAt[r][3 * H + ii];
+        if (a == 0.0f) continue;
+        v = first ? ((a == 1.0f) ? s[ii][c] : a * s[ii][c]) : fmaf(a, s[ii][c], v);
+        first = false;
+      }
+      y[4 * r + c] = v;
+    }
+}
+
+}  // namespace w2
+
+struct W2Smem {
+  float *R0, *R1, *R2, *U0, *U1, *U2;
+};
+
+// One wave's whole program for transform half HH (rows 3HH..3HH+2); the kernel branches once
+// on the wave's half so the stage loop is straight-line code for each.
+template <int EPI, int HH>
+__device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __restrict__ x, const float* __restrict__ U,
+                                           const float* __restrict__ bias, const float* __restrict__ res,
+                                           float* __restrict__ y, int C, int K, int H, int W, int img, int x0,
+                                           int y0, int kb, int c0, int csplit, int wv, int dbg) {
+  using w2::kChF;
+  using w2::kInstr;
+  using w2::kRawF;
+  using w2::kRawInstr;
+  using w2::kRowF;
+  using w2::kUF;
+  using w2::kUP;
+  float *R0 = sm.R0, *R1 = sm.R1, *R2 = sm.R2, *U0 = sm.U0, *U1 = sm.U1, *U2 = sm.U2;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wm = wv & 3;
+  const size_t plane = (size_t)H * W;
+  const size_t ximg = (size_t)img * C * plane;
+
+  // this wave's DMA chunks of a stage: chunk g = wv + 8m (raw chunks 0..21, then U chunks 0..19)
+  unsigned voff[3];
+  int nraw = 0;
+#pragma unroll
+  for (int m = 0; m < 3; ++m) {
+    const int gi = wv + 8 * m;
+    voff[m] = w2::kOOB;
+    if (gi < kRawInstr) {
+      ++nraw;
+      const int f = 64 * gi + lane;   // 16-B chunk of the slot
+      const int ch = f / (kChF / 4);
+      const int e = f - ch * (kChF / 4);
+      const int row = e / 10, c4 = e - row * 10;
+      const int yy = y0 - 1 + row, xx = x0 - 4 + 4 * c4;
+      if (row < 34 && yy >= 0 && yy < H && xx >= 0 && xx < W)
+        voff[m] = (unsigned)((ximg + (size_t)ch * plane + (size_t)yy * W + xx) * 4);
+    }
+  }
+  const int nuw = (kInstr - 1 - wv) / 8 + 1 - nraw;   // U chunks of this wave
+  const int ufirst = wv + 8 * nraw - kRawInstr;       // its first U chunk
+  const bool six = nraw + nuw == 6;                   // DMA instructions per stage group: 6 or 5
+  const size_t xend = (size_t)(img + 1) * C * plane;  // the buffer ends with this image
+  const float* Ub = U + ((size_t)kb * C + c0) * w2::kNC * kUP;
+  const int nst = csplit / w2::kCK;
+
+  // group t = {raw(t+1) → raw slot (t+1)%3, U(t) → U slot t%3}
+  auto issue_raw = [&](int t, float* rs_lds) {
+    const bool ok = t < nst;
+    const size_t off = ((size_t)c0 + (size_t)(ok ? t : 0) * w2::kCK) * plane;
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(x + off), (short)0, ok ? (int)((xend - off) * 4) : 0, 0x00020000);
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+      if (m < nraw && !(dbg & 4))
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)(rs_lds + 256 * (wv + 8 * m)), 16, voff[m], 0, 0, 0);
+  };
+  auto issue_group = [&](int t, float* rs_lds, float* us_lds) {
+    issue_raw(t + 1, rs_lds);
+    const __amdgpu_buffer_rsrc_t ru =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(Ub + (size_t)t * kUF), (short)0, kUF * 4, 0x00020000);
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      if (m < nuw && !(dbg & 8)) {
+        const int q = ufirst + 8 * m;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ru, (lds_ptr_t)(us_lds + 256 * q), 16, lane * 16, q * 1024, 0, 0);
+      }
+  };
+
+  // lane → (tile, stage channel) = its A-operand row; the patch's first row in the region
+  const int tx = lane & 7, ty = 2 * wm + ((lane >> 3) & 1), kc = lane >> 4;
+  const int roff = kc * kChF + 4 * ty * kRowF + 4 * tx;
+  // B operand: U[kc][16 blk + (lane & 15)][18 HH + q] (rows padded to 40, halves at 0 and 20)
+  const int uoff = (kc * w2::kNC + (lane & 15)) * kUP + 20 * HH;
+
+  f32x4 acc[2][18];
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int q = 0; q < 18; ++q) acc[b][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float acur[18], anext[18];
+
+  auto mfmas = [&](const float* us) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const float* ub = us + uoff + b * 16 * kUP;
+      float u[18];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 v = *reinterpret_cast<const float4*>(ub + 4 * j);
+        u[4 * j] = v.x;
+        u[4 * j + 1] = v.y;
+        u[4 * j + 2] = v.z;
+        u[4 * j + 3] = v.w;
+      }
+      const float2 v2 = *reinterpret_cast<const float2*>(ub + 16);
+      u[16] = v2.x;
+      u[17] = v2.y;
+#pragma unroll
+      for (int q = 0; q < 18; ++q) acc[b][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(acur[q], u[q], acc[b][q], 0, 0, 0);
+    }
+  };
+
+  // prologue: raw(0), groups 0 and 1; wait for raw(0) and transform it
+  issue_raw(0, R0);
+  issue_group(0, R1, U0);
+  if (nst > 1) issue_group(1, R2, U1);
+  if (nst > 1) {
+    if (six) W2_VMCNT(12);
+    else W2_VMCNT(10);
+  } else {
+    W2_VMCNT(0);
+  }
+  __syncthreads();
+  w2::half_transform<HH>(R0 + roff, acur);
+
+  // stage s: wait for group s (raw(s+1), U(s)); barrier; issue group s+2 into the slots freed by
+  // stage s-1; transform raw(s+1) (slot (s+1)%3) and run the MFMAs on U(s) (slot s%3).  The SIMD
+  // partners (waves w, w+4: the two halves) do these in opposite orders, so one's transform
+  // (VALU) runs beside the other's MFMAs.
+  auto step = [&](int s, float* Rn, float* Us, float* Ri, float* Ui) {
+    if (s + 1 < nst) {
+      if (six) W2_VMCNT(6);
+      else W2_VMCNT(5);
+    } else {
+      W2_VMCNT(0);
+    }
+    __syncthreads();
+    if (s + 2 < nst) issue_group(s + 2, Ri, Ui);
+    const bool tr = s + 1 < nst && !(dbg & 1);
+    if (HH == 0) {
+      if (tr) w2::half_transform<HH>(Rn + roff, anext);
+      if (!(dbg & 2)) mfmas(Us);
+    } else {
+      if (!(dbg & 2)) mfmas(Us);
+      if (tr) w2::half_transform<HH>(Rn + roff, anext);
+    }
+#pragma unroll
+    for (int q = 0; q < 18; ++q) acur[q] = anext[q];
+  };
+  for (int s = 0; s < ((dbg & 16) ? 0 : nst); s += 3) {
+    step(s, R1, U0, R0, U2);
+    if (s + 1 < nst) step(s + 1, R2, U1, R1, U0);
+    if (s + 2 < nst) step(s + 2, R0, U2, R2, U1);
+  }
+
+  // epilogue: lane holds tiles 4(lane>>4)+r of the wave's 16 (ty = 2wm + (lane>>5),
+  // tx = 4((lane>>4)&1) + r) × channel 16 blk + (lane&15), rows 3HH..3HH+2 of M.  Per block of 16
+  // channels: the other half's waves stage their partial tiles in LDS ([ch][32 rows][32 px]),
+  // this half's waves add theirs in place, then every thread stores whole 128-B rows.
+  W2_VMCNT(0);
+  __syncthreads();
+  if (dbg & 32) return;
+  // channel c of a block: a 32×32-float plane in R0/R1/R2/U0 (four channels each, skewed by 16
+  // floats per buffer so the 8-lane store groups hit distinct banks)
+  auto plane_of = [&](int c) -> float* {
+    float* b = (c >> 2) == 0 ? R0 : (c >> 2) == 1 ? R1 : (c >> 2) == 2 ? R2 : U0;
+    return b + (c & 3) * 1028 + (c >> 2) * 16;
+  };
+  float* pl = plane_of(lane & 15);
+  const int oty = 2 * wm + (lane >> 5);
+  const int otx0 = 4 * ((lane >> 4) & 1);
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+    if (HH != blk) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float m[18], o[16];
+#pragma unroll
+        for (int q = 0; q < 18; ++q) m[q] = acc[blk][q][r];
+        w2::half_output<HH>(m, o);
+#pragma unroll
+        for (int f = 0; f < 4; ++f)
+          *reinterpret_cast<float4*>(pl + (4 * oty + f) * 32 + 4 * (otx0 + r)) =
+              make_float4(o[4 * f], o[4 * f + 1], o[4 * f + 2], o[4 * f + 3]);
+      }
+    }
+    __syncthreads();
+    if (HH == blk) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float m[18], o[16];
+#pragma unroll
+        for (int q = 0; q < 18; ++q) m[q] = acc[blk][q][r];
+        w2::half_output<HH>(m, o);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          float4* d = reinterpret_cast<float4*>(pl + (4 * oty + f) * 32 + 4 * (otx0 + r));
+          const float4 p = *d;
+          *d = make_float4(o[4 * f] + p.x, o[4 * f + 1] + p.y, o[4 * f + 2] + p.z, o[4 * f + 3] + p.w);
+        }
+      }
+    }
+    __syncthreads();
+    // 16 channels × 32 rows × 8 chunks of 16 B; a wave instruction = 8 whole rows of one channel
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int idx = i * w2::kThreads + tid;
+      const int c = idx >> 8, row = (idx >> 3) & 31, c4 = idx & 7;
+      const float4 v0 = *reinterpret_cast<const float4*>(plane_of(c) + row * 32 + 4 * c4);
+      const int k = kb * w2::kNC + 16 * blk + c;
+      const float bv = (EPI & 1) ? bias[k] : 0.0f;
+      const size_t o = (((size_t)img * K + k) * H + y0 + row) * W + x0 + 4 * c4;
+      float4 v = make_float4(v0.x + bv, v0.y + bv, v0.z + bv, v0.w + bv);
+      if (EPI & 2) {
+        const float4 rv = *reinterpret_cast<const float4*>(res + o);
+        v.x += rv.x;
+        v.y += rv.y;
+        v.z += rv.z;
+        v.w += rv.w;
+      }
+      *reinterpret_cast<float4*>(y + o) = v;
+    }
+    if (blk == 0) __syncthreads();
+  }
+}
+
+template <int EPI>
+__global__ __launch_bounds__(w2::kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void wino2_kernel(
+    const float* __restrict__ x, const float* __restrict__ U, const float* __restrict__ bias,
+    const float* __restrict__ res, float* __restrict__ y, int nimg, int C, int K, int H, int W, int bw, int bpi,
+    int nblk, int nkb, int kb_major, int csplit, int dbg) {
+  // separate LDS objects per ring slot: the compiler tells a DMA into one slot from a ds_read of
+  // another and does not wait for outstanding DMAs before every LDS read
+  __shared__ __attribute__((aligned(16))) float R0[w2::kRawF], R1[w2::kRawF], R2[w2::kRawF];
+  __shared__ __attribute__((aligned(16))) float U0[w2::kUF], U1[w2::kUF], U2[w2::kUF];
+  // workgroup → (input-channel split, 32×32-pixel block, channel block); consecutive logical ids
+  // share one XCD.  A split sums its csplit input channels into slab sp of y (the workspace).
+  const int G = gridDim.x;
+  const int g = blockIdx.x;
+  const int Lg = (G % 8 == 0) ? (g % 8) * (G / 8) + g / 8 : g;
+  const int sp = Lg / (nblk * nkb);
+  const int L = Lg - sp * (nblk * nkb);
+  y += (size_t)sp * nimg * K * H * W;
+  int tb, kb;
+  if (kb_major) {
+    kb = L / nblk;
+    tb = L - kb * nblk;
+  } else {
+    tb = L / nkb;
+    kb = L - tb * nkb;
+  }
+  const int img = tb / bpi;
+  const int br = tb - img * bpi;
+  const int by = br / bw;
+  const int x0 = 32 * (br - by * bw), y0 = 32 * by;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const W2Smem sm{R0, R1, R2, U0, U1, U2};
+  const int c0 = sp * csplit;
+  if (wv < 4) wino2_body<EPI, 0>(sm, x, U, bias, res, y, C, K, H, W, img, x0, y0, kb, c0, csplit, wv, dbg);
+  else wino2_body<EPI, 1>(sm, x, U, bias, res, y, C, K, H, W, img, x0, y0, kb, c0, csplit, wv, dbg);
+}
+
+// U2[kb][c][k%32][40]: positions 0..17 at 0..17, 18..35 at 20..37, the rest zero
+__global__ void wino2_weights_kernel(const float* __restrict__ w, int K, int C, int flip, float* __restrict__ U) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i >= (long long)K * C) return;
+  const int k = (int)(i / C), c = (int)(i - (long long)k * C);
+  double g[9];
+  for (int u = 0; u < 3; ++u)
+    for (int v = 0; v < 3; ++v)
+      g[3 * u + v] = flip ? (double)w[((size_t)c * K + k) * 9 + (2 - u) * 3 + (2 - v)]
+                          : (double)w[((size_t)k * C + c) * 9 + u * 3 + v];
+  const double Gm[6][3] = {{1.0, 0.0, 0.0},
+                           {1.0 / 3, 1.0 / 3, 1.0 / 3},
+                           {-1.0 / 3, 1.0 / 3, -1.0 / 3},
+                           {-16.0 / 15, -8.0 / 15, -4.0 / 15},
+                           {1.0 / 15, -2.0 / 15, 4.0 / 15},
+                           {0.0, 0.0, 1.0}};
+  double t[6][3];
+  for (int a = 0; a < 6; ++a)
+    for (int v = 0; v < 3; ++v) t[a][v] = Gm[a][0] * g[v] + Gm[a][1] * g[3 + v] + Gm[a][2] * g[6 + v];
+  float* out = U + (((size_t)(k / w2::kNC) * C + c) * w2::kNC + (k % w2::kNC)) * w2::kUP;
+  for (int p = 0; p < w2::kUP; ++p) out[p] = 0.0f;
+  for (int a = 0; a < 6; ++a)
+    for (int b = 0; b < 6; ++b) {
+      const int p = 6 * a + b;
+      out[p < 18 ? p : p + 2] = (float)(t[a][0] * Gm[b][0] + t[a][1] * Gm[b][1] + t[a][2] * Gm[b][2]);
+    }
+}
+
+}  // namespace
+
+extern "C" int skp_wino2_weights(const float* w, int K, int C, int flip, float* U, void* stream) {
+  SKP_CHECK_ARG(w && U, "null pointer");
+  SKP_CHECK_ARG(K > 0 && C > 0, "non-positive shape");
+  SKP_CHECK_ARG(K % w2::kNC == 0, "output channels must be a multiple of 32");
+  const long long n = (long long)K * C;
+  hipLaunchKernelGGL(wino2_weights_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), w, K, C,
+                     flip, U);
+  SKP_LAUNCH_CHECK();
+  return SKP_OK;
+}
+
+extern "C" int skp_conv3x3_wino2(const float* x, const float* U, const float* bias, const float* residual, float* y,
+                                 int B, int C, int K, int H, int W, int nsplit, float* ws, void* stream) {
+  SKP_CHECK_ARG(x && U && y, "null pointer");
+  SKP_CHECK_ARG(B > 0 && C > 0 && K > 0 && H > 0 && W > 0, "non-positive shape");
+  SKP_CHECK_ARG(C % w2::kCK == 0, "input channels must be a multiple of 4");
+  SKP_CHECK_ARG(K % w2::kNC == 0, "output channels must be a multiple of 32");
+  SKP_CHECK_ARG(H % 32 == 0 && W % 32 == 0, "H and W must be multiples of 32");
+  SKP_CHECK_ARG(nsplit >= 1 && C % (w2::kCK * nsplit) == 0, "nsplit must divide C into multiples of 4");
+  SKP_CHECK_ARG(nsplit == 1 || ws, "split-K needs a workspace of nsplit·B·K·H·W floats");
+  SKP_CHECK_ARG(aligned16(x) && aligned16(U) && aligned16(y) && (!residual || aligned16(residual)) &&
+                    (!ws || aligned16(ws)),
+                "tensors must be 16-byte aligned");
+  SKP_CHECK_ARG((long long)B * C * H * W * 4 < 0x7fffffffLL, "input larger than 2 GiB (32-bit buffer offsets)");
+  const int bw = W / 32, bpi = (H / 32) * bw;
+  const long long nblk = (long long)B * bpi;
+  const int nkb = K / w2::kNC;
+  SKP_CHECK_ARG(nblk * nkb * nsplit <= 0x7fffffffLL, "grid too large");
+  const long long ubytes = (long long)K * C * w2::kUP * 4;
+  // dev switches (SKP_WINO2_DEBUG): 1 skip transforms, 2 skip MFMAs, 4 skip input DMA, 8 skip weight DMA,
+  // 16 skip the stage loop, 32 skip the epilogue; SKP_WINO2_ORDER 1 tile-major, 2 channel-block-major
+  static const int dbg = getenv("SKP_WINO2_DEBUG") ? atoi(getenv("SKP_WINO2_DEBUG")) : 0;
+  static const int order = getenv("SKP_WINO2_ORDER") ? atoi(getenv("SKP_WINO2_ORDER")) : 0;
+  const int kb_major = order ? order == 2 : ubytes > (2LL << 20);
+  const int epi = nsplit > 1 ? 0 : (bias ? 1 : 0) | (residual ? 2 : 0);
+  float* out = nsplit > 1 ? ws : y;
+  hipStream_t st = as_stream(stream);
+  const dim3 grid((unsigned)(nblk * nkb * nsplit));
+#define SKP_WG2(E)                                                                                              \
+  hipLaunchKernelGGL((wino2_kernel<E>), grid, dim3(w2::kThreads), 0, st, x, U, bias, residual, out, B, C, K, H, W, \
+                     bw, bpi, (int)nblk, nkb, kb_major, C / nsplit, dbg)
+  switch (epi) {
+    case 0: SKP_WG2(0); break;
+    case 1: SKP_WG2(1); break;
+    case 2: SKP_WG2(2); break;
+    default: SKP_WG2(3); break;
+  }
+#undef SKP_WG2
+  SKP_LAUNCH_CHECK();
+  if (nsplit > 1) return splitk_reduce(ws, nsplit, B, K, H * W, bias, residual, y, st);
   return SKP_OK;
 }

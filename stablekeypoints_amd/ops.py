@@ -4,6 +4,7 @@ Every function here launches the HIP kernels through the C ABI (``_lib``) on the
 current HIP stream; there is no CPU or eager-torch fallback for the hot path.
 """
 import ctypes
+import os
 
 import torch
 
@@ -607,45 +608,83 @@ def tokens_proj_out(h, weight, bias, residual):
 # K·C·36 floats; built once, on first use, on the weight's device and stream).
 import weakref as _weakref
 
-_WINO_U = {}   # id(weight) -> (weakref(weight), {flip: (version, U)})
-# Below this many (64-tile × 32-channel) workgroups the Winograd kernel leaves most of the
-# 256 CUs idle and MIOpen's split-K kernels are faster (tools/conv_probe.py --wino at batch 8:
-# 160 workgroups (640 channels at 32²) still win, 80 (1280 at 16²) lose).
+_WINO_U = {}   # id(weight) -> (weakref(weight), {(flip, v2): (version, U)})
+# Shapes whose grid stays below this even after splitting go to MIOpen.
 WINO_MIN_WORKGROUPS = 128
+# Which kernel takes an eligible shape: "auto" = skp_conv3x3_wino2 where H and W are multiples
+# of 32 (every VAE-encoder layer, the UNet's 64² and 32² layers), skp_conv3x3_wino elsewhere;
+# "v1" forces the first kernel (A/B runs: SKP_WINO=v1).  SKP_WINO_SPLIT=0 disables split-K.
+WINO_KERNEL = os.environ.get("SKP_WINO", "auto")
+WINO_SPLIT = os.environ.get("SKP_WINO_SPLIT", "1") != "0"
 
 
-def _wino_u(weight, flip):
+def _wino_v2(H, W):
+    return WINO_KERNEL != "v1" and H % 32 == 0 and W % 32 == 0
+
+
+def _wino_u(weight, flip, v2=False):
     ent = _WINO_U.get(id(weight))
     if ent is None or ent[0]() is not weight:
         key = id(weight)
         ent = (_weakref.ref(weight, lambda _r, key=key: _WINO_U.pop(key, None)), {})
         _WINO_U[key] = ent
     per = ent[1]
-    hit = per.get(flip)
+    hit = per.get((flip, v2))
     if hit is not None and hit[0] == weight._version:
         return hit[1]
     w = _c(weight.detach())
     K, C = (w.shape[0], w.shape[1]) if not flip else (w.shape[1], w.shape[0])
-    U = torch.empty(K * C * 36, device=w.device, dtype=F32)
-    call("skp_wino_weights", ptr(w), K, C, int(flip), ptr(U), stream(w.device))
-    per[flip] = (weight._version, U)
+    U = torch.empty(K * C * (40 if v2 else 36), device=w.device, dtype=F32)
+    call("skp_wino2_weights" if v2 else "skp_wino_weights", ptr(w), K, C, int(flip), ptr(U), stream(w.device))
+    per[(flip, v2)] = (weight._version, U)
     return U
 
 
+def _wino_plan(B, C, K, H, W):
+    """(v2, nsplit, workgroups) for a (B, C, H, W) → (B, K, H, W) convolution.
+
+    One workgroup per CU (their LDS), so a grid runs in ceil(workgroups / 256) rounds of
+    (stages × ≈2.4 µs + ≈5 µs); splitting the input channels S ways shortens a workgroup S-fold
+    and adds (S + 1) passes over the output for the partial sums.  The split with the least
+    modelled time wins (measured at batch 8: 64² × 320 and 32² × 640 channels at 4 and 8 splits
+    instead of 1.25 and 0.63 rounds)."""
+    v2 = _wino_v2(H, W)
+    if v2:
+        wgs = B * (H // 32) * (W // 32) * (K // 32)
+    else:
+        wgs = -(-(B * (H // 4) * (W // 4)) // 64) * (K // 32)
+    out_bytes = B * K * H * W * 4
+
+    def cost(s):
+        rounds = -(-wgs * s // 256)
+        return rounds * ((C // s // 4) * 2.4e-6 + 5e-6) + (s > 1) * (s + 1) * out_bytes / 5e12
+
+    nsplit = 1
+    if WINO_SPLIT:
+        cands = [s for s in range(1, 33) if C % (4 * s) == 0 and (s == 1 or C // s >= 32)]
+        nsplit = min(cands, key=cost)
+    return v2, nsplit, wgs * nsplit
+
+
 def wino_eligible(B, C, K, H, W, min_workgroups=None):
-    """Whether skp_conv3x3_wino takes a (B, C, H, W) → (B, K, H, W) 3×3 convolution."""
+    """Whether a Winograd kernel takes a (B, C, H, W) → (B, K, H, W) 3×3 convolution."""
     if C % 4 or K % 32 or H % 4 or W % 4:
         return False
-    wgs = -(-(B * (H // 4) * (W // 4)) // 64) * (K // 32)
+    wgs = _wino_plan(B, C, K, H, W)[2]
     return wgs >= (WINO_MIN_WORKGROUPS if min_workgroups is None else min_workgroups)
 
 
-def _wino_launch(x, U, bias, residual, K):
+def _wino_conv(x, weight, flip, bias, residual, K):
     B, C, H, W = x.shape
+    v2, nsplit, _ = _wino_plan(B, C, K, H, W)
+    U = _wino_u(weight, flip, v2)
     y = torch.empty(B, K, H, W, device=x.device, dtype=F32)
-    with _timed("skp_conv3x3_wino", 0):
-        call("skp_conv3x3_wino", ptr(x), ptr(U), ptr(bias) if bias is not None else None,
-             ptr(residual) if residual is not None else None, ptr(y), B, C, K, H, W, stream(x.device))
+    ws = torch.empty(nsplit, B, K, H, W, device=x.device, dtype=F32) if nsplit > 1 else None
+    name = "skp_conv3x3_wino2" if v2 else "skp_conv3x3_wino"
+    with _timed(name, 0):
+        call(name, ptr(x), ptr(U), ptr(bias) if bias is not None else None,
+             ptr(residual) if residual is not None else None, ptr(y), B, C, K, H, W, nsplit,
+             ptr(ws) if ws is not None else None, stream(x.device))
     return y
 
 
@@ -658,8 +697,8 @@ class Conv3x3(torch.autograd.Function):
     def forward(ctx, x, weight, bias, residual):
         x = _c(x)
         K = weight.shape[0]
-        y = _wino_launch(x, _wino_u(weight, False), None if bias is None else _c(bias.detach()),
-                         None if residual is None else _c(residual), K)
+        y = _wino_conv(x, weight, False, None if bias is None else _c(bias.detach()),
+                       None if residual is None else _c(residual), K)
         ctx.weight = weight
         ctx.xshape = x.shape
         ctx.has_res = residual is not None
@@ -674,7 +713,7 @@ class Conv3x3(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dy = _c(dy)
             if wino_eligible(B, K, C, H, W):
-                dx = _wino_launch(dy, _wino_u(w, True), None, None, C)
+                dx = _wino_conv(dy, w, True, None, None, C)
             else:
                 dx = torch.nn.grad.conv2d_input(ctx.xshape, w.detach(), dy, padding=1)
         return dx, None, None, (dy if ctx.has_res else None)

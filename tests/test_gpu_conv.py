@@ -32,7 +32,9 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("B,C,K,H,W", [(2, 64, 64, 32, 32), (2, 4, 32, 20, 20), (1, 32, 96, 12, 28),
-                                       (3, 128, 64, 16, 8), (1, 512, 64, 8, 8), (2, 36, 32, 4, 4)])
+                                       (3, 128, 64, 16, 8), (1, 512, 64, 8, 8), (2, 36, 32, 4, 4),
+                                       (1, 8, 32, 32, 32), (2, 12, 64, 64, 96), (1, 40, 32, 96, 32),
+                                       (3, 4, 32, 32, 64)])
 @pytest.mark.parametrize("bias,res", [(False, False), (True, False), (True, True)])
 def test_conv3x3_forward_vs_fp64(all_shapes, B, C, K, H, W, bias, res):
     ops = all_shapes
@@ -49,7 +51,8 @@ def test_conv3x3_forward_vs_fp64(all_shapes, B, C, K, H, W, bias, res):
     assert _rel(y.cpu(), ref) < 3e-5
 
 
-@pytest.mark.parametrize("B,C,K,H,W", [(2, 64, 32, 16, 16), (1, 32, 64, 12, 20), (2, 320, 320, 8, 8)])
+@pytest.mark.parametrize("B,C,K,H,W", [(2, 64, 32, 16, 16), (1, 32, 64, 12, 20), (2, 320, 320, 8, 8),
+                                       (2, 64, 32, 32, 64), (1, 96, 64, 64, 32)])
 def test_conv3x3_input_gradient_vs_fp64(all_shapes, B, C, K, H, W):
     ops = all_shapes
     g = torch.Generator().manual_seed(K + H)
@@ -82,6 +85,62 @@ def test_conv3x3_vae_shape_and_weight_cache(all_shapes):
     y2 = ops.conv3x3(x, w, b)
     ref2 = F.conv2d(x.double(), w.double(), b.double(), 1, 1)
     assert _rel(y2, ref2) < 3e-5
+
+
+@pytest.mark.parametrize("H,W", [(32, 32), (64, 96)])
+def test_conv3x3_v2_zero_padding_at_every_edge(all_shapes, H, W):
+    """skp_conv3x3_wino2 zero-pads by loading out-of-range rows / 16-B chunks as zeros: a
+    constant input must give, at every border pixel and corner, the partial 3×3 sum of the
+    in-image taps only (exactly, the weights being small integers)."""
+    ops = all_shapes
+    assert ops._wino_v2(H, W)
+    C, K = 4, 32
+    x = torch.ones(2, C, H, W, device=DEV)
+    w = torch.randint(-2, 3, (K, C, 3, 3), generator=torch.Generator().manual_seed(5)).float()
+    y = ops.conv3x3(x, w.to(DEV))
+    ref = F.conv2d(x.cpu().double(), w.double(), None, 1, 1)
+    assert (y.cpu().double() - ref).abs().max().item() < 1e-4
+
+
+def test_conv3x3_v1_v2_agree(all_shapes, monkeypatch):
+    """The two Winograd kernels compute the same convolution (same transform points; only the
+    summation order differs)."""
+    ops = all_shapes
+    g = torch.Generator(device=DEV).manual_seed(9)
+    x = torch.randn(2, 64, 64, 64, device=DEV, generator=g)
+    w = torch.randn(64, 64, 3, 3, device=DEV, generator=g) / 24
+    y2 = ops.conv3x3(x, w)
+    monkeypatch.setattr(ops, "WINO_KERNEL", "v1")
+    y1 = ops.conv3x3(x, w)
+    assert (y1 - y2).abs().max().item() < 1e-5 * y1.abs().max().item()
+
+
+@pytest.mark.parametrize("B,C,K,H,W", [(2, 256, 64, 16, 16), (1, 384, 32, 32, 32), (2, 512, 64, 8, 8)])
+def test_conv3x3_split_k_vs_fp64_and_unsplit(all_shapes, monkeypatch, B, C, K, H, W):
+    """Split-K (input channels over several workgroup sets + one reduction pass with the bias
+    and the residual) equals fp64 and the unsplit kernel; the forward and the input gradient."""
+    ops = all_shapes
+    assert ops._wino_plan(B, C, K, H, W)[1] > 1 and ops._wino_plan(B, K, C, H, W)[1] >= 1
+    g = torch.Generator().manual_seed(C + H)
+    x = torch.randn(B, C, H, W, generator=g)
+    w = torch.randn(K, C, 3, 3, generator=g) / (3 * C ** 0.5)
+    b = torch.randn(K, generator=g)
+    r = torch.randn(B, K, H, W, generator=g)
+    dy = torch.randn(B, K, H, W, generator=g)
+    outs = []
+    for split in (True, False):
+        monkeypatch.setattr(ops, "WINO_SPLIT", split)
+        xd = x.to(DEV).requires_grad_(True)
+        y = ops.conv3x3(xd, w.to(DEV), b.to(DEV), r.to(DEV))
+        (y * dy.to(DEV)).sum().backward()
+        outs.append((y.detach().cpu(), xd.grad.cpu()))
+    x64 = x.double().requires_grad_(True)
+    ref = F.conv2d(x64, w.double(), b.double(), 1, 1) + r.double()
+    (ref * dy.double()).sum().backward()
+    for y, dx in outs:
+        assert _rel(y, ref.detach()) < 3e-5
+        assert _rel(dx, x64.grad) < 3e-5
+    assert (outs[0][0] - outs[1][0]).abs().max().item() < 1e-5 * outs[1][0].abs().max().item()
 
 
 def test_conv3x3_falls_back_to_miopen_for_ineligible_shapes():
