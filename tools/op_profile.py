@@ -28,7 +28,23 @@ if shapes:
         if e.key.startswith("aten::") and t > 0:
             rows.append((t, e.key, e.count, str(e.input_shapes)[:150]))
     rows.sort(reverse=True)
-    for t, k, n, sh in rows[:120]:
+    for t, k, n, sh in rows[:int(os.environ.get("ROWS", "120"))]:
         print(f"{t / 1e3:8.3f} ms {n:5d} {k:36s} {sh}")
+    tot = {}
+    for t, k, n, sh in rows:
+        a = tot.setdefault(k, [0.0, 0])
+        a[0] += t
+        a[1] += n
+    print("--- per aten op (all shapes)")
+    for k, (t, n) in sorted(tot.items(), key=lambda kv: -kv[1][0]):
+        print(f"{t / 1e3:8.3f} ms {n:5d} {k}")
+    ker = {}
+    for e in prof.key_averages():
+        t = getattr(e, "self_device_time_total", 0) or getattr(e, "self_cuda_time_total", 0)
+        if t > 0 and not e.key.startswith("aten::"):
+            ker[e.key] = (t, e.count)
+    print("--- device kernels / non-aten (self time)")
+    for k, (t, n) in sorted(ker.items(), key=lambda kv: -kv[1][0])[:60]:
+        print(f"{t / 1e3:8.3f} ms {n:5d} {k[:150]}")
 else:
     print(prof.key_averages().table(sort_by="self_cuda_time_total", row_limit=45, max_name_column_width=60))
