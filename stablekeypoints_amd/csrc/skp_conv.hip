@@ -632,9 +632,9 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
   for (int b = 0; b < 2; ++b)
 #pragma unroll
     for (int q = 0; q < 18; ++q) acc[b][q] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float acur[18], anext[18];
+  float a0[18], a1[18];   // A operands of the even / odd stages (no copies between stages)
 
-  auto mfmas = [&](const float* us) {
+  auto mfmas = [&](const float* us, const float (&acur)[18]) {
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
       const float* ub = us + uoff + b * 16 * kUP;
@@ -666,13 +666,13 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
     W2_VMCNT(0);
   }
   __syncthreads();
-  w2::half_transform<HH>(R0 + roff, acur);
+  w2::half_transform<HH>(R0 + roff, a0);
 
   // stage s: wait for group s (raw(s+1), U(s)); barrier; issue group s+2 into the slots freed by
   // stage s-1; transform raw(s+1) (slot (s+1)%3) and run the MFMAs on U(s) (slot s%3).  The SIMD
   // partners (waves w, w+4: the two halves) do these in opposite orders, so one's transform
   // (VALU) runs beside the other's MFMAs.
-  auto step = [&](int s, float* Rn, float* Us, float* Ri, float* Ui) {
+  auto step = [&](int s, float* Rn, float* Us, float* Ri, float* Ui, const float (&acur)[18], float (&anext)[18]) {
     if (s + 1 < nst) {
       if (six) W2_VMCNT(6);
       else W2_VMCNT(5);
@@ -684,18 +684,20 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
     const bool tr = s + 1 < nst && !(dbg & 1);
     if (HH == 0) {
       if (tr) w2::half_transform<HH>(Rn + roff, anext);
-      if (!(dbg & 2)) mfmas(Us);
+      if (!(dbg & 2)) mfmas(Us, acur);
     } else {
-      if (!(dbg & 2)) mfmas(Us);
+      if (!(dbg & 2)) mfmas(Us, acur);
       if (tr) w2::half_transform<HH>(Rn + roff, anext);
     }
-#pragma unroll
-    for (int q = 0; q < 18; ++q) acur[q] = anext[q];
   };
-  for (int s = 0; s < ((dbg & 16) ? 0 : nst); s += 3) {
-    step(s, R1, U0, R0, U2);
-    if (s + 1 < nst) step(s + 1, R2, U1, R1, U0);
-    if (s + 2 < nst) step(s + 2, R0, U2, R2, U1);
+  // unrolled by 6: ring slot s%3, A-operand buffer s%2
+  for (int s = 0; s < ((dbg & 16) ? 0 : nst); s += 6) {
+    step(s, R1, U0, R0, U2, a0, a1);
+    if (s + 1 < nst) step(s + 1, R2, U1, R1, U0, a1, a0);
+    if (s + 2 < nst) step(s + 2, R0, U2, R2, U1, a0, a1);
+    if (s + 3 < nst) step(s + 3, R1, U0, R0, U2, a1, a0);
+    if (s + 4 < nst) step(s + 4, R2, U1, R1, U0, a0, a1);
+    if (s + 5 < nst) step(s + 5, R0, U2, R2, U1, a1, a0);
   }
 
   // epilogue: lane holds tiles 4(lane>>4)+r of the wave's 16 (ty = 2wm + (lane>>5),
