@@ -466,18 +466,38 @@ namespace w2 {
 
 constexpr int kNC = 32;                    // output channels per workgroup
 constexpr int kCK = 4;                     // input channels per stage
-constexpr int kRowF = 40;                  // floats per region row (ten 16-B chunks)
-constexpr int kChF = 1408;                 // floats per channel's region (34 rows + pad; ≡ 0 mod 64)
-constexpr int kRawF = kCK * kChF;          // 5632 floats = 22 KB per raw slot
-constexpr int kRawInstr = kRawF / 256;     // 22 1-KB DMA chunks
+// Block geometry: a workgroup's 64 output tiles are TXB×TXB tiles of each of NI images' regions.
+//   TXB 8: a 32×32-pixel block of one image (H, W multiples of 32); region 34 rows × 10 chunks
+//   TXB 4: four whole 16×16 images; region 18 rows × 6 chunks per image
+// The channel stride (floats) makes the patch reads' ds_read_b128 lane groups conflict-free.
+template <int TXB>
+struct Geo;
+template <>
+struct Geo<8> {
+  static constexpr int NI = 1, RR = 34, RC = 10, CHF = 1408;
+};
+template <>
+struct Geo<4> {
+  static constexpr int NI = 4, RR = 18, RC = 6, CHF = 1744;
+};
+template <int TXB>
+struct GeoT : Geo<TXB> {
+  using Geo<TXB>::NI;
+  using Geo<TXB>::RR;
+  using Geo<TXB>::RC;
+  using Geo<TXB>::CHF;
+  static constexpr int RF = 4 * RC;                                   // floats per region row
+  static constexpr int RAWF = (4 * CHF + 255) / 256 * 256;            // raw slot, whole 1-KB chunks
+  static constexpr int RAW_INSTR = RAWF / 256;
+  static_assert(NI * RR * RF <= CHF, "channel region");
+};
 constexpr int kUP = 40;                    // floats per (input, output channel) U row
 constexpr int kUF = kCK * kNC * kUP;       // 5120 floats = 20 KB per U slot
 constexpr int kUInstr = kUF / 256;         // 20
-constexpr int kInstr = kRawInstr + kUInstr;   // 42 per stage, ≤ 6 per wave
 constexpr int kThreads = 512;
 constexpr unsigned kOOB = 0x80000000u;     // buffer offset past any num_records (< 2 GiB): loads 0
-static_assert(kRawF % 256 == 0 && kUF % 256 == 0, "whole 1-KB chunks");
-static_assert(3 * (kRawF + kUF) * 4 <= 160 * 1024, "LDS");
+static_assert(kUF % 256 == 0, "whole 1-KB chunks");
+static_assert(3 * (GeoT<8>::RAWF + kUF) * 4 <= 160 * 1024 && 3 * (GeoT<4>::RAWF + kUF) * 4 <= 160 * 1024, "LDS");
 static_assert(2 * 8 * 1024 <= kUF * 4, "epilogue exchange: two waves' 8 KB per ring buffer");
 
 // Bᵀ (rows i = transform row, columns a = patch row) for the points (0, 1, -1, 1/2, -2, ∞)
@@ -495,14 +515,14 @@ __device__ constexpr float kAt[4][6] = {{1.f, 1.f, 1.f, 1.f, 1.f, 0.f},
 
 // Transform rows 3H..3H+2 of V = Bᵀ d B for this lane's patch (region rows at `raw`, the
 // patch's first row; columns: .w of chunk 0, chunk 1, .x of chunk 2) → a[18] = V[3H+ii][j].
-template <int H>
+template <int H, int RF>
 __device__ __forceinline__ void half_transform(const float* raw, float* a) {
   float t[3][6];
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
-    const float4 c0 = *reinterpret_cast<const float4*>(raw + r * kRowF);
-    const float4 c1 = *reinterpret_cast<const float4*>(raw + r * kRowF + 4);
-    const float4 c2 = *reinterpret_cast<const float4*>(raw + r * kRowF + 8);
+    const float4 c0 = *reinterpret_cast<const float4*>(raw + r * RF);
+    const float4 c1 = *reinterpret_cast<const float4*>(raw + r * RF + 4);
+    const float4 c2 = *reinterpret_cast<const float4*>(raw + r * RF + 8);
     const float d[6] = {c0.w, c1.x, c1.y, c1.z, c1.w, c2.x};
 #pragma unroll
     for (int ii = 0; ii < 3; ++ii) {
@@ -555,16 +575,16 @@ struct W2Smem {
 
 // One wave's whole program for transform half HH (rows 3HH..3HH+2); the kernel branches once
 // on the wave's half so the stage loop is straight-line code for each.
-template <int EPI, int HH>
+template <int EPI, int HH, int TXB>
 __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __restrict__ x, const float* __restrict__ U,
                                            const float* __restrict__ bias, const float* __restrict__ res,
                                            float* __restrict__ y, int C, int K, int H, int W, int img, int x0,
                                            int y0, int kb, int c0, int csplit, int wv, int dbg) {
-  using w2::kChF;
-  using w2::kInstr;
-  using w2::kRawF;
-  using w2::kRawInstr;
-  using w2::kRowF;
+  using Geo = w2::GeoT<TXB>;
+  constexpr int kChF = Geo::CHF, kRowF = Geo::RF, kRawInstr = Geo::RAW_INSTR, NI = Geo::NI, RR = Geo::RR,
+                RC = Geo::RC;
+  constexpr int kInstr = kRawInstr + w2::kUInstr;
+  constexpr int kMaxRaw = (kRawInstr + 7) / 8;
   using w2::kUF;
   using w2::kUP;
   float *R0 = sm.R0, *R1 = sm.R1, *R2 = sm.R2, *U0 = sm.U0, *U1 = sm.U1, *U2 = sm.U2;
@@ -573,11 +593,12 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
   const size_t plane = (size_t)H * W;
   const size_t ximg = (size_t)img * C * plane;
 
-  // this wave's DMA chunks of a stage: chunk g = wv + 8m (raw chunks 0..21, then U chunks 0..19)
-  unsigned voff[3];
+  // this wave's DMA chunks of a stage: chunk g = wv + 8m (the raw slot's chunks, then U's 20);
+  // raw chunk → (channel, image of the block, region row, 16-B column chunk)
+  unsigned voff[kMaxRaw];
   int nraw = 0;
 #pragma unroll
-  for (int m = 0; m < 3; ++m) {
+  for (int m = 0; m < kMaxRaw; ++m) {
     const int gi = wv + 8 * m;
     voff[m] = w2::kOOB;
     if (gi < kRawInstr) {
@@ -585,16 +606,17 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
       const int f = 64 * gi + lane;   // 16-B chunk of the slot
       const int ch = f / (kChF / 4);
       const int e = f - ch * (kChF / 4);
-      const int row = e / 10, c4 = e - row * 10;
+      const int ii = e / (RR * RC), rem = e - ii * (RR * RC);
+      const int row = rem / RC, c4 = rem - row * RC;
       const int yy = y0 - 1 + row, xx = x0 - 4 + 4 * c4;
-      if (row < 34 && yy >= 0 && yy < H && xx >= 0 && xx < W)
-        voff[m] = (unsigned)((ximg + (size_t)ch * plane + (size_t)yy * W + xx) * 4);
+      if (ch < w2::kCK && ii < NI && yy >= 0 && yy < H && xx >= 0 && xx < W)
+        voff[m] = (unsigned)((ximg + ((size_t)ii * C + ch) * plane + (size_t)yy * W + xx) * 4);
     }
   }
   const int nuw = (kInstr - 1 - wv) / 8 + 1 - nraw;   // U chunks of this wave
   const int ufirst = wv + 8 * nraw - kRawInstr;       // its first U chunk
   const bool six = nraw + nuw == 6;                   // DMA instructions per stage group: 6 or 5
-  const size_t xend = (size_t)(img + 1) * C * plane;  // the buffer ends with this image
+  const size_t xend = (size_t)(img + NI) * C * plane; // the buffer ends with the block's last image
   const float* Ub = U + ((size_t)kb * C + c0) * w2::kNC * kUP;
   const int nst = csplit / w2::kCK;
 
@@ -605,7 +627,7 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(x + off), (short)0, ok ? (int)((xend - off) * 4) : 0, 0x00020000);
 #pragma unroll
-    for (int m = 0; m < 3; ++m)
+    for (int m = 0; m < kMaxRaw; ++m)
       if (m < nraw && !(dbg & 4))
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)(rs_lds + 256 * (wv + 8 * m)), 16, voff[m], 0, 0, 0);
   };
@@ -621,9 +643,12 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
       }
   };
 
-  // lane → (tile, stage channel) = its A-operand row; the patch's first row in the region
-  const int tx = lane & 7, ty = 2 * wm + ((lane >> 3) & 1), kc = lane >> 4;
-  const int roff = kc * kChF + 4 * ty * kRowF + 4 * tx;
+  // lane → (tile, stage channel) = its A-operand row; the patch's first row in the region.
+  // TXB 8: wave wm has tile rows 2wm, 2wm+1; TXB 4: wave wm has image wm of the block.
+  const int kc = lane >> 4;
+  const int tx = lane & (TXB - 1);
+  const int ty = TXB == 8 ? 2 * wm + ((lane >> 3) & 1) : (lane >> 2) & 3;
+  const int roff = kc * kChF + (TXB == 8 ? 0 : wm * RR * kRowF) + 4 * ty * kRowF + 4 * tx;
   // B operand: U[kc][16 blk + (lane & 15)][18 HH + q] (rows padded to 40, halves at 0 and 20)
   const int uoff = (kc * w2::kNC + (lane & 15)) * kUP + 20 * HH;
 
@@ -666,7 +691,7 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
     W2_VMCNT(0);
   }
   __syncthreads();
-  w2::half_transform<HH>(R0 + roff, a0);
+  w2::half_transform<HH, kRowF>(R0 + roff, a0);
 
   // stage s: wait for group s (raw(s+1), U(s)); barrier; issue group s+2 into the slots freed by
   // stage s-1; transform raw(s+1) (slot (s+1)%3) and run the MFMAs on U(s) (slot s%3).  The SIMD
@@ -683,11 +708,11 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
     if (s + 2 < nst) issue_group(s + 2, Ri, Ui);
     const bool tr = s + 1 < nst && !(dbg & 1);
     if (HH == 0) {
-      if (tr) w2::half_transform<HH>(Rn + roff, anext);
+      if (tr) w2::half_transform<HH, kRowF>(Rn + roff, anext);
       if (!(dbg & 2)) mfmas(Us, acur);
     } else {
       if (!(dbg & 2)) mfmas(Us, acur);
-      if (tr) w2::half_transform<HH>(Rn + roff, anext);
+      if (tr) w2::half_transform<HH, kRowF>(Rn + roff, anext);
     }
   };
   // unrolled by 6: ring slot s%3, A-operand buffer s%2
@@ -713,9 +738,12 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
     float* b = (c >> 2) == 0 ? R0 : (c >> 2) == 1 ? R1 : (c >> 2) == 2 ? R2 : U0;
     return b + (c & 3) * 1028 + (c >> 2) * 16;
   };
+  // this lane's output tile row within the 1024-float plane: TXB 8: tiles (2wm + lane>>5, 4((lane>>4)&1)
+  // + r) of the 32×32 block; TXB 4: image wm (256 floats), tile row lane>>4, tiles r = 0..3
   float* pl = plane_of(lane & 15);
-  const int oty = 2 * wm + (lane >> 5);
-  const int otx0 = 4 * ((lane >> 4) & 1);
+  const int pbase = TXB == 8 ? (4 * (2 * wm + (lane >> 5))) * 32 + 4 * (4 * ((lane >> 4) & 1))
+                             : wm * 256 + (4 * (lane >> 4)) * 16;
+  constexpr int PW = TXB == 8 ? 32 : 16;   // plane row width
 #pragma unroll
   for (int blk = 0; blk < 2; ++blk) {
     if (HH != blk) {
@@ -727,7 +755,7 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
         w2::half_output<HH>(m, o);
 #pragma unroll
         for (int f = 0; f < 4; ++f)
-          *reinterpret_cast<float4*>(pl + (4 * oty + f) * 32 + 4 * (otx0 + r)) =
+          *reinterpret_cast<float4*>(pl + pbase + f * PW + 4 * r) =
               make_float4(o[4 * f], o[4 * f + 1], o[4 * f + 2], o[4 * f + 3]);
       }
     }
@@ -741,22 +769,29 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
         w2::half_output<HH>(m, o);
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
-          float4* d = reinterpret_cast<float4*>(pl + (4 * oty + f) * 32 + 4 * (otx0 + r));
+          float4* d = reinterpret_cast<float4*>(pl + pbase + f * PW + 4 * r);
           const float4 p = *d;
           *d = make_float4(o[4 * f] + p.x, o[4 * f + 1] + p.y, o[4 * f + 2] + p.z, o[4 * f + 3] + p.w);
         }
       }
     }
     __syncthreads();
-    // 16 channels × 32 rows × 8 chunks of 16 B; a wave instruction = 8 whole rows of one channel
+    // 16 channels × 1024 floats in 16-B chunks; a wave instruction = 1 KB of one channel:
+    // TXB 8: 8 whole rows of the 32×32 block; TXB 4: one whole 16×16 image plane
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int idx = i * w2::kThreads + tid;
-      const int c = idx >> 8, row = (idx >> 3) & 31, c4 = idx & 7;
-      const float4 v0 = *reinterpret_cast<const float4*>(plane_of(c) + row * 32 + 4 * c4);
+      const int c = idx >> 8, q = idx & 255;
+      const float4 v0 = *reinterpret_cast<const float4*>(plane_of(c) + 4 * q);
       const int k = kb * w2::kNC + 16 * blk + c;
       const float bv = (EPI & 1) ? bias[k] : 0.0f;
-      const size_t o = (((size_t)img * K + k) * H + y0 + row) * W + x0 + 4 * c4;
+      size_t o;
+      if (TXB == 8) {
+        const int row = q >> 3, c4 = q & 7;
+        o = (((size_t)img * K + k) * H + y0 + row) * W + x0 + 4 * c4;
+      } else {
+        o = ((size_t)(img + (q >> 6)) * K + k) * 256 + 4 * (q & 63);
+      }
       float4 v = make_float4(v0.x + bv, v0.y + bv, v0.z + bv, v0.w + bv);
       if (EPI & 2) {
         const float4 rv = *reinterpret_cast<const float4*>(res + o);
@@ -771,14 +806,15 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
   }
 }
 
-template <int EPI>
+template <int EPI, int TXB>
 __global__ __launch_bounds__(w2::kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void wino2_kernel(
     const float* __restrict__ x, const float* __restrict__ U, const float* __restrict__ bias,
     const float* __restrict__ res, float* __restrict__ y, int nimg, int C, int K, int H, int W, int bw, int bpi,
     int nblk, int nkb, int kb_major, int csplit, int dbg) {
   // separate LDS objects per ring slot: the compiler tells a DMA into one slot from a ds_read of
   // another and does not wait for outstanding DMAs before every LDS read
-  __shared__ __attribute__((aligned(16))) float R0[w2::kRawF], R1[w2::kRawF], R2[w2::kRawF];
+  __shared__ __attribute__((aligned(16))) float R0[w2::GeoT<TXB>::RAWF], R1[w2::GeoT<TXB>::RAWF],
+      R2[w2::GeoT<TXB>::RAWF];
   __shared__ __attribute__((aligned(16))) float U0[w2::kUF], U1[w2::kUF], U2[w2::kUF];
   // workgroup → (input-channel split, 32×32-pixel block, channel block); consecutive logical ids
   // share one XCD.  A split sums its csplit input channels into slab sp of y (the workspace).
@@ -796,15 +832,22 @@ __global__ __launch_bounds__(w2::kThreads) __attribute__((amdgpu_waves_per_eu(2,
     tb = L / nkb;
     kb = L - tb * nkb;
   }
-  const int img = tb / bpi;
-  const int br = tb - img * bpi;
-  const int by = br / bw;
-  const int x0 = 32 * (br - by * bw), y0 = 32 * by;
+  // TXB 8: block = 32×32 pixels of one image; TXB 4: images 4tb..4tb+3 whole
+  int img, x0 = 0, y0 = 0;
+  if (TXB == 8) {
+    img = tb / bpi;
+    const int br = tb - img * bpi;
+    const int by = br / bw;
+    x0 = 32 * (br - by * bw);
+    y0 = 32 * by;
+  } else {
+    img = 4 * tb;
+  }
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const W2Smem sm{R0, R1, R2, U0, U1, U2};
   const int c0 = sp * csplit;
-  if (wv < 4) wino2_body<EPI, 0>(sm, x, U, bias, res, y, C, K, H, W, img, x0, y0, kb, c0, csplit, wv, dbg);
-  else wino2_body<EPI, 1>(sm, x, U, bias, res, y, C, K, H, W, img, x0, y0, kb, c0, csplit, wv, dbg);
+  if (wv < 4) wino2_body<EPI, 0, TXB>(sm, x, U, bias, res, y, C, K, H, W, img, x0, y0, kb, c0, csplit, wv, dbg);
+  else wino2_body<EPI, 1, TXB>(sm, x, U, bias, res, y, C, K, H, W, img, x0, y0, kb, c0, csplit, wv, dbg);
 }
 
 // U2[kb][c][k%32][40]: positions 0..17 at 0..17, 18..35 at 20..37, the rest zero
@@ -854,7 +897,9 @@ extern "C" int skp_conv3x3_wino2(const float* x, const float* U, const float* bi
   SKP_CHECK_ARG(B > 0 && C > 0 && K > 0 && H > 0 && W > 0, "non-positive shape");
   SKP_CHECK_ARG(C % w2::kCK == 0, "input channels must be a multiple of 4");
   SKP_CHECK_ARG(K % w2::kNC == 0, "output channels must be a multiple of 32");
-  SKP_CHECK_ARG(H % 32 == 0 && W % 32 == 0, "H and W must be multiples of 32");
+  const bool g16 = H == 16 && W == 16;
+  SKP_CHECK_ARG((H % 32 == 0 && W % 32 == 0) || (g16 && B % 4 == 0),
+                "H and W must be multiples of 32, or 16×16 with B a multiple of 4");
   SKP_CHECK_ARG(nsplit >= 1 && C % (w2::kCK * nsplit) == 0, "nsplit must divide C into multiples of 4");
   SKP_CHECK_ARG(nsplit == 1 || ws, "split-K needs a workspace of nsplit·B·K·H·W floats");
   SKP_CHECK_ARG(aligned16(x) && aligned16(U) && aligned16(y) && (!residual || aligned16(residual)) &&
@@ -862,7 +907,7 @@ extern "C" int skp_conv3x3_wino2(const float* x, const float* U, const float* bi
                 "tensors must be 16-byte aligned");
   SKP_CHECK_ARG((long long)B * C * H * W * 4 < 0x7fffffffLL, "input larger than 2 GiB (32-bit buffer offsets)");
   const int bw = W / 32, bpi = (H / 32) * bw;
-  const long long nblk = (long long)B * bpi;
+  const long long nblk = g16 ? B / 4 : (long long)B * bpi;
   const int nkb = K / w2::kNC;
   SKP_CHECK_ARG(nblk * nkb * nsplit <= 0x7fffffffLL, "grid too large");
   // dev switches (SKP_WINO2_DEBUG): 1 skip transforms, 2 skip MFMAs, 4 skip input DMA, 8 skip weight DMA,
@@ -876,9 +921,13 @@ extern "C" int skp_conv3x3_wino2(const float* x, const float* U, const float* bi
   float* out = nsplit > 1 ? ws : y;
   hipStream_t st = as_stream(stream);
   const dim3 grid((unsigned)(nblk * nkb * nsplit));
-#define SKP_WG2(E)                                                                                              \
-  hipLaunchKernelGGL((wino2_kernel<E>), grid, dim3(w2::kThreads), 0, st, x, U, bias, residual, out, B, C, K, H, W, \
-                     bw, bpi, (int)nblk, nkb, kb_major, C / nsplit, dbg)
+#define SKP_WG2(E)                                                                                            \
+  if (g16)                                                                                                    \
+    hipLaunchKernelGGL((wino2_kernel<E, 4>), grid, dim3(w2::kThreads), 0, st, x, U, bias, residual, out, B, C, K, \
+                       H, W, bw, bpi, (int)nblk, nkb, kb_major, C / nsplit, dbg);                             \
+  else                                                                                                        \
+    hipLaunchKernelGGL((wino2_kernel<E, 8>), grid, dim3(w2::kThreads), 0, st, x, U, bias, residual, out, B, C, K, \
+                       H, W, bw, bpi, (int)nblk, nkb, kb_major, C / nsplit, dbg)
   switch (epi) {
     case 0: SKP_WG2(0); break;
     case 1: SKP_WG2(1); break;

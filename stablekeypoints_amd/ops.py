@@ -612,14 +612,18 @@ _WINO_U = {}   # id(weight) -> (weakref(weight), {(flip, v2): (version, U)})
 # Shapes whose grid stays below this even after splitting go to MIOpen.
 WINO_MIN_WORKGROUPS = 128
 # Which kernel takes an eligible shape: "auto" = skp_conv3x3_wino2 where H and W are multiples
-# of 32 (every VAE-encoder layer, the UNet's 64² and 32² layers), skp_conv3x3_wino elsewhere;
+# of 32 (every VAE-encoder layer, the UNet's 64² and 32² layers) or 16×16 with the batch a
+# multiple of 4 (the UNet's 16² layers), skp_conv3x3_wino elsewhere (8²);
 # "v1" forces the first kernel (A/B runs: SKP_WINO=v1).  SKP_WINO_SPLIT=0 disables split-K.
 WINO_KERNEL = os.environ.get("SKP_WINO", "auto")
 WINO_SPLIT = os.environ.get("SKP_WINO_SPLIT", "1") != "0"
 
 
-def _wino_v2(H, W):
-    return WINO_KERNEL != "v1" and H % 32 == 0 and W % 32 == 0
+def _wino_v2(H, W, B=None):
+    """skp_conv3x3_wino2 takes H, W multiples of 32, and 16×16 images four at a time."""
+    if WINO_KERNEL == "v1":
+        return False
+    return (H % 32 == 0 and W % 32 == 0) or (H == 16 and W == 16 and B is not None and B % 4 == 0)
 
 
 def _wino_u(weight, flip, v2=False):
@@ -648,9 +652,9 @@ def _wino_plan(B, C, K, H, W):
     and adds (S + 1) passes over the output for the partial sums.  The split with the least
     modelled time wins (measured at batch 8: 64² × 320 and 32² × 640 channels at 4 and 8 splits
     instead of 1.25 and 0.63 rounds)."""
-    v2 = _wino_v2(H, W)
+    v2 = _wino_v2(H, W, B)
     if v2:
-        wgs = B * (H // 32) * (W // 32) * (K // 32)
+        wgs = (B // 4 if H == 16 else B * (H // 32) * (W // 32)) * (K // 32)
     else:
         wgs = -(-(B * (H // 4) * (W // 4)) // 64) * (K // 32)
     out_bytes = B * K * H * W * 4

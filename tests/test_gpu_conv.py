@@ -34,7 +34,7 @@ def _rel(a, b):
 @pytest.mark.parametrize("B,C,K,H,W", [(2, 64, 64, 32, 32), (2, 4, 32, 20, 20), (1, 32, 96, 12, 28),
                                        (3, 128, 64, 16, 8), (1, 512, 64, 8, 8), (2, 36, 32, 4, 4),
                                        (1, 8, 32, 32, 32), (2, 12, 64, 64, 96), (1, 40, 32, 96, 32),
-                                       (3, 4, 32, 32, 64)])
+                                       (3, 4, 32, 32, 64), (4, 8, 32, 16, 16), (8, 36, 64, 16, 16)])
 @pytest.mark.parametrize("bias,res", [(False, False), (True, False), (True, True)])
 def test_conv3x3_forward_vs_fp64(all_shapes, B, C, K, H, W, bias, res):
     ops = all_shapes
@@ -52,7 +52,7 @@ def test_conv3x3_forward_vs_fp64(all_shapes, B, C, K, H, W, bias, res):
 
 
 @pytest.mark.parametrize("B,C,K,H,W", [(2, 64, 32, 16, 16), (1, 32, 64, 12, 20), (2, 320, 320, 8, 8),
-                                       (2, 64, 32, 32, 64), (1, 96, 64, 64, 32)])
+                                       (2, 64, 32, 32, 64), (1, 96, 64, 64, 32), (4, 64, 96, 16, 16)])
 def test_conv3x3_input_gradient_vs_fp64(all_shapes, B, C, K, H, W):
     ops = all_shapes
     g = torch.Generator().manual_seed(K + H)
@@ -87,27 +87,28 @@ def test_conv3x3_vae_shape_and_weight_cache(all_shapes):
     assert _rel(y2, ref2) < 3e-5
 
 
-@pytest.mark.parametrize("H,W", [(32, 32), (64, 96)])
+@pytest.mark.parametrize("H,W", [(32, 32), (64, 96), (16, 16)])
 def test_conv3x3_v2_zero_padding_at_every_edge(all_shapes, H, W):
     """skp_conv3x3_wino2 zero-pads by loading out-of-range rows / 16-B chunks as zeros: a
     constant input must give, at every border pixel and corner, the partial 3×3 sum of the
     in-image taps only (exactly, the weights being small integers)."""
     ops = all_shapes
-    assert ops._wino_v2(H, W)
+    assert ops._wino_v2(H, W, 4)
     C, K = 4, 32
-    x = torch.ones(2, C, H, W, device=DEV)
+    x = torch.ones(4, C, H, W, device=DEV)
     w = torch.randint(-2, 3, (K, C, 3, 3), generator=torch.Generator().manual_seed(5)).float()
     y = ops.conv3x3(x, w.to(DEV))
     ref = F.conv2d(x.cpu().double(), w.double(), None, 1, 1)
     assert (y.cpu().double() - ref).abs().max().item() < 1e-4
 
 
-def test_conv3x3_v1_v2_agree(all_shapes, monkeypatch):
+@pytest.mark.parametrize("B,HW", [(2, 64), (8, 16)])
+def test_conv3x3_v1_v2_agree(all_shapes, monkeypatch, B, HW):
     """The two Winograd kernels compute the same convolution (same transform points; only the
-    summation order differs)."""
+    summation order differs); both block geometries of the region kernel."""
     ops = all_shapes
     g = torch.Generator(device=DEV).manual_seed(9)
-    x = torch.randn(2, 64, 64, 64, device=DEV, generator=g)
+    x = torch.randn(B, 64, HW, HW, device=DEV, generator=g)
     w = torch.randn(64, 64, 3, 3, device=DEV, generator=g) / 24
     y2 = ops.conv3x3(x, w)
     monkeypatch.setattr(ops, "WINO_KERNEL", "v1")
@@ -115,7 +116,8 @@ def test_conv3x3_v1_v2_agree(all_shapes, monkeypatch):
     assert (y1 - y2).abs().max().item() < 1e-5 * y1.abs().max().item()
 
 
-@pytest.mark.parametrize("B,C,K,H,W", [(2, 256, 64, 16, 16), (1, 384, 32, 32, 32), (2, 512, 64, 8, 8)])
+@pytest.mark.parametrize("B,C,K,H,W", [(2, 256, 64, 16, 16), (1, 384, 32, 32, 32), (2, 512, 64, 8, 8),
+                                       (4, 512, 64, 16, 16)])
 def test_conv3x3_split_k_vs_fp64_and_unsplit(all_shapes, monkeypatch, B, C, K, H, W):
     """Split-K (input channels over several workgroup sets + one reduction pass with the bias
     and the residual) equals fp64 and the unsplit kernel; the forward and the input gradient."""
