@@ -680,16 +680,26 @@ def wino_eligible(B, C, K, H, W, min_workgroups=None):
 
 def _wino_conv(x, weight, flip, bias, residual, K):
     B, C, H, W = x.shape
+    y = torch.empty(B, K, H, W, device=x.device, dtype=F32)
+    # the kernels address x through 32-bit buffer offsets: batches above 2 GiB run in chunks
+    per_img = C * H * W * 4
+    bmax = max(1, (2 ** 31 - 1) // per_img)
+    for b0 in range(0, B, bmax):
+        b1 = min(B, b0 + bmax)
+        _wino_launch(x[b0:b1], weight, flip, bias, None if residual is None else residual[b0:b1], y[b0:b1], K)
+    return y
+
+
+def _wino_launch(x, weight, flip, bias, residual, y, K):
+    B, C, H, W = x.shape
     v2, nsplit, _ = _wino_plan(B, C, K, H, W)
     U = _wino_u(weight, flip, v2)
-    y = torch.empty(B, K, H, W, device=x.device, dtype=F32)
     ws = torch.empty(nsplit, B, K, H, W, device=x.device, dtype=F32) if nsplit > 1 else None
     name = "skp_conv3x3_wino2" if v2 else "skp_conv3x3_wino"
     with _timed(name, 0):
         call(name, ptr(x), ptr(U), ptr(bias) if bias is not None else None,
              ptr(residual) if residual is not None else None, ptr(y), B, C, K, H, W, nsplit,
              ptr(ws) if ws is not None else None, stream(x.device))
-    return y
 
 
 class Conv3x3(torch.autograd.Function):

@@ -145,6 +145,22 @@ def test_conv3x3_split_k_vs_fp64_and_unsplit(all_shapes, monkeypatch, B, C, K, H
     assert (outs[0][0] - outs[1][0]).abs().max().item() < 1e-5 * outs[1][0].abs().max().item()
 
 
+def test_conv3x3_batch_above_2gib_runs_in_chunks(all_shapes):
+    """An input above 2 GiB (the kernels' 32-bit buffer offsets; the SDXL VAE at 1024², batch 8)
+    runs as batch chunks: same result as MIOpen (fp32) over the whole batch, bias and residual
+    included."""
+    ops = all_shapes
+    g = torch.Generator(device=DEV).manual_seed(4)
+    x = torch.randn(5, 128, 1024, 1024, device=DEV, generator=g)
+    assert x.numel() * 4 > 2 ** 31
+    w = torch.randn(128, 128, 3, 3, device=DEV, generator=g) / 34
+    b = torch.randn(128, device=DEV, generator=g)
+    r = torch.randn_like(x)
+    y = ops.conv3x3(x, w, b, r)
+    ref = F.conv2d(x, w, b, 1, 1) + r
+    assert (y - ref).abs().max().item() < 3e-5 * ref.abs().max().item()
+
+
 def test_conv3x3_falls_back_to_miopen_for_ineligible_shapes():
     """conv_in (3 channels) / conv_out (8 channels) shapes go to MIOpen, not the Winograd kernel."""
     from stablekeypoints_amd import ops
