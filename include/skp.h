@@ -162,6 +162,10 @@ int skp_groupnorm_bwd(const float* x, const float* dy, const float* gamma, const
  * softmax(q kᵀ·scale) v): per row of P (rows × cols), dS = alpha·P ⊙ (dP − Σ P ⊙ dP),
  * written over dP (alpha = the logits' scale, baddbmm's backward folded in).  cols ≤ 16384. */
 int skp_softmax_bwd(const float* P, float* dP, long long rows, int cols, float alpha, void* stream);
+/* Its forward, in place: S (rows × cols, cols % 4 == 0, ≤ 16384) ← softmax over each row
+ * (torch order: max-subtracted exp, divided by the row sum).  One read and one write of S
+ * (the (B·H, 4096, 4096) scores of the 64²-token layers are 4.3 GB at batch 8).           */
+int skp_softmax_fwd(float* S, long long rows, int cols, void* stream);
 /* out = a + (h + bias[c]) over (B, C, HW): diffusers ResnetBlock2D `x + conv2(...)` with the
  * convolution's bias folded into the residual add (same rounding order).         */
 int skp_residual_bias_add(const float* a, const float* h, const float* bias, int B, int C, long long HW,

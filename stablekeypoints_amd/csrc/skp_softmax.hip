@@ -75,7 +75,81 @@ __global__ __launch_bounds__(TPR) void softmax_bwd_kernel(const float* __restric
   }
 }
 
+// In-place row softmax, torch order: m = max, e = exp(x − m), y = e / Σe.  A row stays in
+// registers between the two reductions: one read and one write of S.
+template <int TPR, int EPT>   // float4 lanes: EPT % 4 == 0
+__global__ __launch_bounds__(TPR) void softmax_fwd_kernel(float* __restrict__ S, long long rows, int cols) {
+  __shared__ float sred[2][TPR / WAVE];
+  const long long row = blockIdx.x;
+  if (row >= rows) return;
+  float* p = S + row * cols;
+  float v[EPT];
+  float m = -INFINITY;
+#pragma unroll
+  for (int q = 0; q < EPT / 4; ++q) {
+    const int e = 4 * (threadIdx.x + q * TPR);
+    float4 a = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    if (e < cols) a = *reinterpret_cast<const float4*>(p + e);
+    v[4 * q] = a.x;
+    v[4 * q + 1] = a.y;
+    v[4 * q + 2] = a.z;
+    v[4 * q + 3] = a.w;
+    m = fmaxf(m, fmaxf(fmaxf(a.x, a.y), fmaxf(a.z, a.w)));
+  }
+  const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
+  m = wave_max(m);
+  if (TPR > WAVE) {
+    if (lane == 0) sred[0][wid] = m;
+    __syncthreads();
+    float t = sred[0][0];
+#pragma unroll
+    for (int w = 1; w < TPR / WAVE; ++w) t = fmaxf(t, sred[0][w]);
+    m = t;
+  }
+  float sum = 0.0f;
+#pragma unroll
+  for (int q = 0; q < EPT; ++q) {
+    v[q] = expf(v[q] - m);
+    sum += v[q];
+  }
+  sum = wave_sum(sum);
+  if (TPR > WAVE) {
+    if (lane == 0) sred[1][wid] = sum;
+    __syncthreads();
+    float t = 0.0f;
+#pragma unroll
+    for (int w = 0; w < TPR / WAVE; ++w) t += sred[1][w];
+    sum = t;
+  }
+#pragma unroll
+  for (int q = 0; q < EPT / 4; ++q) {
+    const int e = 4 * (threadIdx.x + q * TPR);
+    if (e < cols)
+      *reinterpret_cast<float4*>(p + e) =
+          make_float4(v[4 * q] / sum, v[4 * q + 1] / sum, v[4 * q + 2] / sum, v[4 * q + 3] / sum);
+  }
+}
+
 }  // namespace
+
+extern "C" int skp_softmax_fwd(float* S, long long rows, int cols, void* stream) {
+  SKP_CHECK_ARG(S, "null pointer");
+  SKP_CHECK_ARG(rows > 0 && cols > 0, "non-positive shape");
+  SKP_CHECK_ARG(cols <= 16384 && cols % 4 == 0, "cols must be a multiple of 4, at most 16384");
+  SKP_CHECK_ARG(rows <= 0x7fffffffLL, "too many rows");
+  SKP_CHECK_ARG((reinterpret_cast<uintptr_t>(S) & 15) == 0, "S must be 16-byte aligned");
+  hipStream_t st = as_stream(stream);
+  const dim3 grid((unsigned)rows);
+#define SKP_SF(T, E) hipLaunchKernelGGL((softmax_fwd_kernel<T, E>), grid, dim3(T), 0, st, S, rows, cols)
+  if (cols <= 64 * 4) SKP_SF(64, 4);
+  else if (cols <= 64 * 8) SKP_SF(64, 8);
+  else if (cols <= 64 * 16) SKP_SF(64, 16);
+  else if (cols <= 256 * 16) SKP_SF(256, 16);
+  else SKP_SF(1024, 16);
+#undef SKP_SF
+  SKP_LAUNCH_CHECK();
+  return SKP_OK;
+}
 
 extern "C" int skp_softmax_bwd(const float* P, float* dP, long long rows, int cols, float alpha, void* stream) {
   SKP_CHECK_ARG(P && dP, "null pointer");

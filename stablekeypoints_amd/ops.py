@@ -513,17 +513,32 @@ def residual_bias_add(a, h, bias):
     return ResidualBiasAdd.apply(a, h, bias)
 
 
+def softmax_(s):
+    """In-place row softmax of a contiguous fp32 (…, cols) tensor (skp_softmax_fwd), torch
+    semantics; falls back to torch's when cols is not a multiple of 4."""
+    if s.dtype != F32 or not s.is_contiguous() or s.shape[-1] % 4 or s.shape[-1] > 16384 or \
+            s.data_ptr() % 16:
+        return s.copy_(s.softmax(dim=-1))
+    call("skp_softmax_fwd", ptr(s), s.numel() // s.shape[-1], s.shape[-1], stream(s.device))
+    return s
+
+
+def attention_probs(q, k, scale):
+    """softmax(q kᵀ·scale) for (B·H, S, D) q and (B·H, S', D) k: hipBLASLt baddbmm, then the
+    softmax in place (skp_softmax_fwd)."""
+    sim = torch.baddbmm(torch.empty(q.shape[0], q.shape[1], k.shape[1], dtype=q.dtype, device=q.device),
+                        q, k.transpose(1, 2), beta=0, alpha=scale)
+    return softmax_(sim)
+
+
 class MathAttention(torch.autograd.Function):
     """softmax(q kᵀ·scale) v over (B·H, S, D) (diffusers-0.8.0 math path): hipBLASLt GEMMs and
-    torch softmax forward; the backward's softmax gradient (with baddbmm's scale folded in) is
-    one skp_softmax_bwd pass written over dP."""
+    the in-place skp_softmax_fwd; the backward's softmax gradient (with baddbmm's scale folded
+    in) is one skp_softmax_bwd pass written over dP."""
 
     @staticmethod
     def forward(ctx, q, k, v, scale):
-        sim = torch.baddbmm(torch.empty(q.shape[0], q.shape[1], k.shape[1], dtype=q.dtype, device=q.device),
-                            q, k.transpose(1, 2), beta=0, alpha=scale)
-        p = sim.softmax(dim=-1)
-        del sim
+        p = attention_probs(q, k, scale)
         ctx.save_for_backward(q, k, v, p)
         ctx.scale = scale
         return torch.bmm(p, v)

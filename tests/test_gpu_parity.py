@@ -486,6 +486,20 @@ def test_math_attention_fused_softmax_backward_vs_fp64(BH, S, L, D):
         assert (a.double() - b).abs().max().item() < 1e-4 * max(1.0, b.abs().max().item())
 
 
+@pytest.mark.parametrize("rows,cols", [(64, 4096), (33, 500), (128, 1024), (7, 77), (5, 16384), (9, 12)])
+def test_softmax_fwd_in_place_vs_torch(rows, cols):
+    """skp_softmax_fwd (in place) vs torch.softmax: within 2 ulp-level (1e-6 relative to the row
+    max) including large-magnitude and -inf entries; non-multiple-of-4 rows fall back to torch."""
+    from stablekeypoints_amd import ops
+    g = torch.Generator().manual_seed(rows * cols)
+    s = (torch.randn(rows, cols, generator=g) * 8).to(DEV)
+    s[0, : cols // 2] = float("-inf")
+    ref = torch.softmax(s.double(), -1)
+    out = ops.softmax_(s.clone())
+    assert (out.double() - ref).abs().max().item() < 1e-6
+    assert torch.allclose(out.sum(-1).double(), torch.ones(rows, dtype=torch.float64, device=DEV), atol=1e-5)
+
+
 def test_residual_bias_add_bitexact():
     """a + (h + bias[c]) equals torch's two adds bit for bit; gradients pass through."""
     from stablekeypoints_amd import ops
