@@ -166,6 +166,11 @@ int skp_softmax_bwd(const float* P, float* dP, long long rows, int cols, float a
  * (torch order: max-subtracted exp, divided by the row sum).  One read and one write of S
  * (the (B·H, 4096, 4096) scores of the 64²-token layers are 4.3 GB at batch 8).           */
 int skp_softmax_fwd(float* S, long long rows, int cols, void* stream);
+/* diffusers GEGLU (the UNet FeedForward's proj → chunk(2) → x·gelu(gate), exact-erf GELU):
+ * h (rows, 2I) → out (rows, I), and its backward dh (rows, 2I) from dout (rows, I).
+ * I % 4 == 0, 16-byte aligned.                                                 */
+int skp_geglu_fwd(const float* h, long long rows, int I, float* out, void* stream);
+int skp_geglu_bwd(const float* h, const float* dout, long long rows, int I, float* dh, void* stream);
 /* out = a + (h + bias[c]) over (B, C, HW): diffusers ResnetBlock2D `x + conv2(...)` with the
  * convolution's bias folded into the residual add (same rounding order).         */
 int skp_residual_bias_add(const float* a, const float* h, const float* bias, int B, int C, long long HW,

@@ -558,6 +558,39 @@ class MathAttention(torch.autograd.Function):
         return dq, dk, dv, None
 
 
+class Geglu(torch.autograd.Function):
+    """x · gelu(gate) over the two halves of a (…, 2I) projection (diffusers GEGLU): one fused
+    pass each way (skp_geglu_fwd / skp_geglu_bwd)."""
+
+    @staticmethod
+    def forward(ctx, h):
+        h = _c(h)
+        I = h.shape[-1] // 2
+        out = torch.empty(*h.shape[:-1], I, device=h.device, dtype=F32)
+        call("skp_geglu_fwd", ptr(h), h.numel() // h.shape[-1], I, ptr(out), stream(h.device))
+        ctx.save_for_backward(h)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (h,) = ctx.saved_tensors
+        dout = _c(dout)
+        dh = torch.empty_like(h)
+        call("skp_geglu_bwd", ptr(h), ptr(dout), h.numel() // h.shape[-1], h.shape[-1] // 2, ptr(dh),
+             stream(h.device))
+        return dh
+
+
+def geglu(h):
+    """diffusers GEGLU's `x, gate = h.chunk(2, -1); x * gelu(gate)` (exact GELU) on the HIP
+    device; torch's form where the half width is not a multiple of 4."""
+    _lib.require_device(h)
+    if h.dtype != F32 or h.shape[-1] % 8:
+        x, gate = h.chunk(2, dim=-1)
+        return x * torch.nn.functional.gelu(gate)
+    return Geglu.apply(h)
+
+
 def math_attention(q, k, v, scale):
     """softmax(q kᵀ·scale) v with the fused softmax backward (HIP device)."""
     _lib.require_device(q, k, v)

@@ -121,7 +121,11 @@ class GEGLU(nn.Module):
         self.proj = nn.Linear(dim_in, dim_out * 2)
 
     def forward(self, x):
-        x, gate = self.proj(x).chunk(2, dim=-1)
+        h = self.proj(x)
+        if USE_FUSED_GROUPNORM and h.is_cuda:
+            from .. import ops   # one fused pass each way (skp_geglu_fwd / _bwd)
+            return ops.geglu(h)
+        x, gate = h.chunk(2, dim=-1)
         return x * F.gelu(gate)
 
 

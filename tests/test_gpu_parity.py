@@ -500,6 +500,24 @@ def test_softmax_fwd_in_place_vs_torch(rows, cols):
     assert torch.allclose(out.sum(-1).double(), torch.ones(rows, dtype=torch.float64, device=DEV), atol=1e-5)
 
 
+@pytest.mark.parametrize("shape", [(2, 64, 2560), (3, 7, 16), (1, 5, 24)])
+def test_geglu_fused_vs_torch(shape):
+    """ops.geglu (skp_geglu_fwd/_bwd) vs torch's chunk · gelu and its autograd, fp32."""
+    import torch.nn.functional as F
+    from stablekeypoints_amd import ops
+    g = torch.Generator().manual_seed(shape[-1])
+    h = (torch.randn(*shape, generator=g) * 3).to(DEV).requires_grad_(True)
+    out = ops.geglu(h)
+    dout = torch.randn(*out.shape, generator=g).to(DEV)
+    (out * dout).sum().backward()
+    hr = h.detach().clone().requires_grad_(True)
+    x, gate = hr.chunk(2, dim=-1)
+    ref = x * F.gelu(gate)
+    (ref * dout).sum().backward()
+    assert (out - ref).abs().max().item() < 1e-5 * max(1.0, ref.abs().max().item())
+    assert (h.grad - hr.grad).abs().max().item() < 1e-5 * max(1.0, hr.grad.abs().max().item())
+
+
 def test_residual_bias_add_bitexact():
     """a + (h + bias[c]) equals torch's two adds bit for bit; gradients pass through."""
     from stablekeypoints_amd import ops
