@@ -715,6 +715,9 @@ def _wino_plan(B, C, K, H, W):
     if WINO_SPLIT:
         cands = [s for s in range(1, 33) if C % (4 * s) == 0 and (s == 1 or C // s >= 32)]
         nsplit = min(cands, key=cost)
+        force = int(os.environ.get("SKP_WINO_NSPLIT", "0"))   # dev: measure a given split
+        if force and C % (4 * force) == 0:
+            nsplit = force
     return v2, nsplit, wgs * nsplit
 
 
