@@ -797,6 +797,13 @@ def conv3x3(x, weight, bias=None, residual=None):
         raise ValueError(f"conv3x3: weight {tuple(weight.shape)} does not fit input {tuple(x.shape)}")
     if residual is not None and tuple(residual.shape) != (B, K, H, W):
         raise ValueError(f"conv3x3: residual {tuple(residual.shape)} is not ({B}, {K}, {H}, {W})")
+    if C % 4 and C < 16 and x.dtype == F32 and wino_eligible(B, C + 4 - C % 4, K, H, W):
+        # input layers (RGB: 3 channels): one zero channel makes them Winograd-eligible; the
+        # padded weight's transform is rebuilt per call (K·4 entries)
+        pad = 4 - C % 4
+        xp = torch.nn.functional.pad(x, (0, 0, 0, 0, 0, pad))
+        wp = torch.nn.functional.pad(weight.detach(), (0, 0, 0, 0, 0, pad))
+        return Conv3x3.apply(xp, wp, bias, residual)
     if x.dtype != F32 or not wino_eligible(B, C, K, H, W):
         y = torch.nn.functional.conv2d(x, weight, bias, 1, 1)
         return y if residual is None else residual + y

@@ -18,7 +18,7 @@ With 1024² images the latents are 128²; the up_blocks[0] cross-attention runs 
 import torch
 import torch.nn as nn
 
-from .unet import (CrossAttnDownBlock2D, CrossAttnUpBlock2D, DownBlock2D, TimestepEmbedding, UNetMidBlock2DCrossAttn,
+from .unet import (_conv_in, CrossAttnDownBlock2D, CrossAttnUpBlock2D, DownBlock2D, TimestepEmbedding, UNetMidBlock2DCrossAttn,
                    UpBlock2D, gn_act, timestep_embedding)
 
 SDXL_CONFIG = dict(block_out_channels=(320, 640, 1280), transformer_depth=(0, 2, 10), head_dim=64,
@@ -89,7 +89,7 @@ class SDXLUNet(nn.Module):
         timesteps = timestep.reshape(-1).to(sample.device).expand(sample.shape[0])
         emb = self.time_embedding(timestep_embedding(timesteps, self.time_proj_dim).to(sample.dtype))
         emb = emb + self.added_embedding(sample, added_cond_kwargs)
-        h = self.conv_in(sample)
+        h = _conv_in(self.conv_in, sample)
         res = (h,)
         for blk in self.down_blocks:
             h, r = blk(h, emb, encoder_hidden_states)

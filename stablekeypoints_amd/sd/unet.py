@@ -43,6 +43,15 @@ def _fused(x, *modules):
     return USE_FUSED_GROUPNORM and x.is_cuda and not any(p.requires_grad for m in modules for p in m.parameters())
 
 
+def _conv_in(conv, x):
+    """An input 3×3 convolution (latent or RGB channels): Winograd (channels zero-padded to a
+    multiple of 4) when the fused kernels apply."""
+    if _fused(x, conv):
+        from .. import ops
+        return ops.conv3x3(x, conv.weight, conv.bias)
+    return conv(x)
+
+
 def gn_act(norm, x, act, shift=None):
     """act(norm(x + shift)) for an nn.GroupNorm ``norm`` (``shift``: None or a per-(sample,
     channel) offset (B or 1, C)): on the HIP device the fused libskp kernel (frozen affine
@@ -426,7 +435,7 @@ class UNet2DConditionModel(nn.Module):
             timestep = torch.tensor([timestep], dtype=torch.long, device=sample.device)
         timesteps = timestep.reshape(-1).to(sample.device).expand(sample.shape[0])
         emb = self.time_embedding(timestep_embedding(timesteps, self.time_proj_dim).to(sample.dtype))
-        h = self.conv_in(sample)
+        h = _conv_in(self.conv_in, sample)
         res = (h,)
         for blk in self.down_blocks:
             h, r = blk(h, emb, encoder_hidden_states)

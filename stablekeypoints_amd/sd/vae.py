@@ -9,7 +9,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .unet import ResnetBlock2D, Downsample2D, gn_act, attention_core
+from .unet import ResnetBlock2D, Downsample2D, gn_act, attention_core, _fused, _conv_in
 
 
 class AttentionBlock(nn.Module):
@@ -79,7 +79,7 @@ class Encoder(nn.Module):
         self.conv_out = nn.Conv2d(block_out_channels[-1], 2 * latent_channels, 3, padding=1)
 
     def forward(self, x):
-        x = self.conv_in(x)
+        x = _conv_in(self.conv_in, x)
         for blk in self.down_blocks:
             x = blk(x)
         x = self.mid_block(x)

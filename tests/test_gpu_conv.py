@@ -162,12 +162,32 @@ def test_conv3x3_batch_above_2gib_runs_in_chunks(all_shapes):
 
 
 def test_conv3x3_falls_back_to_miopen_for_ineligible_shapes():
-    """conv_in (3 channels) / conv_out (8 channels) shapes go to MIOpen, not the Winograd kernel."""
+    """conv_out (8 output channels) goes to MIOpen, not the Winograd kernel."""
     from stablekeypoints_amd import ops
-    x = torch.randn(1, 3, 16, 16, device=DEV)
-    w = torch.randn(32, 3, 3, 3, device=DEV)
-    assert not ops.wino_eligible(1, 3, 32, 16, 16, min_workgroups=1)
-    assert torch.allclose(ops.conv3x3(x, w), F.conv2d(x, w, None, 1, 1), atol=1e-5)
+    x = torch.randn(1, 32, 16, 16, device=DEV)
+    w = torch.randn(8, 32, 3, 3, device=DEV)
+    assert not ops.wino_eligible(1, 32, 8, 16, 16, min_workgroups=1)
+    assert torch.allclose(ops.conv3x3(x, w), F.conv2d(x, w, None, 1, 1), atol=1e-4)
+
+
+@pytest.mark.parametrize("C", [3, 1, 6])
+def test_conv3x3_input_layer_channels_zero_padded(all_shapes, C):
+    """conv_in (RGB: 3 channels; latents: 4): channels padded with zeros to a multiple of 4 run on
+    the Winograd kernel, forward and input gradient vs fp64, bias included."""
+    ops = all_shapes
+    g = torch.Generator().manual_seed(C)
+    x = torch.randn(4, C, 32, 32, generator=g)
+    w = torch.randn(64, C, 3, 3, generator=g) / 3
+    b = torch.randn(64, generator=g)
+    dy = torch.randn(4, 64, 32, 32, generator=g)
+    xd = x.to(DEV).requires_grad_(True)
+    y = ops.conv3x3(xd, w.to(DEV), b.to(DEV))
+    (y * dy.to(DEV)).sum().backward()
+    x64 = x.double().requires_grad_(True)
+    ref = F.conv2d(x64, w.double(), b.double(), 1, 1)
+    (ref * dy.double()).sum().backward()
+    assert _rel(y.detach().cpu(), ref.detach()) < 3e-5
+    assert _rel(xd.grad.cpu(), x64.grad) < 3e-5
 
 
 def test_sd_models_winograd_vs_miopen(monkeypatch):
