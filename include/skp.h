@@ -38,16 +38,19 @@ int skp_version(void);
  * ptp_utils.py:508-538 (bicubic(x) -> to_q -> q kᵀ·scale -> softmax).  With
  * z_low = the layer's normal-path logits q kᵀ·scale at s×s (ptp_utils.py:493),
  * attn[b,p,n] = softmax_n(bicubic_{s->R}(z_low[b,:,n])[p]).
- *   z_low (BH, s*s, N) -> attn (BH, R*R, N).                                     */
-int skp_capture_fwd(const float* z_low, int BH, int s, int N, int R, float* attn, void* stream);
+ *   z_low (BH, s*s, N) -> attn (BH, R*R, N).  `stats` (may be NULL): (BH, R*R, 2) floats
+ *   receive each pixel's softmax row max and 1/Σexp, which the backward can reuse.     */
+int skp_capture_fwd(const float* z_low, int BH, int s, int N, int R, float* attn, float* stats, void* stream);
 
 /* Backward of skp_capture_fwd: dz_low = bicubicᵀ( a ⊙ (g − Σ_n a g) ), g = gscale·dattn.
  * Row b of g starts at dattn + (b / group)·sb and is read with strides (sp, sn), so a
  * broadcast gradient needs no materialisation: the layer/head mean of collect_maps gives
  * group = BH, sb = 0; a per-image map gradient (B, N, R²) gives group = heads,
- * sb = N·R², sp = 1, sn = R².  `workspace` holds BH*R*s*N floats (row-adjoint partials). */
+ * sb = N·R², sp = 1, sn = R².  `workspace` holds BH*R*s*N floats (row-adjoint partials).
+ * `stats`: the forward's per-pixel (max, 1/Σ) or NULL (recomputed by two row reductions). */
 int skp_capture_bwd(const float* z_low, int BH, int s, int N, int R, const float* dattn, int group, long long sb,
-                    long long sp, long long sn, float gscale, float* dz_low, float* workspace, void* stream);
+                    long long sp, long long sn, float gscale, const float* stats, float* dz_low, float* workspace,
+                    void* stream);
 
 /* ---------------------------------------------------------------- A3 aggregate
  * optimize.collect_maps (optimize.py:27-79), token-major output:

@@ -16,8 +16,9 @@ _c_int, _c_float, _c_ll, _p = ctypes.c_int, ctypes.c_float, ctypes.c_longlong, c
 
 # name -> argtypes (restype int unless noted)
 _SIGS = {
-    "skp_capture_fwd": [_p, _c_int, _c_int, _c_int, _c_int, _p, _p],
-    "skp_capture_bwd": [_p, _c_int, _c_int, _c_int, _c_int, _p, _c_int, _c_ll, _c_ll, _c_ll, _c_float, _p, _p, _p],
+    "skp_capture_fwd": [_p, _c_int, _c_int, _c_int, _c_int, _p, _p, _p],
+    "skp_capture_bwd": [_p, _c_int, _c_int, _c_int, _c_int, _p, _c_int, _c_ll, _c_ll, _c_ll, _c_float, _p, _p, _p,
+                        _p],
     "skp_aggregate": [ctypes.POINTER(_p), _c_int, _c_int, _c_int, _c_int, _p, _c_int, _p, _p],
     "skp_resize_bilinear": [_p, _c_int, _c_int, _c_int, _p, _p],
     "skp_resize_bilinear_bwd": [_p, _c_int, _c_int, _c_int, _p, _p],

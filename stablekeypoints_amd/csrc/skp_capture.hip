@@ -29,7 +29,8 @@ constexpr int kWaves = kThreads / WAVE;
 // of attn leaves as 1 KiB float4 wave stores.  NQ = quads per lane (N <= 256*NQ).
 template <int NQ, bool VEC, bool NTS = false>
 __global__ __launch_bounds__(kThreads) void capture_fwd_kernel(const float* __restrict__ z, int BH, int s, int N,
-                                                               int R, float* __restrict__ attn) {
+                                                               int R, float* __restrict__ attn,
+                                                               float2* __restrict__ stats) {
   extern __shared__ __attribute__((aligned(16))) float V[];
   constexpr int Np = NQ * 4 * WAVE;
   // block -> (b, y) with b fastest: consecutive blocks (one per XCD under round-robin
@@ -110,6 +111,7 @@ __global__ __launch_bounds__(kThreads) void capture_fwd_kernel(const float* __re
     }
     ssum = wave_sum(ssum);
     const float inv = 1.0f / ssum;
+    if (stats && lane == 0) stats[((size_t)b * R + y) * R + x] = make_float2(m, inv);   // row max, 1/Σ
     float* o = orow + (size_t)x * N;
 #pragma unroll
     for (int c = 0; c < NQ; ++c) {
@@ -194,15 +196,17 @@ __global__ __launch_bounds__(kBwdThreads) void capture_bwd_rows_kernel(const flo
                                                                        const float* __restrict__ g, int group,
                                                                        long long sb, long long sp, long long sn,
                                                                        float gscale, int share,
+                                                                       const float2* __restrict__ stats,
                                                                        float* __restrict__ ws) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int Np = NT * kBwdThreads;
-  constexpr int Gp = Np + 1;        // padded G row: the transposed chunk stores hit distinct banks
-  constexpr int NCH = Np / WAVE;
+  constexpr int Gp = Np + 4;        // G rows 16-B aligned (float4 token quads) and bank-skewed
+  constexpr int Npq = Np / 4;
+  constexpr int NQB = Npq / WAVE;   // token quads per lane in the per-pixel pass
   float* V = lds;                                   // s × Np   vertical bicubic pass of z_low for row y
   float* TW = V + s * Np;                           // R × 4    tap weights (16-B aligned: Np % 4 == 0)
   int* TL = reinterpret_cast<int*>(TW + R * 4);     // R        first tap column before clamping
-  float* G = reinterpret_cast<float*>(TL + R);      // CH × Gp  g, then dZ, of the current pixel chunk
+  float* G = TW + R * 4 + ((R + 3) & ~3);           // CH × Gp  g, then dZ, of the current pixel chunk
   // block -> (b, y).  When `share` consecutive heads read the same gradient rows (the heads of
   // one image: group > 1, or a broadcast g), the heads of one (image, y) go to the same XCD back
   // to back (workgroups are dispatched round-robin over the 8 XCDs), so that XCD's L2 fetches
@@ -321,45 +325,72 @@ __global__ __launch_bounds__(kBwdThreads) void capture_bwd_rows_kernel(const flo
       }
     }
     __syncthreads();
+    // one wave per pixel, lanes own token quads (ds_read_b128 of V and G): recompute the
+    // softmax row a (with the forward's row max and 1/Σ when `stats` is given, else by two
+    // wave reductions), then dZ = a ⊙ (g − Σ a g) over g in place
+    const float4* V4 = reinterpret_cast<const float4*>(V);
     for (int xx = wid; xx < nx; xx += kBwdWaves) {
       const int x = x0 + xx;
       const int lo = TL[x];
       const int i0 = max(lo, 0), i1 = min(max(lo + 1, 0), s - 1);
       const int i2 = min(lo + 2, s - 1), i3 = min(lo + 3, s - 1);
       const float4 w = *reinterpret_cast<const float4*>(TW + 4 * x);
-      float a[NCH];
-      float m = -INFINITY;
+      float4 a[NQB];
 #pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        const int n = c * WAVE + lane;
-        float v = w.x * V[i0 * Np + n];
-        v += w.y * V[i1 * Np + n];
-        v += w.z * V[i2 * Np + n];
-        v += w.w * V[i3 * Np + n];
-        a[c] = n < N ? v : -INFINITY;
-        m = fmaxf(m, a[c]);
+      for (int c = 0; c < NQB; ++c) {
+        const int q = c * WAVE + lane;
+        const float4 a0 = V4[i0 * Npq + q], a1 = V4[i1 * Npq + q];
+        const float4 a2 = V4[i2 * Npq + q], a3 = V4[i3 * Npq + q];
+        a[c].x = w.x * a0.x + w.y * a1.x + w.z * a2.x + w.w * a3.x;
+        a[c].y = w.x * a0.y + w.y * a1.y + w.z * a2.y + w.w * a3.y;
+        a[c].z = w.x * a0.z + w.y * a1.z + w.z * a2.z + w.w * a3.z;
+        a[c].w = w.x * a0.w + w.y * a1.w + w.z * a2.w + w.w * a3.w;
       }
-      m = wave_max(m);
+      float m, inv;
+      if (stats) {
+        const float2 st = stats[((size_t)b * R + y) * R + x];
+        m = st.x;
+        inv = st.y;
+      } else {
+        m = -INFINITY;
+#pragma unroll
+        for (int c = 0; c < NQB; ++c) {
+          const int n = 4 * (c * WAVE + lane);
+          if (n < N) m = fmaxf(m, a[c].x);
+          if (n + 1 < N) m = fmaxf(m, a[c].y);
+          if (n + 2 < N) m = fmaxf(m, a[c].z);
+          if (n + 3 < N) m = fmaxf(m, a[c].w);
+        }
+        m = wave_max(m);
+      }
       float ssum = 0.0f;
 #pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        a[c] = __expf(a[c] - m);
-        ssum += a[c];
+      for (int c = 0; c < NQB; ++c) {
+        const int n = 4 * (c * WAVE + lane);
+        a[c].x = n < N ? __expf(a[c].x - m) : 0.0f;
+        a[c].y = n + 1 < N ? __expf(a[c].y - m) : 0.0f;
+        a[c].z = n + 2 < N ? __expf(a[c].z - m) : 0.0f;
+        a[c].w = n + 3 < N ? __expf(a[c].w - m) : 0.0f;
+        ssum += (a[c].x + a[c].y) + (a[c].z + a[c].w);
       }
-      ssum = wave_sum(ssum);
-      const float inv = 1.0f / ssum;
-      float* Gx = G + xx * Gp;
+      if (!stats) inv = 1.0f / wave_sum(ssum);
+      float4* Gx = reinterpret_cast<float4*>(G + xx * Gp);
       float dot = 0.0f;
 #pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        a[c] *= inv;
-        dot += a[c] * Gx[c * WAVE + lane];
+      for (int c = 0; c < NQB; ++c) {
+        a[c].x *= inv;
+        a[c].y *= inv;
+        a[c].z *= inv;
+        a[c].w *= inv;
+        const float4 g = Gx[c * WAVE + lane];
+        dot += a[c].x * g.x + a[c].y * g.y + a[c].z * g.z + a[c].w * g.w;
       }
       dot = wave_sum(dot);
 #pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        const int n = c * WAVE + lane;
-        Gx[n] = a[c] * (Gx[n] - dot);
+      for (int c = 0; c < NQB; ++c) {
+        const int q = c * WAVE + lane;
+        const float4 g = Gx[q];
+        Gx[q] = make_float4(a[c].x * (g.x - dot), a[c].y * (g.y - dot), a[c].z * (g.z - dot), a[c].w * (g.w - dot));
       }
     }
     __syncthreads();
@@ -596,7 +627,7 @@ __global__ void bilinear_bwd_kernel(const float* __restrict__ gout, int C, int R
 }
 
 template <int NQ>
-void launch_fwd(const float* z, int BH, int s, int N, int R, float* attn, hipStream_t st) {
+void launch_fwd(const float* z, int BH, int s, int N, int R, float* attn, float2* stats, hipStream_t st) {
   const size_t lds = (size_t)s * NQ * 4 * WAVE * sizeof(float);
   const bool vec = (N % 4 == 0) && ((reinterpret_cast<uintptr_t>(z) & 15) == 0) &&
                    ((reinterpret_cast<uintptr_t>(attn) & 15) == 0);
@@ -605,28 +636,28 @@ void launch_fwd(const float* z, int BH, int s, int N, int R, float* attn, hipStr
   const bool nts = lds > 48 * 1024;
   if (vec && nts)
     hipLaunchKernelGGL((capture_fwd_kernel<NQ, true, true>), dim3(BH * R), dim3(kThreads), lds, st, z, BH, s, N, R,
-                       attn);
+                       attn, stats);
   else if (vec)
-    hipLaunchKernelGGL((capture_fwd_kernel<NQ, true>), dim3(BH * R), dim3(kThreads), lds, st, z, BH, s, N, R, attn);
+    hipLaunchKernelGGL((capture_fwd_kernel<NQ, true>), dim3(BH * R), dim3(kThreads), lds, st, z, BH, s, N, R, attn, stats);
   else
-    hipLaunchKernelGGL((capture_fwd_kernel<NQ, false>), dim3(BH * R), dim3(kThreads), lds, st, z, BH, s, N, R, attn);
+    hipLaunchKernelGGL((capture_fwd_kernel<NQ, false>), dim3(BH * R), dim3(kThreads), lds, st, z, BH, s, N, R, attn, stats);
 }
 
 size_t bwd_rows_lds(int s, int N, int R, int CH);
 
 template <int NT>
 void launch_bwd_rows(const float* z, int BH, int s, int N, int R, int CH, const float* g, int group, long long sb,
-                     long long sp, long long sn, float gscale, float* ws, hipStream_t st) {
+                     long long sp, long long sn, float gscale, const float2* stats, float* ws, hipStream_t st) {
   const size_t lds = bwd_rows_lds(s, N, R, CH);
   const int share = sb == 0 ? BH : group;   // heads reading the same gradient rows
   hipLaunchKernelGGL((capture_bwd_rows_kernel<NT>), dim3(BH * R), dim3(kBwdThreads), lds, st, z, BH, s, N, R, CH, g,
-                     group, sb, sp, sn, gscale, share, ws);
+                     group, sb, sp, sn, gscale, share, stats, ws);
 }
 
 int nt_for(int N);
 size_t bwd_rows_lds(int s, int N, int R, int CH) {
   const size_t np = (size_t)nt_for(N) * kBwdThreads;
-  return (s * np + (size_t)CH * (np + 1) + (size_t)R * 5) * sizeof(float);
+  return (s * np + (size_t)CH * (np + 4) + (size_t)R * 4 + (((size_t)R + 3) & ~(size_t)3)) * sizeof(float);
 }
 
 int nq_for(int N) {  // float4 quads per lane for the forward
@@ -657,7 +688,8 @@ int pick_chunk(int s, int N, int R) {
 
 }  // namespace
 
-extern "C" int skp_capture_fwd(const float* z_low, int BH, int s, int N, int R, float* attn, void* stream) {
+extern "C" int skp_capture_fwd(const float* z_low, int BH, int s, int N, int R, float* attn, float* stats,
+                               void* stream) {
   SKP_CHECK_ARG(z_low && attn, "null pointer");
   SKP_CHECK_ARG(BH > 0 && s > 0 && R > 0 && N > 0, "non-positive shape");
   const int nq = nq_for(N);
@@ -665,17 +697,17 @@ extern "C" int skp_capture_fwd(const float* z_low, int BH, int s, int N, int R, 
   SKP_CHECK_ARG((size_t)s * nq * 4 * WAVE * 4 <= 160 * 1024, "s*N too large for LDS");
   hipStream_t st = as_stream(stream);
   switch (nq) {
-    case 1: launch_fwd<1>(z_low, BH, s, N, R, attn, st); break;
-    case 2: launch_fwd<2>(z_low, BH, s, N, R, attn, st); break;
-    default: launch_fwd<4>(z_low, BH, s, N, R, attn, st); break;
+    case 1: launch_fwd<1>(z_low, BH, s, N, R, attn, reinterpret_cast<float2*>(stats), st); break;
+    case 2: launch_fwd<2>(z_low, BH, s, N, R, attn, reinterpret_cast<float2*>(stats), st); break;
+    default: launch_fwd<4>(z_low, BH, s, N, R, attn, reinterpret_cast<float2*>(stats), st); break;
   }
   SKP_LAUNCH_CHECK();
   return SKP_OK;
 }
 
 extern "C" int skp_capture_bwd(const float* z_low, int BH, int s, int N, int R, const float* dattn, int group,
-                               long long sb, long long sp, long long sn, float gscale, float* dz_low,
-                               float* workspace, void* stream) {
+                               long long sb, long long sp, long long sn, float gscale, const float* stats,
+                               float* dz_low, float* workspace, void* stream) {
   SKP_CHECK_ARG(z_low && dattn && dz_low && workspace, "null pointer");
   SKP_CHECK_ARG(group >= 1, "group must be >= 1");
   SKP_CHECK_ARG(BH > 0 && s > 0 && R > 0 && N > 0, "non-positive shape");
@@ -686,8 +718,9 @@ extern "C" int skp_capture_bwd(const float* z_low, int BH, int s, int N, int R, 
   const int CH = pick_chunk(s, N, R);
   SKP_CHECK_ARG(bwd_rows_lds(s, N, R, CH) <= 160 * 1024, "s*N too large for LDS");
   hipStream_t st = as_stream(stream);
-  if (nt == 1) launch_bwd_rows<1>(z_low, BH, s, N, R, CH, dattn, group, sb, sp, sn, gscale, workspace, st);
-  else launch_bwd_rows<2>(z_low, BH, s, N, R, CH, dattn, group, sb, sp, sn, gscale, workspace, st);
+  const float2* st2 = reinterpret_cast<const float2*>(stats);
+  if (nt == 1) launch_bwd_rows<1>(z_low, BH, s, N, R, CH, dattn, group, sb, sp, sn, gscale, st2, workspace, st);
+  else launch_bwd_rows<2>(z_low, BH, s, N, R, CH, dattn, group, sb, sp, sn, gscale, st2, workspace, st);
   SKP_LAUNCH_CHECK();
   const int chunks = (int)(((long long)s * N + kColThreads - 1) / kColThreads);
   hipLaunchKernelGGL(capture_bwd_cols_kernel, dim3(chunks, BH), dim3(kColThreads), 0, st, workspace, BH, s, N, R,

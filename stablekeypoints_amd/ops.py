@@ -91,7 +91,7 @@ class CaptureAttn(torch.autograd.Function):
         assert S == s * s
         attn = torch.empty(BH, R * R, N, device=z.device, dtype=F32)
         with _timed("skp_capture_fwd", (BH * R * R * N + BH * S * N) * 4):
-            call("skp_capture_fwd", ptr(z), BH, s, N, R, ptr(attn), stream(z.device))
+            call("skp_capture_fwd", ptr(z), BH, s, N, R, ptr(attn), None, stream(z.device))
         ctx.save_for_backward(z)
         ctx.s, ctx.R = s, R
         return attn
@@ -102,9 +102,10 @@ class CaptureAttn(torch.autograd.Function):
         return capture_bwd(z, ctx.s, ctx.R, dattn), None, None
 
 
-def capture_bwd(z, s, R, dattn, gscale=1.0, group=1, strides=None):
+def capture_bwd(z, s, R, dattn, gscale=1.0, group=1, strides=None, stats=None):
     """dz_low for g = gscale·dattn; ``dattn`` (BH, R², N) of any strides, or with ``group``/
-    ``strides`` = (sb, sp, sn) a per-group gradient (row b uses group b // group)."""
+    ``strides`` = (sb, sp, sn) a per-group gradient (row b uses group b // group).  ``stats``:
+    the forward's per-pixel softmax (max, 1/Σ), (BH, R², 2), or None (recomputed)."""
     BH, S, N = z.shape
     if dattn.dtype != F32:
         dattn = dattn.float()
@@ -117,8 +118,8 @@ def capture_bwd(z, s, R, dattn, gscale=1.0, group=1, strides=None):
     ws = torch.empty(BH, R, s, N, device=z.device, dtype=F32)
     dz = torch.empty_like(z)
     with _timed("skp_capture_bwd", (BH * S * N * 2 + BH * R * s * N * 2) * 4):
-        call("skp_capture_bwd", ptr(z), BH, s, N, R, ptr(dattn), int(group), sb, sp, sn, float(gscale), ptr(dz),
-             ptr(ws), stream(z.device))
+        call("skp_capture_bwd", ptr(z), BH, s, N, R, ptr(dattn), int(group), sb, sp, sn, float(gscale),
+             ptr(stats) if stats is not None else None, ptr(dz), ptr(ws), stream(z.device))
     return dz
 
 
@@ -194,9 +195,11 @@ class CaptureMaps(torch.autograd.Function):
         dev = zs[0].device
         RR = R * R
         attn = [torch.empty(BH, RR, N, device=dev, dtype=F32) for _ in range(L)]
-        for z, a, s in zip(zs, attn, sizes):
+        # per-pixel softmax (max, 1/Σ) of every layer, kept for the backward (8 B per pixel-head)
+        stats = [torch.empty(BH, RR, 2, device=dev, dtype=F32) for _ in range(L)]
+        for z, a, st, s in zip(zs, attn, stats, sizes):
             with _timed("skp_capture_fwd", (BH * RR * N + BH * s * s * N) * 4):
-                call("skp_capture_fwd", ptr(z), BH, s, N, R, ptr(a), stream(dev))
+                call("skp_capture_fwd", ptr(z), BH, s, N, R, ptr(a), ptr(st), stream(dev))
         out = torch.empty(B, N, R, R, device=dev, dtype=F32)
         for b in range(B):
             off = b * H * RR * N * 4
@@ -205,19 +208,21 @@ class CaptureMaps(torch.autograd.Function):
                 call("skp_aggregate", ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)), L, H, RR, N, None, N,
                      ptr(out[b]), stream(dev))
         del attn
-        ctx.save_for_backward(*zs)
+        ctx.save_for_backward(*zs, *stats)
         ctx.meta = (B, H, R, N, list(sizes))
         return out
 
     @staticmethod
     def backward(ctx, dmaps):
-        zs = ctx.saved_tensors
+        saved = ctx.saved_tensors
+        L = len(saved) // 2
+        zs, stats = saved[:L], saved[L:]
         B, H, R, N, sizes = ctx.meta
         dmaps = _c(dmaps)                       # (B, N, R, R)
         RR = R * R
         scale = 1.0 / float(len(zs) * H)
-        dzs = [capture_bwd(z, s, R, dmaps, gscale=scale, group=H, strides=(N * RR, 1, RR))
-               for z, s in zip(zs, sizes)]
+        dzs = [capture_bwd(z, s, R, dmaps, gscale=scale, group=H, strides=(N * RR, 1, RR), stats=st)
+               for z, s, st in zip(zs, sizes, stats)]
         return (None, None, None) + tuple(dzs)
 
 

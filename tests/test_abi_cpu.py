@@ -34,9 +34,9 @@ def test_bad_arguments_rejected_without_gpu():
     if not os.path.exists(_lib.LIB_PATH):
         pytest.skip("libskp.so not built")
     L = _lib.lib()
-    rc = L.skp_capture_fwd(None, 8, 16, 500, 128, None, None)
+    rc = L.skp_capture_fwd(None, 8, 16, 500, 128, None, None, None)
     assert rc == -1 and b"null" in L.skp_last_error()
-    rc = L.skp_capture_fwd(ctypes.c_void_p(16), 8, 16, 5000, 128, ctypes.c_void_p(16), None)
+    rc = L.skp_capture_fwd(ctypes.c_void_p(16), 8, 16, 5000, 128, ctypes.c_void_p(16), None, None)
     assert rc == -1 and b"1024" in L.skp_last_error()
     rc = L.skp_fps(ctypes.c_void_p(16), 10, 8, 8, ctypes.c_void_p(16), 1, 4, ctypes.c_void_p(16), None,
                    ctypes.c_void_p(16), None)

@@ -518,6 +518,29 @@ def test_geglu_fused_vs_torch(shape):
     assert (h.grad - hr.grad).abs().max().item() < 1e-5 * max(1.0, hr.grad.abs().max().item())
 
 
+@pytest.mark.parametrize("BH,s,R,N", [(4, 16, 128, 500), (2, 8, 32, 77), (3, 32, 64, 1000)])
+def test_capture_bwd_with_forward_stats_equals_recomputed(BH, s, R, N):
+    """skp_capture_fwd's per-pixel (max, 1/Σ) stats: equal to the attention's own row max /
+    normaliser, and the backward fed with them equals the backward that recomputes them."""
+    from stablekeypoints_amd import ops
+    from stablekeypoints_amd._lib import call, ptr, stream
+    g = torch.Generator().manual_seed(BH * s + N)
+    z = (torch.randn(BH, s * s, N, generator=g) * 2).to(DEV)
+    attn = torch.empty(BH, R * R, N, device=DEV)
+    stats = torch.empty(BH, R * R, 2, device=DEV)
+    call("skp_capture_fwd", ptr(z), BH, s, N, R, ptr(attn), ptr(stats), stream(z.device))
+    ref = ops.capture_attn(z, s, R)
+    assert torch.equal(attn, ref)
+    zu = torch.nn.functional.interpolate(z.view(BH, s, s, N).permute(0, 3, 1, 2), size=(R, R), mode="bicubic",
+                                         align_corners=False).permute(0, 2, 3, 1).reshape(BH, R * R, N)
+    assert (stats[..., 0] - zu.max(-1).values).abs().max().item() < 1e-4
+    assert (stats[..., 1] * torch.exp(zu - stats[..., :1]).sum(-1) - 1).abs().max().item() < 1e-5
+    gr = torch.randn(BH, R * R, N, generator=g).to(DEV)
+    d0 = ops.capture_bwd(z, s, R, gr)
+    d1 = ops.capture_bwd(z, s, R, gr, stats=stats)
+    assert (d1 - d0).abs().max().item() < 1e-5 * max(1.0, d0.abs().max().item())
+
+
 def test_residual_bias_add_bitexact():
     """a + (h + bias[c]) equals torch's two adds bit for bit; gradients pass through."""
     from stablekeypoints_amd import ops

@@ -57,9 +57,16 @@ def main():
             res[name] = timed(lambda: ops.capture_bwd(zs[16], 16, R, gb), args.iters)
         elif name == "bwd32":
             res[name] = timed(lambda: ops.capture_bwd(zs[32], 32, R, gb), args.iters)
-        elif name in ("bwd16b2", "bwd32b2"):
-            sz = 16 if name == "bwd16b2" else 32
-            res[name] = timed(lambda: ops.capture_bwd(zb2[sz], sz, R, gmap, 0.03125, H, bstr), args.iters)
+        elif name in ("bwd16b2", "bwd32b2", "bwd16b2s", "bwd32b2s"):
+            sz = 16 if name.startswith("bwd16") else 32
+            st = None
+            if name.endswith("s"):   # with the forward's per-pixel softmax stats (the bench's path)
+                from stablekeypoints_amd._lib import call, ptr, stream
+                st = torch.empty(2 * H, R * R, 2, device=dev)
+                scratch = torch.empty(2 * H, R * R, N, device=dev)
+                call("skp_capture_fwd", ptr(zb2[sz]), 2 * H, sz, N, R, ptr(scratch), ptr(st), stream(dev))
+                del scratch
+            res[name] = timed(lambda: ops.capture_bwd(zb2[sz], sz, R, gmap, 0.03125, H, bstr, stats=st), args.iters)
         elif name == "sum1g":   # read-bandwidth reference: torch reduction over a fresh 1 GiB tensor
             big = torch.empty(256 * 1024 * 1024, device=dev).normal_()
             res[name] = timed(lambda: big.sum(), args.iters)
