@@ -196,7 +196,8 @@ int skp_conv3x3_wino(const float* x, const float* U, const float* bias, const fl
 /* The same convolution for H % 32 == W % 32 == 0 (workgroup = 32×32 output pixels × 32
  * channels, three stages of input region and weights in flight, transforms straight into the
  * MFMA operands).  skp_wino2_weights writes U as [K/32][C][32][40] (positions 0..17 at 0..17,
- * 18..35 at 20..37, zero pads); flip as above.                                              */
+ * 18..35 at 20..37, zero pads); flip as above.  Also 16×16 images with B % 4 == 0 (four
+ * whole images per workgroup).  */
 int skp_wino2_weights(const float* w, int K, int C, int flip, float* U, void* stream);
 int skp_conv3x3_wino2(const float* x, const float* U, const float* bias, const float* residual, float* y, int B,
                       int C, int K, int H, int W, int nsplit, float* ws, void* stream);
