@@ -169,6 +169,12 @@ int skp_softmax_bwd(const float* P, float* dP, long long rows, int cols, float a
  * (torch order: max-subtracted exp, divided by the row sum).  One read and one write of S
  * (the (B·H, 4096, 4096) scores of the 64²-token layers are 4.3 GB at batch 8).           */
 int skp_softmax_fwd(float* S, long long rows, int cols, void* stream);
+/* Fused score gradient of the math attention's backward: out = alpha·P ⊙ (dO·Vᵀ − D) with
+ * dO·Vᵀ on the f32 matrix cores (never materialised) and D[row] = dO_row·O_row (the forward
+ * output); P (BH, S, L), dO (BH, S, d), V (BH, L, d), D (BH, S).  out may alias P.
+ * S, L multiples of 64; d ∈ {40, 64, 80, 160}.                                         */
+int skp_attn_dscore(const float* P, const float* dO, const float* V, const float* D, float* out, int BH, int S, int L,
+                    int d, float alpha, void* stream);
 /* diffusers GEGLU (the UNet FeedForward's proj → chunk(2) → x·gelu(gate), exact-erf GELU):
  * h (rows, 2I) → out (rows, I), and its backward dh (rows, 2I) from dout (rows, I).
  * I % 4 == 0, 16-byte aligned.                                                 */

@@ -179,3 +179,90 @@ extern "C" int skp_softmax_bwd(const float* P, float* dP, long long rows, int co
   SKP_LAUNCH_CHECK();
   return SKP_OK;
 }
+
+// ------------------------------------------------------------------------------------------------
+// Fused attention score gradient (diffusers math attention backward, the 4096-token layers):
+//   dS = alpha · P ⊙ (dO·Vᵀ − D),   D[row] = Σ_j P_row,j (dO·Vᵀ)_row,j = dO_row · O_row
+// dP = dO·Vᵀ is computed on the fly on the f32 matrix cores (K = the head dim) instead of being
+// written and re-read as a (B·H, S, L) tensor, and D comes from the forward output (the flash-
+// attention identity), so one pass reads P once and writes dS once (over P when out == P).
+// Workgroup = 64 keys × 64 rows of one head, 4 waves.  The dO and V tiles are staged in LDS
+// (16-B global loads, rows padded to d+1 floats: conflict-free operand reads); wave w computes
+// dPᵀ for keys 16w..16w+15 × the four 16-row blocks with four independent accumulators, so each
+// lane ends with 4 consecutive keys of one row: P is read and dS written as float4.
+namespace {
+typedef float f32x4a __attribute__((ext_vector_type(4)));
+
+template <int KS>   // head dim / 4
+__global__ __launch_bounds__(256) void attn_dscore_kernel(const float* P, const float* __restrict__ dO,
+                                                          const float* __restrict__ V, const float* __restrict__ D,
+                                                          float* out, int S, int L, float alpha) {
+  constexpr int d = 4 * KS, dp = d + 1;
+  __shared__ float sO[64 * dp], sV[64 * dp];
+  const int b = blockIdx.z;
+  const int r0 = blockIdx.y * 64, k0 = blockIdx.x * 64;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  {
+    const float4* gO = reinterpret_cast<const float4*>(dO + ((size_t)b * S + r0) * d);
+    const float4* gV = reinterpret_cast<const float4*>(V + ((size_t)b * L + k0) * d);
+    for (int e = t; e < 64 * KS; e += 256) {
+      const int row = e / KS, c = 4 * (e - row * KS);
+      const float4 o = gO[e], v = gV[e];
+      float* po = sO + row * dp + c;
+      float* pv = sV + row * dp + c;
+      po[0] = o.x; po[1] = o.y; po[2] = o.z; po[3] = o.w;
+      pv[0] = v.x; pv[1] = v.y; pv[2] = v.z; pv[3] = v.w;
+    }
+  }
+  __syncthreads();
+  // A = V rows (keys 16w + (lane&15)), B = dO rows (16bj + (lane&15)); k = 4ks + (lane>>4)
+  const float* va = sV + (16 * w + (lane & 15)) * dp + (lane >> 4);
+  const float* ob = sO + (lane & 15) * dp + (lane >> 4);
+  f32x4a acc[4];
+#pragma unroll
+  for (int bj = 0; bj < 4; ++bj) acc[bj] = f32x4a{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const float a = va[4 * ks];
+#pragma unroll
+    for (int bj = 0; bj < 4; ++bj)
+      acc[bj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, ob[16 * bj * dp + 4 * ks], acc[bj], 0, 0, 0);
+  }
+  // lane: keys k0 + 16w + 4(lane>>4) .. +3 of row r0 + 16bj + (lane&15)
+  const int key = k0 + 16 * w + 4 * (lane >> 4);
+#pragma unroll
+  for (int bj = 0; bj < 4; ++bj) {
+    const int row = r0 + 16 * bj + (lane & 15);
+    const float dr = D[(size_t)b * S + row];
+    const size_t o = ((size_t)b * S + row) * L + key;
+    const float4 p = *reinterpret_cast<const float4*>(P + o);
+    *reinterpret_cast<float4*>(out + o) =
+        make_float4(alpha * (p.x * (acc[bj][0] - dr)), alpha * (p.y * (acc[bj][1] - dr)),
+                    alpha * (p.z * (acc[bj][2] - dr)), alpha * (p.w * (acc[bj][3] - dr)));
+  }
+}
+}  // namespace
+
+extern "C" int skp_attn_dscore(const float* P, const float* dO, const float* V, const float* D, float* out, int BH,
+                               int S, int L, int d, float alpha, void* stream) {
+  SKP_CHECK_ARG(P && dO && V && D && out, "null pointer");
+  SKP_CHECK_ARG(BH > 0 && S > 0 && L > 0 && d > 0, "non-positive shape");
+  SKP_CHECK_ARG(S % 64 == 0 && L % 64 == 0, "S and L must be multiples of 64");
+  SKP_CHECK_ARG(((reinterpret_cast<uintptr_t>(P) | reinterpret_cast<uintptr_t>(dO) | reinterpret_cast<uintptr_t>(V) |
+                  reinterpret_cast<uintptr_t>(out)) & 15) == 0,
+                "tensors must be 16-byte aligned");
+  SKP_CHECK_ARG(BH <= 65535 && S / 64 <= 65535, "grid too large");
+  const dim3 grid((unsigned)(L / 64), (unsigned)(S / 64), (unsigned)BH);
+  hipStream_t st = as_stream(stream);
+#define SKP_DS(K) hipLaunchKernelGGL((attn_dscore_kernel<K>), grid, dim3(256), 0, st, P, dO, V, D, out, S, L, alpha)
+  switch (d) {
+    case 40: SKP_DS(10); break;
+    case 64: SKP_DS(16); break;
+    case 80: SKP_DS(20); break;
+    case 160: SKP_DS(40); break;
+    default: SKP_CHECK_ARG(false, "head dim must be 40, 64, 80 or 160");
+  }
+#undef SKP_DS
+  SKP_LAUNCH_CHECK();
+  return SKP_OK;
+}

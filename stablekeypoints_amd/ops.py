@@ -538,26 +538,37 @@ def attention_probs(q, k, scale):
 
 class MathAttention(torch.autograd.Function):
     """softmax(q kᵀ·scale) v over (B·H, S, D) (diffusers-0.8.0 math path): hipBLASLt GEMMs and
-    the in-place skp_softmax_fwd; the backward's softmax gradient (with baddbmm's scale folded
-    in) is one skp_softmax_bwd pass written over dP."""
+    the in-place skp_softmax_fwd.  Backward: dV = Pᵀ dO (hipBLASLt), then the score gradient
+    with baddbmm's scale folded in — one skp_attn_dscore pass over P (dO·Vᵀ on the matrix
+    cores, never materialised; D = rowsum(dO ⊙ O)) where the shapes allow, else dP = dO Vᵀ and
+    one skp_softmax_bwd pass written over it — then dQ = dS K, dK = dSᵀ Q."""
 
     @staticmethod
     def forward(ctx, q, k, v, scale):
         p = attention_probs(q, k, scale)
-        ctx.save_for_backward(q, k, v, p)
+        out = torch.bmm(p, v)
+        ctx.save_for_backward(q, k, v, p, out)
         ctx.scale = scale
-        return torch.bmm(p, v)
+        return out
 
     @staticmethod
     def backward(ctx, dout):
-        q, k, v, p = ctx.saved_tensors
+        q, k, v, p, out = ctx.saved_tensors
         dout = dout.contiguous()
         dv = torch.bmm(p.transpose(1, 2), dout) if ctx.needs_input_grad[2] else None
         dq = dk = None
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
-            ds = torch.bmm(dout, v.transpose(1, 2))                 # dP, overwritten by scale·dS
-            call("skp_softmax_bwd", ptr(p), ptr(ds), p.shape[0] * p.shape[1], p.shape[2], float(ctx.scale),
-                 stream(p.device))
+            BH, S, L = p.shape
+            d = q.shape[2]
+            if S % 64 == 0 and L % 64 == 0 and d in (40, 64, 80, 160) and v.is_contiguous():
+                D = (dout * out).sum(-1)
+                ds = torch.empty_like(p)
+                call("skp_attn_dscore", ptr(p), ptr(dout), ptr(v), ptr(D), ptr(ds), BH, S, L, d,
+                     float(ctx.scale), stream(p.device))
+            else:
+                ds = torch.bmm(dout, v.transpose(1, 2))             # dP, overwritten by scale·dS
+                call("skp_softmax_bwd", ptr(p), ptr(ds), p.shape[0] * p.shape[1], p.shape[2], float(ctx.scale),
+                     stream(p.device))
             dq = torch.bmm(ds, k) if ctx.needs_input_grad[0] else None
             dk = torch.bmm(ds.transpose(1, 2), q) if ctx.needs_input_grad[1] else None
         return dq, dk, dv, None

@@ -466,6 +466,7 @@ def test_groupnorm_act_vs_torch_fp64(B, C, H, W, G, act, shifted):
 
 
 @pytest.mark.parametrize("BH,S,L,D", [(16, 256, 256, 40), (4, 1024, 1024, 80), (8, 256, 500, 160), (3, 64, 77, 40),
+                                      (2, 256, 256, 160), (2, 1024, 1024, 64), (2, 128, 192, 40),
                                       (2, 4096, 4096, 40)])
 def test_math_attention_fused_softmax_backward_vs_fp64(BH, S, L, D):
     """ops.math_attention: forward and (q, k, v) gradients vs torch fp64 autograd."""

@@ -1,0 +1,46 @@
+"""Dev tool: time the math-attention backward's score-gradient paths at the 64²-token shape."""
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+from stablekeypoints_amd import ops
+from stablekeypoints_amd._lib import call, ptr, stream
+
+dev = "cuda:0"
+BH, S, L, d = 64, 4096, 4096, 40
+g = torch.Generator(device=dev).manual_seed(0)
+q = torch.randn(BH, S, d, device=dev, generator=g)
+k = torch.randn(BH, L, d, device=dev, generator=g)
+v = torch.randn(BH, L, d, device=dev, generator=g)
+p = ops.attention_probs(q, k, d ** -0.5)
+out = torch.bmm(p, v)
+dout = torch.randn_like(out)
+
+
+def timed(fn, iters=5):
+    fn(); torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record(); torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters
+
+
+def old():
+    ds = torch.bmm(dout, v.transpose(1, 2))
+    call("skp_softmax_bwd", ptr(p), ptr(ds), BH * S, L, 0.158, stream(dev))
+    return ds
+
+
+ds_new = torch.empty_like(p)
+
+
+def new():
+    D = (dout * out).sum(-1)
+    call("skp_attn_dscore", ptr(p), ptr(dout), ptr(v), ptr(D), ptr(ds_new), BH, S, L, d, 0.158, stream(dev))
+    return ds_new
+
+
+print(f"old (dP GEMM + softmax_bwd): {timed(old):.3f} ms   fused dscore: {timed(new):.3f} ms")
+a, b = old(), new()
+print("max rel diff", ((a - b).abs().max() / a.abs().max()).item())
