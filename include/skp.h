@@ -175,6 +175,11 @@ int skp_softmax_fwd(float* S, long long rows, int cols, void* stream);
  * S, L multiples of 64; d ∈ {40, 64, 80, 160}.                                         */
 int skp_attn_dscore(const float* P, const float* dO, const float* V, const float* D, float* out, int BH, int S, int L,
                     int d, float alpha, void* stream);
+/* Forward-only fused attention O = softmax(scale·Q Kᵀ) V (online softmax; no score tensor) for
+ * layers that need no backward.  Q (BH, S, d), K, V (BH, L, d), O (BH, S, d); S, L multiples
+ * of 64; d ∈ {40, 64, 80}.                                                      */
+int skp_attn_fwd(const float* Q, const float* K, const float* V, float* O, int BH, int S, int L, int d, float scale,
+                 void* stream);
 /* diffusers GEGLU (the UNet FeedForward's proj → chunk(2) → x·gelu(gate), exact-erf GELU):
  * h (rows, 2I) → out (rows, I), and its backward dh (rows, 2I) from dout (rows, I).
  * I % 4 == 0, 16-byte aligned.                                                 */

@@ -266,3 +266,128 @@ extern "C" int skp_attn_dscore(const float* P, const float* dO, const float* V, 
   SKP_LAUNCH_CHECK();
   return SKP_OK;
 }
+
+// ------------------------------------------------------------------------------------------------
+// Forward-only fused attention O = softmax(scale·Q Kᵀ) V for the UNet's self-attention layers
+// that need no backward (the first 64²-token layer: its input does not depend on the token
+// embedding), so no (B·H, S, L) score or probability tensor is written or read.
+// Workgroup = 64 query rows of one head, 4 waves (16 rows each), looping over 64-key blocks:
+//   Sᵀ = K·Qᵀ on the f32 matrix cores (lane: 4 consecutive keys × 1 query row of each 16-key
+//   sub-block), online row max / sum (a row's 64 keys live in 4 lanes: two xor-shuffles), then
+//   Oᵀ += Vᵀ·Pᵀ with the same (permuted) key order as the k dimension — the C layout of Sᵀ is
+//   the B operand as it stands, no transposition.  K / V tiles are staged in LDS (16-B loads).
+namespace {
+
+template <int KS, int DB>   // head dim / 4, 16-wide head-dim blocks (d ≤ 16·DB)
+__global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__ Q, const float* __restrict__ K,
+                                                       const float* __restrict__ V, float* __restrict__ O, int S,
+                                                       int L, float scale) {
+  constexpr int d = 4 * KS, dp = d + 1;
+  __shared__ float sK[64 * dp], sV[64 * 16 * DB];   // sV rows padded to 16·DB with zeros
+  const int b = blockIdx.y;
+  const int r0 = blockIdx.x * 64;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int row = r0 + 16 * w + (lane & 15);        // this lane's query row
+  // B operand of Sᵀ = K·Qᵀ: Qᵀ[k = 4ks + (lane>>4)][j = row] (pre-scaled)
+  float qv[KS];
+  {
+    const float* q = Q + ((size_t)b * S + row) * d + (lane >> 4);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qv[ks] = q[4 * ks] * scale;
+  }
+  f32x4a o[DB];
+#pragma unroll
+  for (int db = 0; db < DB; ++db) o[db] = f32x4a{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.0f;
+  for (int k0 = 0; k0 < L; k0 += 64) {
+    __syncthreads();   // previous block's tiles consumed
+    {
+      const float4* gK = reinterpret_cast<const float4*>(K + ((size_t)b * L + k0) * d);
+      const float4* gV = reinterpret_cast<const float4*>(V + ((size_t)b * L + k0) * d);
+      for (int e = t; e < 64 * KS; e += 256) {
+        const int key = e / KS, c = 4 * (e - key * KS);
+        const float4 kk = gK[e], vv = gV[e];
+        float* pk = sK + key * dp + c;
+        pk[0] = kk.x; pk[1] = kk.y; pk[2] = kk.z; pk[3] = kk.w;
+        *reinterpret_cast<float4*>(sV + key * 16 * DB + c) = vv;
+      }
+      if (16 * DB > d)
+        for (int e = t; e < 64 * (16 * DB - d); e += 256) {
+          const int key = e / (16 * DB - d), c = d + (e - key * (16 * DB - d));
+          sV[key * 16 * DB + c] = 0.0f;
+        }
+    }
+    __syncthreads();
+    // Sᵀ sub-blocks c: lane holds keys 16c + 4(lane>>4) + r, row (lane & 15)
+    f32x4a s4[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      s4[c] = f32x4a{0.f, 0.f, 0.f, 0.f};
+      const float* kr = sK + (16 * c + (lane & 15)) * dp + (lane >> 4);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) s4[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(kr[4 * ks], qv[ks], s4[c], 0, 0, 0);
+    }
+    float bm = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) bm = fmaxf(bm, fmaxf(fmaxf(s4[c][0], s4[c][1]), fmaxf(s4[c][2], s4[c][3])));
+    bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
+    bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+    const float mn = fmaxf(m, bm);
+    const float corr = __expf(m - mn);   // 0 on the first block (m = -inf)
+    float bs = 0.0f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s4[c][r] = __expf(s4[c][r] - mn);
+        bs += s4[c][r];
+      }
+    bs += __shfl_xor(bs, 16, 64);
+    bs += __shfl_xor(bs, 32, 64);
+    l = l * corr + bs;
+    m = mn;
+#pragma unroll
+    for (int db = 0; db < DB; ++db) o[db] *= corr;
+    // Oᵀ[d][row] += Σ_key V[key][d] · P[key][row]; k-step (c, r) covers keys 16c + 4(lane>>4) + r
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float* vr = sV + (16 * c + 4 * (lane >> 4) + r) * 16 * DB + (lane & 15);
+#pragma unroll
+        for (int db = 0; db < DB; ++db)
+          o[db] = __builtin_amdgcn_mfma_f32_16x16x4f32(vr[16 * db], s4[c][r], o[db], 0, 0, 0);
+      }
+  }
+  // lane: Oᵀ[d = 16db + 4(lane>>4) + r][row (lane & 15)] → O[row][d..d+3]
+  const float inv = 1.0f / l;
+  float* orow = O + ((size_t)b * S + row) * d;
+#pragma unroll
+  for (int db = 0; db < DB; ++db) {
+    const int dd = 16 * db + 4 * (lane >> 4);
+    if (dd < d) *reinterpret_cast<float4*>(orow + dd) = make_float4(o[db][0] * inv, o[db][1] * inv, o[db][2] * inv, o[db][3] * inv);
+  }
+}
+
+}  // namespace
+
+extern "C" int skp_attn_fwd(const float* Q, const float* K, const float* V, float* O, int BH, int S, int L, int d,
+                            float scale, void* stream) {
+  SKP_CHECK_ARG(Q && K && V && O, "null pointer");
+  SKP_CHECK_ARG(BH > 0 && S > 0 && L > 0, "non-positive shape");
+  SKP_CHECK_ARG(S % 64 == 0 && L % 64 == 0, "S and L must be multiples of 64");
+  SKP_CHECK_ARG(BH <= 65535, "grid too large");
+  SKP_CHECK_ARG(((reinterpret_cast<uintptr_t>(K) | reinterpret_cast<uintptr_t>(V) | reinterpret_cast<uintptr_t>(O)) &
+                 15) == 0,
+                "tensors must be 16-byte aligned");
+  const dim3 grid((unsigned)(S / 64), (unsigned)BH);
+  hipStream_t st = as_stream(stream);
+  switch (d) {
+    case 40: hipLaunchKernelGGL((attn_fwd_kernel<10, 3>), grid, dim3(256), 0, st, Q, K, V, O, S, L, scale); break;
+    case 64: hipLaunchKernelGGL((attn_fwd_kernel<16, 4>), grid, dim3(256), 0, st, Q, K, V, O, S, L, scale); break;
+    case 80: hipLaunchKernelGGL((attn_fwd_kernel<20, 5>), grid, dim3(256), 0, st, Q, K, V, O, S, L, scale); break;
+    default: SKP_CHECK_ARG(false, "head dim must be 40, 64 or 80");
+  }
+  SKP_LAUNCH_CHECK();
+  return SKP_OK;
+}

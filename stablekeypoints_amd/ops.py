@@ -536,6 +536,19 @@ def attention_probs(q, k, scale):
     return softmax_(sim)
 
 
+def attention_nograd(q, k, v, scale):
+    """softmax(q kᵀ·scale) v when no gradient is needed: the fused online-softmax kernel
+    (skp_attn_fwd, no score tensor) where the shapes allow, else the scores + in-place softmax."""
+    BH, S, d = q.shape
+    L = k.shape[1]
+    if (q.dtype == F32 and S % 64 == 0 and L % 64 == 0 and d in (40, 64, 80) and q.is_contiguous()
+            and k.is_contiguous() and v.is_contiguous()):
+        out = torch.empty_like(q)
+        call("skp_attn_fwd", ptr(q), ptr(k), ptr(v), ptr(out), BH, S, L, d, float(scale), stream(q.device))
+        return out
+    return torch.bmm(attention_probs(q, k, scale), v)
+
+
 class MathAttention(torch.autograd.Function):
     """softmax(q kᵀ·scale) v over (B·H, S, D) (diffusers-0.8.0 math path): hipBLASLt GEMMs and
     the in-place skp_softmax_fwd.  Backward: dV = Pᵀ dO (hipBLASLt), then the score gradient

@@ -113,8 +113,8 @@ def attention_core(q, k, v, scale, mask=None, heads=1):
         from .. import ops   # same forward; one fused pass for the softmax backward
         return ops.math_attention(q, k, v, scale)
     if mask is None and USE_FUSED_GROUPNORM and q.is_cuda:
-        from .. import ops   # no-grad (or grad-free inputs): in-place fused softmax
-        return torch.bmm(ops.attention_probs(q, k, scale), v)
+        from .. import ops   # no gradient needed: fused online-softmax attention / in-place softmax
+        return ops.attention_nograd(q, k, v, scale)
     sim = torch.baddbmm(torch.empty(q.shape[0], q.shape[1], k.shape[1], dtype=q.dtype, device=q.device),
                         q, k.transpose(1, 2), beta=0, alpha=scale)
     if mask is not None:

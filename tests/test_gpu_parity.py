@@ -542,6 +542,22 @@ def test_capture_bwd_with_forward_stats_equals_recomputed(BH, s, R, N):
     assert (d1 - d0).abs().max().item() < 1e-5 * max(1.0, d0.abs().max().item())
 
 
+@pytest.mark.parametrize("BH,S,L,D", [(8, 4096, 4096, 40), (4, 256, 192, 40), (3, 128, 512, 64), (2, 1024, 1024, 80),
+                                      (2, 64, 77, 40)])
+def test_attention_nograd_fused_vs_fp64(BH, S, L, D):
+    """ops.attention_nograd (skp_attn_fwd: online softmax, no score tensor; the scores path where
+    L is not a multiple of 64) vs torch fp64, including large-magnitude logits."""
+    from stablekeypoints_amd import ops
+    g = torch.Generator().manual_seed(S + L + D)
+    q = (torch.randn(BH, S, D, generator=g) * 2).to(DEV)
+    k = (torch.randn(BH, L, D, generator=g) * 2).to(DEV)
+    v = torch.randn(BH, L, D, generator=g).to(DEV)
+    scale = D ** -0.5
+    out = ops.attention_nograd(q, k, v, scale)
+    ref = torch.softmax(q.double() @ k.double().transpose(1, 2) * scale, -1) @ v.double()
+    assert (out.double() - ref).abs().max().item() < 2e-5
+
+
 def test_residual_bias_add_bitexact():
     """a + (h + bias[c]) equals torch's two adds bit for bit; gradients pass through."""
     from stablekeypoints_amd import ops
