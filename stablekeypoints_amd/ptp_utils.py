@@ -20,7 +20,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
-from .sd.unet import CaptureComplete, attention_core
+from .sd.unet import CaptureComplete, attention_core, kv_projection
 
 
 # --------------------------------------------------------------------------- A2 controller / store
@@ -126,8 +126,7 @@ def register_attention_control(model, controller, feature_upsample_res=256):
             q = self.to_q(x)
             is_cross = context is not None
             context = context if is_cross else x
-            k = self.to_k(context)
-            v = self.to_v(context)
+            k, v = kv_projection(self, context)
             q = self.reshape_heads_to_batch_dim(q)
             k = self.reshape_heads_to_batch_dim(k)
             v = self.reshape_heads_to_batch_dim(v)
@@ -231,8 +230,11 @@ def find_pred_noise(ldm, image, context, noise_level=-1, device="cuda"):
     t = ldm.scheduler.timesteps[noise_level]
     noisy_image = ldm.scheduler.add_noise(latent, noise, t)
     try:
-        pred_noise = ldm.unet(noisy_image, t.repeat(noisy_image.shape[0]),
-                              context.repeat(noisy_image.shape[0], 1, 1))["sample"]
+        # the reference repeats the context per image; a stride-0 expansion is the same tensor
+        # to every consumer, and lets the cross-attention project it once (unet.kv_projection)
+        B = noisy_image.shape[0]
+        ctx = context.expand(B, -1, -1) if context.shape[0] == 1 else context.repeat(B, 1, 1)
+        pred_noise = ldm.unet(noisy_image, t.repeat(B), ctx)["sample"]
     except CaptureComplete:
         pred_noise = None
     return noise, pred_noise

@@ -17,6 +17,8 @@ interface (``heads``, ``scale``, ``to_q``/``to_k``/``to_v``/``to_out``,
 """
 import math
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -97,11 +99,26 @@ class CrossAttention(nn.Module):
     def forward(self, x, context=None, mask=None):
         context = x if context is None else context
         q = self.reshape_heads_to_batch_dim(self.to_q(x))
-        k = self.reshape_heads_to_batch_dim(self.to_k(context))
-        v = self.reshape_heads_to_batch_dim(self.to_v(context))
+        k, v = kv_projection(self, context)
+        k = self.reshape_heads_to_batch_dim(k)
+        v = self.reshape_heads_to_batch_dim(v)
         out = attention_core(q, k, v, self.scale, mask, self.heads)
         out = self.reshape_batch_dim_to_heads(out)
         return self.to_out[1](self.to_out[0](out))
+
+
+SHARED_KV = os.environ.get("SKP_SHARED_KV", "1") != "0"   # A/B switch for kv_projection
+
+
+def kv_projection(attn, context):
+    """to_k(context), to_v(context).  A context whose batch is a stride-0 expansion of one
+    sequence (the token embedding shared by every image of a batched pass) is projected once
+    and the result expanded: the same values, 1/B of the GEMM work forward and backward."""
+    if SHARED_KV and context.dim() == 3 and context.shape[0] > 1 and context.stride(0) == 0:
+        one = context[:1]
+        B = context.shape[0]
+        return attn.to_k(one).expand(B, -1, -1), attn.to_v(one).expand(B, -1, -1)
+    return attn.to_k(context), attn.to_v(context)
 
 
 def attention_core(q, k, v, scale, mask=None, heads=1):
