@@ -198,6 +198,11 @@ def cpu_baseline(args):
 
 
 # ------------------------------------------------------------------------------ GPU bench
+def _tuned_gemms_in_use():
+    from stablekeypoints_amd.tuning import _state
+    return bool(_state["loaded"])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -357,7 +362,8 @@ def main():
                "config": {"workload": workload,
                           "global_batch": world * args.accum, "tokens": args.tokens, "image_res": args.res,
                           "feature_upsample_res": args.upsample_res, "micro_batch": mb,
-                          "parallelism": f"dp{world} (RCCL grad all-reduce)"},
+                          "parallelism": f"dp{world} (RCCL grad all-reduce)",
+                          "tuned_gemms": _tuned_gemms_in_use()},
                "roofline": roof, "cpu_baseline": cpu, "kernels": extra,
                "last_loss": float(rec["loss"])}
         print(json.dumps(out), flush=True)

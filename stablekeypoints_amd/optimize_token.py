@@ -43,6 +43,9 @@ def load_ldm(device, type="CompVis/stable-diffusion-v1-4", feature_upsample_res=
         pass  # hub names cannot be fetched offline: random-init SD-1.5 (seeded) instead
     ldm = (build_sdxl if xl else build_sd15)(seed=seed, device=device, weights=weights, config=config)
     dev = torch.device(device)
+    if dev.type == "cuda":
+        from .tuning import use_tuned_gemms
+        use_tuned_gemms()   # measured hipBLASLt / rocBLAS choices for the UNet/VAE GEMM shapes
     if dev.type == "cuda" and dev.index is None:
         dev = torch.device("cuda", torch.cuda.current_device())
     controllers = {dev: ptp_utils.AttentionStore(early_exit=early_exit)}
