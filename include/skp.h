@@ -175,6 +175,13 @@ int skp_softmax_fwd(float* S, long long rows, int cols, void* stream);
  * S, L multiples of 64; d ∈ {40, 64, 80, 160}.                                         */
 int skp_attn_dscore(const float* P, const float* dO, const float* V, const float* D, float* out, int BH, int S, int L,
                     int d, float alpha, void* stream);
+/* Fused attention backward over key blocks: dS = alpha·P⊙(dO·Vᵀ − D) written to dS (as
+ * skp_attn_dscore) and, from the same registers, dV = Pᵀ·dO and dK = dSᵀ·Q (so dK carries
+ * alpha).  P, dS (BH, S, L); dO, Q (BH, S, d); V, dV, dK (BH, L, d); D = rowsum(dO⊙O) (BH, S).
+ * S, L multiples of 64; d ∈ {40, 64, 80}; dO, Q, V, dV, dK 16-byte aligned.  Replaces the
+ * autograd backward of diffusers' CrossAttention baddbmm → softmax → bmm (attention.py).     */
+int skp_attn_bwd_kv(const float* P, const float* dO, const float* Q, const float* V, const float* D, float* dS,
+                    float* dV, float* dK, int BH, int S, int L, int d, float alpha, void* stream);
 /* Forward-only fused attention O = softmax(scale·Q Kᵀ) V (online softmax; no score tensor) for
  * layers that need no backward.  Q (BH, S, d), K, V (BH, L, d), O (BH, S, d); S, L multiples
  * of 64; d ∈ {40, 64, 80}.                                                      */

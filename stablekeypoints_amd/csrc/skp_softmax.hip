@@ -391,3 +391,202 @@ extern "C" int skp_attn_fwd(const float* Q, const float* K, const float* V, floa
   SKP_LAUNCH_CHECK();
   return SKP_OK;
 }
+
+// ------------------------------------------------------------------------------------------------
+// Fused attention backward over one key block: dS (as skp_attn_dscore), and dV = Pᵀ·dO and
+// dK = dSᵀ·Q accumulated in registers across all query rows, so neither P nor dS is read again
+// by a GEMM.  Workgroup = 64 keys of one head, 4 waves, looping over 64-row blocks; wave w owns
+// rows 16w..16w+15 of each block.  dP = dO·Vᵀ lands in the C layout (lane: rows 4(lane>>4)+r,
+// key lane&15), which is the B operand of dVᵀ += dOᵀ·P and dKᵀ += Qᵀ·dS as it stands, with the
+// reduction over rows in the permuted order r = k-step.  The four waves' partial dV / dK are
+// summed through LDS at the end (fixed order).
+namespace {
+
+template <int KS, int DB, int WPE>   // head dim / 4, 16-wide head-dim blocks, waves per SIMD (d = 40: 2 fit)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void attn_bwd_kv_kernel(const float* __restrict__ P, const float* __restrict__ dO,
+                                                          const float* __restrict__ Q, const float* __restrict__ V,
+                                                          const float* __restrict__ D, float* __restrict__ dS,
+                                                          float* __restrict__ dV, float* __restrict__ dK, int S, int L,
+                                                          float alpha) {
+  constexpr int d = 4 * KS, dp = d + 1, dq = 16 * DB + 1;
+  __shared__ float sV[64 * dp];     // this block's keys
+  __shared__ float sO[2][64 * dq], sQ[2][64 * dq];   // row blocks of dO and Q, double-buffered (zero-padded to 16·DB)
+  __shared__ float sD[2][64];
+  const int b = blockIdx.y, k0 = blockIdx.x * 64;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  {
+    const float4* gV = reinterpret_cast<const float4*>(V + ((size_t)b * L + k0) * d);
+    for (int e = t; e < 64 * KS; e += 256) {
+      const int key = e / KS, c = 4 * (e - key * KS);
+      const float4 v = gV[e];
+      float* p = sV + key * dp + c;
+      p[0] = v.x; p[1] = v.y; p[2] = v.z; p[3] = v.w;
+    }
+    for (int e = t; e < 64 * (dq - d); e += 256) {   // zero pad of the dO / Q tiles (stays zero)
+      const int row = e / (dq - d), c = d + (e - row * (dq - d));
+      sO[0][row * dq + c] = 0.0f; sO[1][row * dq + c] = 0.0f;
+      sQ[0][row * dq + c] = 0.0f; sQ[1][row * dq + c] = 0.0f;
+    }
+  }
+  // the next row block's dO / Q / D / P are fetched into registers at the top of each iteration
+  // and dO / Q / D written to the other LDS buffer at its end, so their latency hides under the MFMAs
+  constexpr int NPF = (64 * KS + 255) / 256;
+  float4 fo[NPF], fq[NPF];
+  float fd = 0.0f;
+  const int rl = 16 * w + 4 * (lane >> 4);
+  auto fetch = [&](int r0) {
+    const float4* gO = reinterpret_cast<const float4*>(dO + ((size_t)b * S + r0) * d);
+    const float4* gQ = reinterpret_cast<const float4*>(Q + ((size_t)b * S + r0) * d);
+#pragma unroll
+    for (int j = 0; j < NPF; ++j) {
+      const int e = t + 256 * j;
+      if (e < 64 * KS) { fo[j] = gO[e]; fq[j] = gQ[e]; }
+    }
+    if (t < 64) fd = D[(size_t)b * S + r0 + t];
+  };
+  auto stash = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < NPF; ++j) {
+      const int e = t + 256 * j;
+      if (e < 64 * KS) {
+        const int row = e / KS, c = 4 * (e - row * KS);
+        float* po = sO[buf] + row * dq + c;
+        float* pq = sQ[buf] + row * dq + c;
+        po[0] = fo[j].x; po[1] = fo[j].y; po[2] = fo[j].z; po[3] = fo[j].w;
+        pq[0] = fq[j].x; pq[1] = fq[j].y; pq[2] = fq[j].z; pq[3] = fq[j].w;
+      }
+    }
+    if (t < 64) sD[buf][t] = fd;
+  };
+  // lane's P / dS elements: rows r0 + rl + r, keys k0 + 16bj + (lane&15)
+  const float* Pl = P + ((size_t)b * S + rl) * L + k0 + (lane & 15);
+  float* dSl = dS + ((size_t)b * S + rl) * L + k0 + (lane & 15);
+  f32x4a pc[4];
+#pragma unroll
+  for (int bj = 0; bj < 4; ++bj)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) pc[bj][r] = Pl[(size_t)r * L + 16 * bj];
+  fetch(0);
+  stash(0);
+  f32x4a dv[DB][4], dk[DB][4];
+#pragma unroll
+  for (int db = 0; db < DB; ++db)
+#pragma unroll
+    for (int bj = 0; bj < 4; ++bj) {
+      dv[db][bj] = f32x4a{0.f, 0.f, 0.f, 0.f};
+      dk[db][bj] = f32x4a{0.f, 0.f, 0.f, 0.f};
+    }
+  for (int r0 = 0, buf = 0; r0 < S; r0 += 64, buf ^= 1) {
+    __syncthreads();
+    const bool more = r0 + 64 < S;
+    f32x4a pn[4];
+    if (more) {
+      fetch(r0 + 64);
+      const float* Pn = Pl + (size_t)(r0 + 64) * L;
+#pragma unroll
+      for (int bj = 0; bj < 4; ++bj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pn[bj][r] = Pn[(size_t)r * L + 16 * bj];
+    }
+    const float* tO = sO[buf];
+    const float* tQ = sQ[buf];
+    // dP = dO·Vᵀ: A = dO[row 16w + (lane&15)][k], B = V[key 16bj + (lane&15)][k], k = 4ks + (lane>>4)
+    f32x4a dp4[4];
+    {
+      const float* oa = tO + (16 * w + (lane & 15)) * dq + (lane >> 4);
+      const float* vb = sV + (lane & 15) * dp + (lane >> 4);
+#pragma unroll
+      for (int bj = 0; bj < 4; ++bj) dp4[bj] = f32x4a{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const float a = oa[4 * ks];
+#pragma unroll
+        for (int bj = 0; bj < 4; ++bj)
+          dp4[bj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, vb[16 * bj * dp + 4 * ks], dp4[bj], 0, 0, 0);
+      }
+    }
+    f32x4a s4[4];
+    float* dSr = dSl + (size_t)r0 * L;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float Dr = sD[buf][rl + r];
+#pragma unroll
+      for (int bj = 0; bj < 4; ++bj) {
+        const float sv = alpha * (pc[bj][r] * (dp4[bj][r] - Dr));
+        dSr[(size_t)r * L + 16 * bj] = sv;
+        s4[bj][r] = sv;
+      }
+    }
+    // dVᵀ[d][key] += Σ_row dO[row][d] P[row][key]; dKᵀ += Σ_row Q[row][d] dS[row][key];
+    // k-step r covers rows 16w + 4(lane>>4) + r
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float* orow = tO + (rl + r) * dq + (lane & 15);
+      const float* qrow = tQ + (rl + r) * dq + (lane & 15);
+#pragma unroll
+      for (int db = 0; db < DB; ++db) {
+        const float ao = orow[16 * db], aq = qrow[16 * db];
+#pragma unroll
+        for (int bj = 0; bj < 4; ++bj) {
+          dv[db][bj] = __builtin_amdgcn_mfma_f32_16x16x4f32(ao, pc[bj][r], dv[db][bj], 0, 0, 0);
+          dk[db][bj] = __builtin_amdgcn_mfma_f32_16x16x4f32(aq, s4[bj][r], dk[db][bj], 0, 0, 0);
+        }
+      }
+    }
+    if (more) {
+      stash(buf ^ 1);
+#pragma unroll
+      for (int bj = 0; bj < 4; ++bj) pc[bj] = pn[bj];
+    }
+  }
+  // sum the four waves' partials (LDS, wave order), then lane: dVᵀ[d = 16db + 4(lane>>4) + r'][key
+  // 16bj + (lane&15)] → dV[key][d..d+3]
+  __syncthreads();
+  float* red = sO[0];   // ≥ 64·dq floats; each pass stages one (db, bj) block per wave: 4 × 256 floats
+  for (int m = 0; m < 2; ++m) {
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+      for (int bj = 0; bj < 4; ++bj) {
+        const f32x4a val = m == 0 ? dv[db][bj] : dk[db][bj];
+        *reinterpret_cast<float4*>(red + (w * 64 + lane) * 4) = make_float4(val[0], val[1], val[2], val[3]);
+        __syncthreads();
+        if (w == 0) {
+          float4 acc = *reinterpret_cast<const float4*>(red + lane * 4);
+#pragma unroll
+          for (int ww = 1; ww < 4; ++ww) {
+            const float4 x = *reinterpret_cast<const float4*>(red + (ww * 64 + lane) * 4);
+            acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
+          }
+          const int dd = 16 * db + 4 * (lane >> 4);
+          const int key = k0 + 16 * bj + (lane & 15);
+          if (dd < d) *reinterpret_cast<float4*>((m == 0 ? dV : dK) + ((size_t)b * L + key) * d + dd) = acc;
+        }
+        __syncthreads();
+      }
+  }
+}
+
+}  // namespace
+
+extern "C" int skp_attn_bwd_kv(const float* P, const float* dO, const float* Q, const float* V, const float* D,
+                               float* dS, float* dV, float* dK, int BH, int S, int L, int d, float alpha,
+                               void* stream) {
+  SKP_CHECK_ARG(P && dO && Q && V && D && dS && dV && dK, "null pointer");
+  SKP_CHECK_ARG(BH > 0 && S > 0 && L > 0, "non-positive shape");
+  SKP_CHECK_ARG(S % 64 == 0 && L % 64 == 0, "S and L must be multiples of 64");
+  SKP_CHECK_ARG(BH <= 65535, "grid too large");
+  SKP_CHECK_ARG(((reinterpret_cast<uintptr_t>(dO) | reinterpret_cast<uintptr_t>(Q) | reinterpret_cast<uintptr_t>(V) |
+                  reinterpret_cast<uintptr_t>(dV) | reinterpret_cast<uintptr_t>(dK)) & 15) == 0,
+                "tensors must be 16-byte aligned");
+  const dim3 grid((unsigned)(L / 64), (unsigned)BH);
+  hipStream_t st = as_stream(stream);
+  switch (d) {
+    case 40: hipLaunchKernelGGL((attn_bwd_kv_kernel<10, 3, 2>), grid, dim3(256), 0, st, P, dO, Q, V, D, dS, dV, dK, S, L, alpha); break;
+    case 64: hipLaunchKernelGGL((attn_bwd_kv_kernel<16, 4, 1>), grid, dim3(256), 0, st, P, dO, Q, V, D, dS, dV, dK, S, L, alpha); break;
+    case 80: hipLaunchKernelGGL((attn_bwd_kv_kernel<20, 5, 1>), grid, dim3(256), 0, st, P, dO, Q, V, D, dS, dV, dK, S, L, alpha); break;
+    default: SKP_CHECK_ARG(false, "head dim must be 40, 64 or 80");
+  }
+  SKP_LAUNCH_CHECK();
+  return SKP_OK;
+}

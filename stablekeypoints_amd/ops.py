@@ -549,12 +549,20 @@ def attention_nograd(q, k, v, scale):
     return torch.bmm(attention_probs(q, k, scale), v)
 
 
+# head dims routed to skp_attn_bwd_kv: d = 40 measured faster end to end (2 waves per SIMD fit);
+# d = 64 / 80 run at one wave per SIMD and measured slower than the unfused path.
+# SKP_ATTN_FUSED_KV=0 disables it, =all routes every supported head dim.
+ATTN_FUSED_KV = {"0": (), "all": (40, 64, 80)}.get(os.environ.get("SKP_ATTN_FUSED_KV", ""), (40,))
+
+
 class MathAttention(torch.autograd.Function):
     """softmax(q kᵀ·scale) v over (B·H, S, D) (diffusers-0.8.0 math path): hipBLASLt GEMMs and
     the in-place skp_softmax_fwd.  Backward: dV = Pᵀ dO (hipBLASLt), then the score gradient
     with baddbmm's scale folded in — one skp_attn_dscore pass over P (dO·Vᵀ on the matrix
     cores, never materialised; D = rowsum(dO ⊙ O)) where the shapes allow, else dP = dO Vᵀ and
-    one skp_softmax_bwd pass written over it — then dQ = dS K, dK = dSᵀ Q."""
+    one skp_softmax_bwd pass written over it — then dQ = dS K, dK = dSᵀ Q.  When K needs a
+    gradient and d ∈ ATTN_FUSED_KV, skp_attn_bwd_kv produces dS, dV and dK in one pass over P
+    (dV, dK accumulated on the matrix cores per key block); only dQ = dS K stays a GEMM."""
 
     @staticmethod
     def forward(ctx, q, k, v, scale):
@@ -568,11 +576,19 @@ class MathAttention(torch.autograd.Function):
     def backward(ctx, dout):
         q, k, v, p, out = ctx.saved_tensors
         dout = dout.contiguous()
+        BH, S, L = p.shape
+        d = q.shape[2]
+        if (d in ATTN_FUSED_KV and S % 64 == 0 and L % 64 == 0 and ctx.needs_input_grad[1]
+                and all(t.is_contiguous() and t.data_ptr() % 16 == 0 for t in (q, v, dout))):
+            D = (dout * out).sum(-1)
+            ds, dv, dk = torch.empty_like(p), torch.empty_like(v), torch.empty_like(k)
+            call("skp_attn_bwd_kv", ptr(p), ptr(dout), ptr(q), ptr(v), ptr(D), ptr(ds), ptr(dv), ptr(dk),
+                 BH, S, L, d, float(ctx.scale), stream(p.device))
+            dq = torch.bmm(ds, k) if ctx.needs_input_grad[0] else None
+            return dq, dk, dv if ctx.needs_input_grad[2] else None, None
         dv = torch.bmm(p.transpose(1, 2), dout) if ctx.needs_input_grad[2] else None
         dq = dk = None
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
-            BH, S, L = p.shape
-            d = q.shape[2]
             if S % 64 == 0 and L % 64 == 0 and d in (40, 64, 80, 160) and v.is_contiguous():
                 D = (dout * out).sum(-1)
                 ds = torch.empty_like(p)

@@ -487,6 +487,32 @@ def test_math_attention_fused_softmax_backward_vs_fp64(BH, S, L, D):
         assert (a.double() - b).abs().max().item() < 1e-4 * max(1.0, b.abs().max().item())
 
 
+@pytest.mark.parametrize("BH,S,L,D,q_grad", [(2, 256, 320, 64, True), (3, 128, 128, 80, False), (1, 4096, 4096, 40, True),
+                                             (5, 64, 640, 40, False)])
+def test_attn_bwd_kv_vs_unfused(monkeypatch, BH, S, L, D, q_grad):
+    """skp_attn_bwd_kv (dS, dV, dK in one pass) vs the unfused backward (skp_attn_dscore + GEMMs)
+    and fp64 autograd, with and without a gradient for q."""
+    from stablekeypoints_amd import ops
+    g = torch.Generator().manual_seed(S * 7 + L)
+    base = [torch.randn(BH, n, D, generator=g).to(DEV) for n in (S, L, L)]
+    dout = torch.randn(BH, S, D, generator=g).to(DEV)
+    grads = {}
+    for fused in (True, False):
+        monkeypatch.setattr(ops, "ATTN_FUSED_KV", (40, 64, 80) if fused else ())
+        q, k, v = (t.clone().requires_grad_(rg) for t, rg in zip(base, (q_grad, True, True)))
+        (ops.math_attention(q, k, v, D ** -0.5) * dout).sum().backward()
+        grads[fused] = [t.grad for t in (q, k, v)]
+    qd, kd, vd = (t.double().requires_grad_(True) for t in base)
+    (torch.softmax(qd @ kd.transpose(1, 2) * D ** -0.5, -1) @ vd * dout.double()).sum().backward()
+    for i, ref in enumerate((qd.grad, kd.grad, vd.grad)):
+        if i == 0 and not q_grad:
+            assert grads[True][0] is None
+            continue
+        tol = 1e-4 * max(1.0, ref.abs().max().item())
+        assert (grads[True][i].double() - ref).abs().max().item() < tol
+        assert (grads[True][i] - grads[False][i]).abs().max().item() < tol
+
+
 @pytest.mark.parametrize("rows,cols", [(64, 4096), (33, 500), (128, 1024), (7, 77), (5, 16384), (9, 12)])
 def test_softmax_fwd_in_place_vs_torch(rows, cols):
     """skp_softmax_fwd (in place) vs torch.softmax: within 2 ulp-level (1e-6 relative to the row

@@ -48,3 +48,23 @@ print(f"forward: scores+softmax+PV {timed(f_old):.3f} ms   fused online-softmax 
       f"max diff {(f_old() - f_new()).abs().max().item():.2e}")
 a, b = old(), new()
 print("max rel diff", ((a - b).abs().max() / a.abs().max()).item())
+
+dv_, dk_ = torch.empty_like(v), torch.empty_like(k)
+
+
+def full_unfused():
+    dv = torch.bmm(p.transpose(1, 2), dout)
+    ds = new()
+    return torch.bmm(ds, k), torch.bmm(ds.transpose(1, 2), q), dv
+
+
+def full_fused():
+    D = (dout * out).sum(-1)
+    call("skp_attn_bwd_kv", ptr(p), ptr(dout), ptr(q), ptr(v), ptr(D), ptr(ds_new), ptr(dv_), ptr(dk_),
+         BH, S, L, d, 0.158, stream(dev))
+    return torch.bmm(ds_new, k), dk_, dv_
+
+
+print(f"full backward: unfused {timed(full_unfused):.3f} ms   fused dS/dV/dK {timed(full_fused):.3f} ms")
+a, b = full_unfused(), full_fused()
+print("max rel diff dq/dk/dv", [((x - y).abs().max() / x.abs().max()).item() for x, y in zip(a, b)])
