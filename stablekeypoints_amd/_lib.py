@@ -46,7 +46,8 @@ _SIGS = {
     "skp_softmax_fwd": [_p, _c_ll, _c_int, _p],
     "skp_attn_dscore": [_p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _p],
     "skp_attn_bwd_kv": [_p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _p],
-    "skp_attn_fwd": [_p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _p],
+    "skp_attn_fwd": [_p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _p],
+    "skp_attn_bwd_flash": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _p],
     "skp_geglu_fwd": [_p, _c_ll, _c_int, _p, _p],
     "skp_geglu_bwd": [_p, _p, _c_ll, _c_int, _p, _p],
     "skp_wino_weights": [_p, _c_int, _c_int, _c_int, _p, _p],

@@ -280,8 +280,8 @@ namespace {
 
 template <int KS, int DB>   // head dim / 4, 16-wide head-dim blocks (d ≤ 16·DB)
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__ Q, const float* __restrict__ K,
-                                                       const float* __restrict__ V, float* __restrict__ O, int S,
-                                                       int L, float scale) {
+                                                       const float* __restrict__ V, float* __restrict__ O,
+                                                       float2* __restrict__ ST, int S, int L, float scale) {
   constexpr int d = 4 * KS, dp = d + 1;
   __shared__ float sK[64 * dp], sV[64 * 16 * DB];   // sV rows padded to 16·DB with zeros
   const int b = blockIdx.y;
@@ -311,7 +311,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
         pk[0] = kk.x; pk[1] = kk.y; pk[2] = kk.z; pk[3] = kk.w;
         *reinterpret_cast<float4*>(sV + key * 16 * DB + c) = vv;
       }
-      if (16 * DB > d)
+      if constexpr (16 * DB > d)
         for (int e = t; e < 64 * (16 * DB - d); e += 256) {
           const int key = e / (16 * DB - d), c = d + (e - key * (16 * DB - d));
           sV[key * 16 * DB + c] = 0.0f;
@@ -367,12 +367,14 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
     const int dd = 16 * db + 4 * (lane >> 4);
     if (dd < d) *reinterpret_cast<float4*>(orow + dd) = make_float4(o[db][0] * inv, o[db][1] * inv, o[db][2] * inv, o[db][3] * inv);
   }
+  // row stats for a backward that recomputes P = exp(scale·q·k − m) / l (the 4 lanes of a row agree)
+  if (ST != nullptr && lane < 16) ST[(size_t)b * S + row] = make_float2(m, inv);
 }
 
 }  // namespace
 
-extern "C" int skp_attn_fwd(const float* Q, const float* K, const float* V, float* O, int BH, int S, int L, int d,
-                            float scale, void* stream) {
+extern "C" int skp_attn_fwd(const float* Q, const float* K, const float* V, float* O, float* stats, int BH, int S,
+                            int L, int d, float scale, void* stream) {
   SKP_CHECK_ARG(Q && K && V && O, "null pointer");
   SKP_CHECK_ARG(BH > 0 && S > 0 && L > 0, "non-positive shape");
   SKP_CHECK_ARG(S % 64 == 0 && L % 64 == 0, "S and L must be multiples of 64");
@@ -380,12 +382,14 @@ extern "C" int skp_attn_fwd(const float* Q, const float* K, const float* V, floa
   SKP_CHECK_ARG(((reinterpret_cast<uintptr_t>(K) | reinterpret_cast<uintptr_t>(V) | reinterpret_cast<uintptr_t>(O)) &
                  15) == 0,
                 "tensors must be 16-byte aligned");
+  SKP_CHECK_ARG((reinterpret_cast<uintptr_t>(stats) & 7) == 0, "stats must be 8-byte aligned");
   const dim3 grid((unsigned)(S / 64), (unsigned)BH);
   hipStream_t st = as_stream(stream);
+  float2* ST = reinterpret_cast<float2*>(stats);
   switch (d) {
-    case 40: hipLaunchKernelGGL((attn_fwd_kernel<10, 3>), grid, dim3(256), 0, st, Q, K, V, O, S, L, scale); break;
-    case 64: hipLaunchKernelGGL((attn_fwd_kernel<16, 4>), grid, dim3(256), 0, st, Q, K, V, O, S, L, scale); break;
-    case 80: hipLaunchKernelGGL((attn_fwd_kernel<20, 5>), grid, dim3(256), 0, st, Q, K, V, O, S, L, scale); break;
+    case 40: hipLaunchKernelGGL((attn_fwd_kernel<10, 3>), grid, dim3(256), 0, st, Q, K, V, O, ST, S, L, scale); break;
+    case 64: hipLaunchKernelGGL((attn_fwd_kernel<16, 4>), grid, dim3(256), 0, st, Q, K, V, O, ST, S, L, scale); break;
+    case 80: hipLaunchKernelGGL((attn_fwd_kernel<20, 5>), grid, dim3(256), 0, st, Q, K, V, O, ST, S, L, scale); break;
     default: SKP_CHECK_ARG(false, "head dim must be 40, 64 or 80");
   }
   SKP_LAUNCH_CHECK();
@@ -400,16 +404,20 @@ extern "C" int skp_attn_fwd(const float* Q, const float* K, const float* V, floa
 // key lane&15), which is the B operand of dVᵀ += dOᵀ·P and dKᵀ += Qᵀ·dS as it stands, with the
 // reduction over rows in the permuted order r = k-step.  The four waves' partial dV / dK are
 // summed through LDS at the end (fixed order).
+// RC (recompute, skp_attn_bwd_flash): P is not read but rebuilt per row block from Q·Kᵀ on the
+// matrix cores (same C layout as dP) and the forward's row stats (m, 1/l), so the forward never
+// writes the (B·H, S, L) probabilities.
 namespace {
 
-template <int KS, int DB, int WPE>   // head dim / 4, 16-wide head-dim blocks, waves per SIMD (d = 40: 2 fit)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void attn_bwd_kv_kernel(const float* __restrict__ P, const float* __restrict__ dO,
-                                                          const float* __restrict__ Q, const float* __restrict__ V,
-                                                          const float* __restrict__ D, float* __restrict__ dS,
-                                                          float* __restrict__ dV, float* __restrict__ dK, int S, int L,
-                                                          float alpha) {
+template <int KS, int DB, int WPE, bool RC>   // head dim / 4, 16-wide head-dim blocks, waves per SIMD, recompute P
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void attn_bwd_kv_kernel(
+    const float* __restrict__ P, const float* __restrict__ dO, const float* __restrict__ Q, const float* __restrict__ V,
+    const float* __restrict__ D, float* __restrict__ dS, float* __restrict__ dV, float* __restrict__ dK, int S, int L,
+    float alpha, const float* __restrict__ Kt, const float2* __restrict__ ST, float scale) {
   constexpr int d = 4 * KS, dp = d + 1, dq = 16 * DB + 1;
   __shared__ float sV[64 * dp];     // this block's keys
+  __shared__ float sK[RC ? 64 * dp : 1];
+  __shared__ float2 sST[2][RC ? 64 : 1];
   __shared__ float sO[2][64 * dq], sQ[2][64 * dq];   // row blocks of dO and Q, double-buffered (zero-padded to 16·DB)
   __shared__ float sD[2][64];
   const int b = blockIdx.y, k0 = blockIdx.x * 64;
@@ -421,6 +429,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
       const float4 v = gV[e];
       float* p = sV + key * dp + c;
       p[0] = v.x; p[1] = v.y; p[2] = v.z; p[3] = v.w;
+      if constexpr (RC) {
+        const float4 kk = reinterpret_cast<const float4*>(Kt + ((size_t)b * L + k0) * d)[e];
+        float* pk = sK + key * dp + c;
+        pk[0] = kk.x; pk[1] = kk.y; pk[2] = kk.z; pk[3] = kk.w;
+      }
     }
     for (int e = t; e < 64 * (dq - d); e += 256) {   // zero pad of the dO / Q tiles (stays zero)
       const int row = e / (dq - d), c = d + (e - row * (dq - d));
@@ -433,6 +446,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
   constexpr int NPF = (64 * KS + 255) / 256;
   float4 fo[NPF], fq[NPF];
   float fd = 0.0f;
+  float2 fst = make_float2(0.0f, 0.0f);
   const int rl = 16 * w + 4 * (lane >> 4);
   auto fetch = [&](int r0) {
     const float4* gO = reinterpret_cast<const float4*>(dO + ((size_t)b * S + r0) * d);
@@ -442,7 +456,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
       const int e = t + 256 * j;
       if (e < 64 * KS) { fo[j] = gO[e]; fq[j] = gQ[e]; }
     }
-    if (t < 64) fd = D[(size_t)b * S + r0 + t];
+    if (t < 64) {
+      fd = D[(size_t)b * S + r0 + t];
+      if constexpr (RC) fst = ST[(size_t)b * S + r0 + t];
+    }
   };
   auto stash = [&](int buf) {
 #pragma unroll
@@ -456,16 +473,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
         pq[0] = fq[j].x; pq[1] = fq[j].y; pq[2] = fq[j].z; pq[3] = fq[j].w;
       }
     }
-    if (t < 64) sD[buf][t] = fd;
+    if (t < 64) {
+      sD[buf][t] = fd;
+      if constexpr (RC) sST[buf][t] = fst;
+    }
   };
   // lane's P / dS elements: rows r0 + rl + r, keys k0 + 16bj + (lane&15)
   const float* Pl = P + ((size_t)b * S + rl) * L + k0 + (lane & 15);
   float* dSl = dS + ((size_t)b * S + rl) * L + k0 + (lane & 15);
   f32x4a pc[4];
+  if constexpr (!RC) {
 #pragma unroll
-  for (int bj = 0; bj < 4; ++bj)
+    for (int bj = 0; bj < 4; ++bj)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) pc[bj][r] = Pl[(size_t)r * L + 16 * bj];
+      for (int r = 0; r < 4; ++r) pc[bj][r] = Pl[(size_t)r * L + 16 * bj];
+  }
   fetch(0);
   stash(0);
   f32x4a dv[DB][4], dk[DB][4];
@@ -482,11 +504,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
     f32x4a pn[4];
     if (more) {
       fetch(r0 + 64);
-      const float* Pn = Pl + (size_t)(r0 + 64) * L;
+      if constexpr (!RC) {
+        const float* Pn = Pl + (size_t)(r0 + 64) * L;
 #pragma unroll
-      for (int bj = 0; bj < 4; ++bj)
+        for (int bj = 0; bj < 4; ++bj)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) pn[bj][r] = Pn[(size_t)r * L + 16 * bj];
+          for (int r = 0; r < 4; ++r) pn[bj][r] = Pn[(size_t)r * L + 16 * bj];
+      }
     }
     const float* tO = sO[buf];
     const float* tQ = sQ[buf];
@@ -503,6 +527,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 #pragma unroll
         for (int bj = 0; bj < 4; ++bj)
           dp4[bj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, vb[16 * bj * dp + 4 * ks], dp4[bj], 0, 0, 0);
+      }
+    }
+    if constexpr (RC) {   // P = exp(scale·Q·Kᵀ − m) / l in the C layout of dP
+      f32x4a sc[4];
+      const float* qa = tQ + (16 * w + (lane & 15)) * dq + (lane >> 4);
+      const float* kb = sK + (lane & 15) * dp + (lane >> 4);
+#pragma unroll
+      for (int bj = 0; bj < 4; ++bj) sc[bj] = f32x4a{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const float a = qa[4 * ks];
+#pragma unroll
+        for (int bj = 0; bj < 4; ++bj)
+          sc[bj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, kb[16 * bj * dp + 4 * ks], sc[bj], 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float2 st = sST[buf][rl + r];
+#pragma unroll
+        for (int bj = 0; bj < 4; ++bj) pc[bj][r] = __expf(sc[bj][r] * scale - st.x) * st.y;
       }
     }
     f32x4a s4[4];
@@ -535,8 +579,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
     }
     if (more) {
       stash(buf ^ 1);
+      if constexpr (!RC) {
 #pragma unroll
-      for (int bj = 0; bj < 4; ++bj) pc[bj] = pn[bj];
+        for (int bj = 0; bj < 4; ++bj) pc[bj] = pn[bj];
+      }
     }
   }
   // sum the four waves' partials (LDS, wave order), then lane: dVᵀ[d = 16db + 4(lane>>4) + r'][key
@@ -582,9 +628,41 @@ extern "C" int skp_attn_bwd_kv(const float* P, const float* dO, const float* Q, 
   const dim3 grid((unsigned)(L / 64), (unsigned)BH);
   hipStream_t st = as_stream(stream);
   switch (d) {
-    case 40: hipLaunchKernelGGL((attn_bwd_kv_kernel<10, 3, 2>), grid, dim3(256), 0, st, P, dO, Q, V, D, dS, dV, dK, S, L, alpha); break;
-    case 64: hipLaunchKernelGGL((attn_bwd_kv_kernel<16, 4, 1>), grid, dim3(256), 0, st, P, dO, Q, V, D, dS, dV, dK, S, L, alpha); break;
-    case 80: hipLaunchKernelGGL((attn_bwd_kv_kernel<20, 5, 1>), grid, dim3(256), 0, st, P, dO, Q, V, D, dS, dV, dK, S, L, alpha); break;
+#define SKP_BKV(KS_, DB_, W_) \
+  hipLaunchKernelGGL((attn_bwd_kv_kernel<KS_, DB_, W_, false>), grid, dim3(256), 0, st, P, dO, Q, V, D, dS, dV, dK, S, L, \
+                     alpha, nullptr, nullptr, 0.0f)
+    case 40: SKP_BKV(10, 3, 2); break;
+    case 64: SKP_BKV(16, 4, 1); break;
+    case 80: SKP_BKV(20, 5, 1); break;
+#undef SKP_BKV
+    default: SKP_CHECK_ARG(false, "head dim must be 40, 64 or 80");
+  }
+  SKP_LAUNCH_CHECK();
+  return SKP_OK;
+}
+
+extern "C" int skp_attn_bwd_flash(const float* Q, const float* K, const float* V, const float* dO, const float* stats,
+                                  const float* D, float* dS, float* dV, float* dK, int BH, int S, int L, int d, float scale,
+                                  void* stream) {
+  SKP_CHECK_ARG(Q && K && V && dO && stats && D && dS && dV && dK, "null pointer");
+  SKP_CHECK_ARG(BH > 0 && S > 0 && L > 0, "non-positive shape");
+  SKP_CHECK_ARG(S % 64 == 0 && L % 64 == 0, "S and L must be multiples of 64");
+  SKP_CHECK_ARG(BH <= 65535, "grid too large");
+  SKP_CHECK_ARG(((reinterpret_cast<uintptr_t>(dO) | reinterpret_cast<uintptr_t>(Q) | reinterpret_cast<uintptr_t>(K) |
+                  reinterpret_cast<uintptr_t>(V) | reinterpret_cast<uintptr_t>(dV) | reinterpret_cast<uintptr_t>(dK)) &
+                 15) == 0 && (reinterpret_cast<uintptr_t>(stats) & 7) == 0,
+                "tensors must be 16-byte aligned (stats 8-byte)");
+  const dim3 grid((unsigned)(L / 64), (unsigned)BH);
+  hipStream_t st = as_stream(stream);
+  const float2* ST = reinterpret_cast<const float2*>(stats);
+  switch (d) {
+#define SKP_BFL(KS_, DB_, W_) \
+  hipLaunchKernelGGL((attn_bwd_kv_kernel<KS_, DB_, W_, true>), grid, dim3(256), 0, st, nullptr, dO, Q, V, D, dS, dV, dK, \
+                     S, L, scale, K, ST, scale)
+    case 40: SKP_BFL(10, 3, 2); break;
+    case 64: SKP_BFL(16, 4, 1); break;
+    case 80: SKP_BFL(20, 5, 1); break;
+#undef SKP_BFL
     default: SKP_CHECK_ARG(false, "head dim must be 40, 64 or 80");
   }
   SKP_LAUNCH_CHECK();

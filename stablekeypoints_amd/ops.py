@@ -544,7 +544,7 @@ def attention_nograd(q, k, v, scale):
     if (q.dtype == F32 and S % 64 == 0 and L % 64 == 0 and d in (40, 64, 80) and q.is_contiguous()
             and k.is_contiguous() and v.is_contiguous()):
         out = torch.empty_like(q)
-        call("skp_attn_fwd", ptr(q), ptr(k), ptr(v), ptr(out), BH, S, L, d, float(scale), stream(q.device))
+        call("skp_attn_fwd", ptr(q), ptr(k), ptr(v), ptr(out), None, BH, S, L, d, float(scale), stream(q.device))
         return out
     return torch.bmm(attention_probs(q, k, scale), v)
 
@@ -636,9 +636,53 @@ def geglu(h):
     return Geglu.apply(h)
 
 
+# head dims whose grad-needing attention keeps no probability tensor (FlashAttention below);
+# SKP_ATTN_FLASH=0 disables it, =all routes every supported head dim
+ATTN_FLASH = {"0": (), "all": (40, 64, 80)}.get(os.environ.get("SKP_ATTN_FLASH", ""), (40,))
+
+
+class FlashAttention(torch.autograd.Function):
+    """softmax(q kᵀ·scale) v without a saved (B·H, S, L) probability tensor: the forward is the
+    online-softmax skp_attn_fwd emitting per-row (max, 1/sum); the backward skp_attn_bwd_flash
+    rebuilds P per key block from q kᵀ and those stats and produces dS, dV, dK in one pass
+    (dQ = dS k stays a GEMM).  Same result as MathAttention within fp32 rounding."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, scale):
+        BH, S, d = q.shape
+        L = k.shape[1]
+        out = torch.empty_like(q)
+        stats = torch.empty(BH, S, 2, device=q.device, dtype=F32)
+        call("skp_attn_fwd", ptr(q), ptr(k), ptr(v), ptr(out), ptr(stats), BH, S, L, d, float(scale),
+             stream(q.device))
+        ctx.save_for_backward(q, k, v, out, stats)
+        ctx.scale = scale
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, k, v, out, stats = ctx.saved_tensors
+        dout = dout.contiguous()
+        BH, S, d = q.shape
+        L = k.shape[1]
+        D = (dout * out).sum(-1)
+        ds = torch.empty(BH, S, L, device=q.device, dtype=F32)
+        dv, dk = torch.empty_like(v), torch.empty_like(k)
+        call("skp_attn_bwd_flash", ptr(q), ptr(k), ptr(v), ptr(dout), ptr(stats), ptr(D), ptr(ds), ptr(dv), ptr(dk),
+             BH, S, L, d, float(ctx.scale), stream(q.device))
+        dq = torch.bmm(ds, k) if ctx.needs_input_grad[0] else None
+        return dq, dk if ctx.needs_input_grad[1] else None, dv if ctx.needs_input_grad[2] else None, None
+
+
 def math_attention(q, k, v, scale):
-    """softmax(q kᵀ·scale) v with the fused softmax backward (HIP device)."""
+    """softmax(q kᵀ·scale) v with a fused backward (HIP device): FlashAttention for the head
+    dims in ATTN_FLASH at 64-multiple shapes, else MathAttention."""
     _lib.require_device(q, k, v)
+    BH, S, d = q.shape
+    L = k.shape[1]
+    if (d in ATTN_FLASH and S % 64 == 0 and L % 64 == 0 and q.dtype == F32
+            and all(t.dtype == F32 and t.is_contiguous() and t.data_ptr() % 16 == 0 for t in (q, k, v))):
+        return FlashAttention.apply(q, k, v, float(scale))
     return MathAttention.apply(q, k, v, float(scale))
 
 

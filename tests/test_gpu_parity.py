@@ -497,6 +497,7 @@ def test_attn_bwd_kv_vs_unfused(monkeypatch, BH, S, L, D, q_grad):
     base = [torch.randn(BH, n, D, generator=g).to(DEV) for n in (S, L, L)]
     dout = torch.randn(BH, S, D, generator=g).to(DEV)
     grads = {}
+    monkeypatch.setattr(ops, "ATTN_FLASH", ())
     for fused in (True, False):
         monkeypatch.setattr(ops, "ATTN_FUSED_KV", (40, 64, 80) if fused else ())
         q, k, v = (t.clone().requires_grad_(rg) for t, rg in zip(base, (q_grad, True, True)))
@@ -511,6 +512,38 @@ def test_attn_bwd_kv_vs_unfused(monkeypatch, BH, S, L, D, q_grad):
         tol = 1e-4 * max(1.0, ref.abs().max().item())
         assert (grads[True][i].double() - ref).abs().max().item() < tol
         assert (grads[True][i] - grads[False][i]).abs().max().item() < tol
+
+
+@pytest.mark.parametrize("BH,S,L,D,q_grad", [(2, 256, 320, 64, True), (3, 128, 128, 80, False), (1, 4096, 4096, 40, True),
+                                             (5, 64, 640, 40, True), (4, 1024, 1024, 40, True)])
+def test_flash_attention_vs_math_and_fp64(monkeypatch, BH, S, L, D, q_grad):
+    """FlashAttention (skp_attn_fwd with row stats + skp_attn_bwd_flash rebuilding P) vs the
+    P-saving MathAttention and fp64 autograd: output and (q, k, v) gradients."""
+    from stablekeypoints_amd import ops
+    g = torch.Generator().manual_seed(S * 3 + L + D)
+    base = [(torch.randn(BH, n, D, generator=g) * 1.5).to(DEV) for n in (S, L, L)]
+    dout = torch.randn(BH, S, D, generator=g).to(DEV)
+    res = {}
+    for flash in (True, False):
+        monkeypatch.setattr(ops, "ATTN_FLASH", (40, 64, 80) if flash else ())
+        q, k, v = (t.clone().requires_grad_(rg) for t, rg in zip(base, (q_grad, True, True)))
+        out = ops.math_attention(q, k, v, D ** -0.5)
+        assert (out.grad_fn.__class__.__name__ == "FlashAttentionBackward") == flash
+        (out * dout).sum().backward()
+        res[flash] = [out.detach()] + [t.grad for t in (q, k, v)]
+    qd, kd, vd = (t.double().requires_grad_(True) for t in base)
+    ref = torch.softmax(qd @ kd.transpose(1, 2) * D ** -0.5, -1) @ vd
+    (ref * dout.double()).sum().backward()
+    # online softmax with the fast exp: within 2e-5 like attention_nograd (north_star bar: 1e-4)
+    assert (res[True][0].double() - ref).abs().max().item() < 2e-5
+    assert (res[True][0] - res[False][0]).abs().max().item() < 2e-5
+    for i, r in enumerate((qd.grad, kd.grad, vd.grad), start=1):
+        if i == 1 and not q_grad:
+            assert res[True][1] is None
+            continue
+        tol = 1e-4 * max(1.0, r.abs().max().item())
+        assert (res[True][i].double() - r).abs().max().item() < tol
+        assert (res[True][i] - res[False][i]).abs().max().item() < tol
 
 
 @pytest.mark.parametrize("rows,cols", [(64, 4096), (33, 500), (128, 1024), (7, 77), (5, 16384), (9, 12)])

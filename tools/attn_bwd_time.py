@@ -68,3 +68,38 @@ def full_fused():
 print(f"full backward: unfused {timed(full_unfused):.3f} ms   fused dS/dV/dK {timed(full_fused):.3f} ms")
 a, b = full_unfused(), full_fused()
 print("max rel diff dq/dk/dv", [((x - y).abs().max() / x.abs().max()).item() for x, y in zip(a, b)])
+
+stats = torch.empty(BH, S, 2, device=dev)
+o_fl = torch.empty_like(q)
+ds_fl, dv_fl, dk_fl = torch.empty_like(p), torch.empty_like(v), torch.empty_like(k)
+
+
+def flash_fwd():
+    call("skp_attn_fwd", ptr(q), ptr(k), ptr(v), ptr(o_fl), ptr(stats), BH, S, L, d, d ** -0.5, stream(dev))
+
+
+def flash_bwd():
+    D = (dout * o_fl).sum(-1)
+    call("skp_attn_bwd_flash", ptr(q), ptr(k), ptr(v), ptr(dout), ptr(stats), ptr(D), ptr(ds_fl), ptr(dv_fl),
+         ptr(dk_fl), BH, S, L, d, d ** -0.5, stream(dev))
+    return torch.bmm(ds_fl, k), dk_fl, dv_fl
+
+
+def math_fwd():
+    pp = ops.attention_probs(q, k, d ** -0.5)
+    return torch.bmm(pp, v)
+
+
+def math_bwd():
+    D = (dout * out).sum(-1)
+    call("skp_attn_bwd_kv", ptr(p), ptr(dout), ptr(q), ptr(v), ptr(D), ptr(ds_new), ptr(dv_), ptr(dk_),
+         BH, S, L, d, d ** -0.5, stream(dev))
+    return torch.bmm(ds_new, k), dk_, dv_
+
+
+print(f"train fwd: math {timed(math_fwd):.3f} ms  flash {timed(flash_fwd):.3f} ms | "
+      f"bwd: math (saved P) {timed(math_bwd):.3f} ms  flash (rebuilt P) {timed(flash_bwd):.3f} ms")
+flash_fwd()
+a, b = math_bwd(), flash_bwd()
+print("flash vs math rel diff dq/dk/dv", [((x - y).abs().max() / x.abs().max()).item() for x, y in zip(a, b)],
+      "out", ((o_fl - out).abs().max() / out.abs().max()).item())
