@@ -638,7 +638,7 @@ def geglu(h):
 
 # head dims whose grad-needing attention keeps no probability tensor (FlashAttention below);
 # SKP_ATTN_FLASH=0 disables it, =all routes every supported head dim
-ATTN_FLASH = {"0": (), "all": (40, 64, 80)}.get(os.environ.get("SKP_ATTN_FLASH", ""), (40,))
+ATTN_FLASH = {"0": (), "all": (40, 64, 80)}.get(os.environ.get("SKP_ATTN_FLASH", ""), (40, 64))
 
 
 class FlashAttention(torch.autograd.Function):
