@@ -183,15 +183,16 @@ int skp_attn_dscore(const float* P, const float* dO, const float* V, const float
 int skp_attn_bwd_kv(const float* P, const float* dO, const float* Q, const float* V, const float* D, float* dS,
                     float* dV, float* dK, int BH, int S, int L, int d, float alpha, void* stream);
 /* Fused attention O = softmax(scale·Q Kᵀ) V (online softmax; no score tensor); with stats
- * non-null also the per-row (max, 1/sum) pairs (BH, S, 2) that skp_attn_bwd_flash consumes.  Q (BH, S, d), K, V (BH, L, d), O (BH, S, d); S, L multiples
- * of 64; d ∈ {40, 64, 80}.                                                      */
+ * non-null also the per-row (max, 1/sum) pairs (BH, S, 2) that skp_attn_bwd_flash consumes.
+ * Q (BH, S, d), K, V (BH, L, d), O (BH, S, d); S a multiple of 64, L any (the last key block
+ * is masked); d ∈ {40, 64, 80}.                                                  */
 int skp_attn_fwd(const float* Q, const float* K, const float* V, float* O, float* stats, int BH, int S, int L, int d,
                  float scale, void* stream);
 /* Attention backward that rebuilds P = exp(scale·Q Kᵀ − m) · (1/l) per key block from the
  * forward's row stats (stats from skp_attn_fwd, (BH, S) × (m, 1/l)) instead of reading a saved P:
  * dS (BH, S, L) = scale·P⊙(dO·Vᵀ − D), dV = Pᵀ·dO, dK = dSᵀ·Q; dQ = dS·K is left to a GEMM.
- * Q, dO (BH, S, d); K, V, dV, dK (BH, L, d); D = rowsum(dO⊙O) (BH, S).  S, L multiples of 64;
- * d ∈ {40, 64, 80}; 16-byte aligned (stats 8).                                                  */
+ * Q, dO (BH, S, d); K, V, dV, dK (BH, L, d); D = rowsum(dO⊙O) (BH, S).  S a multiple of 64,
+ * L any; d ∈ {40, 64, 80}; 16-byte aligned (stats 8).                                                  */
 int skp_attn_bwd_flash(const float* Q, const float* K, const float* V, const float* dO, const float* stats,
                        const float* D, float* dS, float* dV, float* dK, int BH, int S, int L, int d, float scale,
                        void* stream);

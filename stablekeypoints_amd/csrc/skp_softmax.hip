@@ -306,7 +306,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
       const float4* gV = reinterpret_cast<const float4*>(V + ((size_t)b * L + k0) * d);
       for (int e = t; e < 64 * KS; e += 256) {
         const int key = e / KS, c = 4 * (e - key * KS);
-        const float4 kk = gK[e], vv = gV[e];
+        float4 kk = make_float4(0.f, 0.f, 0.f, 0.f), vv = kk;   // keys past L (ragged last block): zero
+        if (k0 + key < L) { kk = gK[e]; vv = gV[e]; }
         float* pk = sK + key * dp + c;
         pk[0] = kk.x; pk[1] = kk.y; pk[2] = kk.z; pk[3] = kk.w;
         *reinterpret_cast<float4*>(sV + key * 16 * DB + c) = vv;
@@ -326,6 +327,13 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
       const float* kr = sK + (16 * c + (lane & 15)) * dp + (lane >> 4);
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) s4[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(kr[4 * ks], qv[ks], s4[c], 0, 0, 0);
+    }
+    if (k0 + 64 > L) {   // keys past L take no probability
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (k0 + 16 * c + 4 * (lane >> 4) + r >= L) s4[c][r] = -INFINITY;
     }
     float bm = -INFINITY;
 #pragma unroll
@@ -377,7 +385,7 @@ extern "C" int skp_attn_fwd(const float* Q, const float* K, const float* V, floa
                             int L, int d, float scale, void* stream) {
   SKP_CHECK_ARG(Q && K && V && O, "null pointer");
   SKP_CHECK_ARG(BH > 0 && S > 0 && L > 0, "non-positive shape");
-  SKP_CHECK_ARG(S % 64 == 0 && L % 64 == 0, "S and L must be multiples of 64");
+  SKP_CHECK_ARG(S % 64 == 0, "S must be a multiple of 64");
   SKP_CHECK_ARG(BH <= 65535, "grid too large");
   SKP_CHECK_ARG(((reinterpret_cast<uintptr_t>(K) | reinterpret_cast<uintptr_t>(V) | reinterpret_cast<uintptr_t>(O)) &
                  15) == 0,
@@ -426,11 +434,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
     const float4* gV = reinterpret_cast<const float4*>(V + ((size_t)b * L + k0) * d);
     for (int e = t; e < 64 * KS; e += 256) {
       const int key = e / KS, c = 4 * (e - key * KS);
-      const float4 v = gV[e];
+      const bool in = k0 + key < L;   // ragged last block (RC only): keys past L are zero
+      const float4 v = in ? gV[e] : make_float4(0.f, 0.f, 0.f, 0.f);
       float* p = sV + key * dp + c;
       p[0] = v.x; p[1] = v.y; p[2] = v.z; p[3] = v.w;
       if constexpr (RC) {
-        const float4 kk = reinterpret_cast<const float4*>(Kt + ((size_t)b * L + k0) * d)[e];
+        const float4 kk = in ? reinterpret_cast<const float4*>(Kt + ((size_t)b * L + k0) * d)[e] : make_float4(0.f, 0.f, 0.f, 0.f);
         float* pk = sK + key * dp + c;
         pk[0] = kk.x; pk[1] = kk.y; pk[2] = kk.z; pk[3] = kk.w;
       }
@@ -546,7 +555,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
       for (int r = 0; r < 4; ++r) {
         const float2 st = sST[buf][rl + r];
 #pragma unroll
-        for (int bj = 0; bj < 4; ++bj) pc[bj][r] = __expf(sc[bj][r] * scale - st.x) * st.y;
+        for (int bj = 0; bj < 4; ++bj)
+          pc[bj][r] = k0 + 16 * bj + (lane & 15) < L ? __expf(sc[bj][r] * scale - st.x) * st.y : 0.0f;
       }
     }
     f32x4a s4[4];
@@ -557,7 +567,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 #pragma unroll
       for (int bj = 0; bj < 4; ++bj) {
         const float sv = alpha * (pc[bj][r] * (dp4[bj][r] - Dr));
-        dSr[(size_t)r * L + 16 * bj] = sv;
+        if (!RC || k0 + 16 * bj + (lane & 15) < L) dSr[(size_t)r * L + 16 * bj] = sv;
         s4[bj][r] = sv;
       }
     }
@@ -606,7 +616,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
           }
           const int dd = 16 * db + 4 * (lane >> 4);
           const int key = k0 + 16 * bj + (lane & 15);
-          if (dd < d) *reinterpret_cast<float4*>((m == 0 ? dV : dK) + ((size_t)b * L + key) * d + dd) = acc;
+          if (dd < d && key < L) *reinterpret_cast<float4*>((m == 0 ? dV : dK) + ((size_t)b * L + key) * d + dd) = acc;
         }
         __syncthreads();
       }
@@ -646,13 +656,13 @@ extern "C" int skp_attn_bwd_flash(const float* Q, const float* K, const float* V
                                   void* stream) {
   SKP_CHECK_ARG(Q && K && V && dO && stats && D && dS && dV && dK, "null pointer");
   SKP_CHECK_ARG(BH > 0 && S > 0 && L > 0, "non-positive shape");
-  SKP_CHECK_ARG(S % 64 == 0 && L % 64 == 0, "S and L must be multiples of 64");
+  SKP_CHECK_ARG(S % 64 == 0, "S must be a multiple of 64");
   SKP_CHECK_ARG(BH <= 65535, "grid too large");
   SKP_CHECK_ARG(((reinterpret_cast<uintptr_t>(dO) | reinterpret_cast<uintptr_t>(Q) | reinterpret_cast<uintptr_t>(K) |
                   reinterpret_cast<uintptr_t>(V) | reinterpret_cast<uintptr_t>(dV) | reinterpret_cast<uintptr_t>(dK)) &
                  15) == 0 && (reinterpret_cast<uintptr_t>(stats) & 7) == 0,
                 "tensors must be 16-byte aligned (stats 8-byte)");
-  const dim3 grid((unsigned)(L / 64), (unsigned)BH);
+  const dim3 grid((unsigned)((L + 63) / 64), (unsigned)BH);
   hipStream_t st = as_stream(stream);
   const float2* ST = reinterpret_cast<const float2*>(stats);
   switch (d) {

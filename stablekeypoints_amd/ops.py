@@ -538,10 +538,11 @@ def attention_probs(q, k, scale):
 
 def attention_nograd(q, k, v, scale):
     """softmax(q kᵀ·scale) v when no gradient is needed: the fused online-softmax kernel
-    (skp_attn_fwd, no score tensor) where the shapes allow, else the scores + in-place softmax."""
+    (skp_attn_fwd, no score tensor; any key count) where the shapes allow, else the scores +
+    in-place softmax."""
     BH, S, d = q.shape
     L = k.shape[1]
-    if (q.dtype == F32 and S % 64 == 0 and L % 64 == 0 and d in (40, 64, 80) and q.is_contiguous()
+    if (q.dtype == F32 and S % 64 == 0 and d in (40, 64, 80) and q.is_contiguous()
             and k.is_contiguous() and v.is_contiguous()):
         out = torch.empty_like(q)
         call("skp_attn_fwd", ptr(q), ptr(k), ptr(v), ptr(out), None, BH, S, L, d, float(scale), stream(q.device))
@@ -676,11 +677,12 @@ class FlashAttention(torch.autograd.Function):
 
 def math_attention(q, k, v, scale):
     """softmax(q kᵀ·scale) v with a fused backward (HIP device): FlashAttention for the head
-    dims in ATTN_FLASH at 64-multiple shapes, else MathAttention."""
+    dims in ATTN_FLASH when S is a multiple of 64 (any key count: the last key block is
+    masked), else MathAttention."""
     _lib.require_device(q, k, v)
     BH, S, d = q.shape
     L = k.shape[1]
-    if (d in ATTN_FLASH and S % 64 == 0 and L % 64 == 0 and q.dtype == F32
+    if (d in ATTN_FLASH and S % 64 == 0 and q.dtype == F32
             and all(t.dtype == F32 and t.is_contiguous() and t.data_ptr() % 16 == 0 for t in (q, k, v))):
         return FlashAttention.apply(q, k, v, float(scale))
     return MathAttention.apply(q, k, v, float(scale))

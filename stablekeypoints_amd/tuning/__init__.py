@@ -6,13 +6,15 @@ regenerates it: one bench run with tuning on, ≈3 min).  Loading it swaps each 
 heuristic kernel choice for the measured one — the same arithmetic (fp32 in, fp32 accumulate),
 a different kernel and reduction order — and leaves unlisted shapes on the default path.  The
 file's validator lines pin PyTorch / HIP / hipBLASLt / rocBLAS versions and the gfx950 arch; on
-any mismatch it is not used.  ``SKP_TUNED_GEMMS=0`` disables it.
+any mismatch it is not used.  ``SKP_TUNED_GEMMS=0`` disables it; ``SKP_TUNED_GEMMS_FILE``
+names another results file (A/B of a re-tuning).
 """
 import os
 
 import torch
 
-TUNED_GEMMS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_gfx950.csv")
+TUNED_GEMMS = os.environ.get("SKP_TUNED_GEMMS_FILE") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                                     "gemm_gfx950.csv")
 _state = {"loaded": None}
 
 

@@ -515,7 +515,8 @@ def test_attn_bwd_kv_vs_unfused(monkeypatch, BH, S, L, D, q_grad):
 
 
 @pytest.mark.parametrize("BH,S,L,D,q_grad", [(2, 256, 320, 64, True), (3, 128, 128, 80, False), (1, 4096, 4096, 40, True),
-                                             (5, 64, 640, 40, True), (4, 1024, 1024, 40, True)])
+                                             (5, 64, 640, 40, True), (4, 1024, 1024, 40, True), (4, 512, 500, 40, True),
+                                             (2, 256, 77, 64, False), (3, 128, 1, 40, True), (2, 64, 129, 80, True)])
 def test_flash_attention_vs_math_and_fp64(monkeypatch, BH, S, L, D, q_grad):
     """FlashAttention (skp_attn_fwd with row stats + skp_attn_bwd_flash rebuilding P) vs the
     P-saving MathAttention and fp64 autograd: output and (q, k, v) gradients."""
@@ -602,10 +603,10 @@ def test_capture_bwd_with_forward_stats_equals_recomputed(BH, s, R, N):
 
 
 @pytest.mark.parametrize("BH,S,L,D", [(8, 4096, 4096, 40), (4, 256, 192, 40), (3, 128, 512, 64), (2, 1024, 1024, 80),
-                                      (2, 64, 77, 40)])
+                                      (2, 64, 77, 40), (8, 4096, 500, 40), (2, 128, 1, 64)])
 def test_attention_nograd_fused_vs_fp64(BH, S, L, D):
-    """ops.attention_nograd (skp_attn_fwd: online softmax, no score tensor; the scores path where
-    L is not a multiple of 64) vs torch fp64, including large-magnitude logits."""
+    """ops.attention_nograd (skp_attn_fwd: online softmax, no score tensor, ragged last key
+    block when L is not a multiple of 64) vs torch fp64, including large-magnitude logits."""
     from stablekeypoints_amd import ops
     g = torch.Generator().manual_seed(S + L + D)
     q = (torch.randn(BH, S, D, generator=g) * 2).to(DEV)
