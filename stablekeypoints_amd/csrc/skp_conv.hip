@@ -50,7 +50,7 @@ constexpr int kNC = 32;                       // output channels per workgroup
 constexpr int kCK = 4;                        // input channels per LDS stage (= MFMA k)
 constexpr int kP = 36;                        // transform positions (6×6)
 constexpr int kThreads = 512;                 // 8 waves, two per SIMD
-constexpr int kVs = kCK * kMT * kP;           // floats per V stage  (9216)
+// V stage: kCK · MT · kP floats (9216 at MT = 64)
 constexpr int kUs = kCK * kNC * kP;           // floats per U stage  (4608)
 constexpr int kUChunks = kUs * 4 / 1024;      // 1-KB DMA chunks per U stage (18)
 constexpr int kRawRow = 64 * 16 + 64 * 4 + 64 * 4;   // bytes per patch row per wave: middle, left, right
@@ -121,7 +121,7 @@ __device__ __forceinline__ void dma_patches(__amdgpu_buffer_rsrc_t rs, const Pat
 }
 
 // This lane's raw patch (LDS) → masked → V = Bᵀ d B → V stage row (ch, tile), 6 positions per row
-__device__ __forceinline__ void transform_patch(const char* raw, unsigned mask, int lane, float* vd) {
+__device__ __forceinline__ void transform_patch(const char* raw, unsigned mask, int lane, float* vd, bool store = true) {
   float d[36];
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
@@ -148,22 +148,30 @@ __device__ __forceinline__ void transform_patch(const char* raw, unsigned mask, 
   for (int i = 0; i < 6; ++i) {
     float v[6];
     bt6(d[6 * i], d[6 * i + 1], d[6 * i + 2], d[6 * i + 3], d[6 * i + 4], d[6 * i + 5], v, 1);
-    *reinterpret_cast<float2*>(vd + 6 * i) = make_float2(v[0], v[1]);
-    *reinterpret_cast<float2*>(vd + 6 * i + 2) = make_float2(v[2], v[3]);
-    *reinterpret_cast<float2*>(vd + 6 * i + 4) = make_float2(v[4], v[5]);
+    if (store) {
+      *reinterpret_cast<float2*>(vd + 6 * i) = make_float2(v[0], v[1]);
+      *reinterpret_cast<float2*>(vd + 6 * i + 2) = make_float2(v[2], v[3]);
+      *reinterpret_cast<float2*>(vd + 6 * i + 4) = make_float2(v[4], v[5]);
+    }
   }
 }
 
-// EPI bit 0: + bias[k]; bit 1: + residual (same layout as y)
-template <int EPI>
+// EPI bit 0: + bias[k]; bit 1: + residual (same layout as y).
+// MT = output tiles per workgroup: 64 (× 32 output channels), or 32 (× 64 output channels) for
+// grids of at most 32 tiles (the UNet's 8² layers at batch 8), where a 64-tile block would run
+// half of its MFMAs on empty tiles; lanes 32-63 of the patch waves then only idle.
+template <int EPI, int MT>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void wino_f4_kernel(
     const float* __restrict__ x, const float* __restrict__ U, const float* __restrict__ bias,
     const float* __restrict__ res, float* __restrict__ y, int nimg, int C, int K, int H, int W, int tw, int tpi,
     int ntiles, int ntb, int nkb, int kb_major, int csplit, int dbg) {
   // separate LDS objects per buffer, so the compiler can tell a DMA into one buffer from a
   // ds_read of another and does not wait for the DMA before every LDS read
-  __shared__ __attribute__((aligned(16))) float V0[kVs], V1[kVs];   // [kCK][kMT][kP]
-  __shared__ __attribute__((aligned(16))) float U0[kUs], U1[kUs];   // [kCK][kNC][kP]
+  constexpr int NC = kMT * kNC / MT;                // output channels per workgroup
+  constexpr int VS = kCK * MT * kP, US = kCK * NC * kP;
+  constexpr int NWM = MT / 16;                      // 16-tile MFMA row blocks
+  __shared__ __attribute__((aligned(16))) float V0[VS], V1[VS];   // [kCK][MT][kP]
+  __shared__ __attribute__((aligned(16))) float U0[US], U1[US];   // [NC / 32][kCK][32][kP]
   __shared__ __attribute__((aligned(16))) char Raw[4 * kRawWave];   // [4 waves][6 rows][mid | left | right]
 
   // workgroup → (input-channel split, tile block, channel block); consecutive logical ids share
@@ -187,13 +195,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wv & 3, wn = wv >> 2;   // this wave's 16 tiles × 16 channels
+  const int wm = wv % NWM, wn = wv / NWM;   // this wave's 16 tiles × 16 channels
   const bool patcher = wv < 4;            // waves 0-3: patches of stage channel wv; 4-7: U slices
   const size_t plane = (size_t)H * W;
   PatchAddr pa;
   {
-    const int pt = tb * kMT + lane;
-    const bool pvalid = pt < ntiles;
+    const int pt = tb * MT + lane;
+    const bool pvalid = lane < MT && pt < ntiles;
     int pb = 0, py0 = 0, px0 = 0;
     if (pvalid) {
       pb = pt / tpi;
@@ -213,23 +221,30 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
       pa.row[r] = (base + (unsigned)(yc * W + px0)) * 4u;
     }
   }
-  const float* Ub = U + ((size_t)kb * C + c0) * kNC * kP;
+  // U is stored in 32-channel slices [K / 32][C][32][kP]; a 64-channel block reads two
+  const float* Ub = U + ((size_t)(kb * (NC / kNC)) * C + c0) * kNC * kP;
+  const size_t uhalf = (size_t)C * kNC * kP;   // floats between consecutive 32-channel slices
   const int nst = csplit / kCK;
   const size_t xfloats = (size_t)nimg * C * plane;
   char* raw = Raw + (wv & 3) * kRawWave;
-  const int vrow = ((wv & 3) * kMT + lane) * kP;   // this patcher lane's V row
+  const bool vstore = lane < MT;
+  const int vrow = ((wv & 3) * MT + (vstore ? lane : 0)) * kP;   // this patcher lane's V row
   // per-stage descriptors: x from the stage's first channel plane, U from the stage's slice
   auto xrsrc = [&](int s) {
     const size_t off = ((size_t)c0 + (size_t)s * kCK) * plane;
     return __builtin_amdgcn_make_buffer_rsrc((void*)(x + off), (short)0, (dbg & 1) ? 0 : (int)((xfloats - off) * 4), 0x00020000);
   };
   auto dma_u = [&](int s, float* ubuf) {
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(Ub + (size_t)s * kUs), (short)0, (dbg & 2) ? 0 : kUs * 4, 0x00020000);
     char* dst = reinterpret_cast<char*>(ubuf);
 #pragma unroll
-    for (int c = wv - 4; c < kUChunks; c += 4)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(dst + c * 1024), 16, lane * 16, c * 1024, 0, 0);
+    for (int h = 0; h < NC / kNC; ++h) {
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(Ub + h * uhalf + (size_t)s * kUs), (short)0, (dbg & 2) ? 0 : kUs * 4, 0x00020000);
+#pragma unroll
+      for (int c = wv - 4; c < kUChunks; c += 4)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(dst + h * kUs * 4 + c * 1024), 16, lane * 16, c * 1024,
+                                                 0, 0);
+    }
   };
 
   f32x4 acc[kP];
@@ -240,7 +255,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
   if (patcher) {
     dma_patches(xrsrc(0), pa, raw);
     __builtin_amdgcn_s_waitcnt(0);   // vmcnt(0) & lgkmcnt(0): this wave's DMA landed
-    transform_patch(raw, pa.mask, lane, V0 + vrow);
+    transform_patch(raw, pa.mask, lane, V0 + vrow, vstore);
     if (nst > 1) dma_patches(xrsrc(1), pa, raw);
   } else {
     dma_u(0, U0);
@@ -249,14 +264,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
   __syncthreads();
 
   // MFMA operands: A = V[k = lane>>4][tile 16·wm + (lane&15)], B = U[k][channel 16·wn + (lane&15)]
-  const int aoff = ((lane >> 4) * kMT + wm * 16 + (lane & 15)) * kP;
-  const int boff = ((lane >> 4) * kNC + wn * 16 + (lane & 15)) * kP;
+  const int aoff = ((lane >> 4) * MT + wm * 16 + (lane & 15)) * kP;
+  const int boff = (wn >> 1) * kUs + ((lane >> 4) * kNC + (wn & 1) * 16 + (lane & 15)) * kP;
   // one stage: prepare stage s+1 into (vn, un), MFMAs on (vc, uc); the loop is unrolled by two
   // so every buffer is a fixed LDS object in each half
   auto phase = [&](int s, const float* vc, const float* uc, float* vn, float* un) {
     if (s + 1 < nst) {
       if (patcher) {
-        if (!(dbg & 4)) transform_patch(raw, pa.mask, lane, vn + vrow);
+        if (!(dbg & 4)) transform_patch(raw, pa.mask, lane, vn + vrow, vstore);
         if (s + 2 < nst) dma_patches(xrsrc(s + 2), pa, raw);
       } else {
         dma_u(s + 1, un);
@@ -283,11 +298,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
   }
 
   // epilogue: lane holds rows 4·(lane>>4)+r (tiles) × column lane&15 (channel) of every position
-  const int k = kb * kNC + wn * 16 + (lane & 15);
+  const int k = kb * NC + wn * 16 + (lane & 15);
   const float bv = (EPI & 1) ? bias[k] : 0.0f;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int t = tb * kMT + wm * 16 + 4 * (lane >> 4) + r;
+    const int t = tb * MT + wm * 16 + 4 * (lane >> 4) + r;
     if (t >= ntiles) continue;
     float m[36], o[16];
 #pragma unroll
@@ -413,7 +428,11 @@ extern "C" int skp_conv3x3_wino(const float* x, const float* U, const float* bia
   const long long ntiles = (long long)B * tpi;
   SKP_CHECK_ARG(ntiles <= 0x7fffffffLL - kMT, "too many tiles");
   SKP_CHECK_ARG((long long)B * C * H * W * 4 < 0x7fffffffLL, "input larger than 2 GiB (32-bit buffer offsets)");
-  const int ntb = (int)((ntiles + kMT - 1) / kMT), nkb = K / kNC;
+  // at most 32 tiles (8² at batch 8): 32-tile × 64-channel workgroups (SKP_WINO_WIDE=0: off)
+  static const bool wide_ok = !getenv("SKP_WINO_WIDE") || atoi(getenv("SKP_WINO_WIDE")) != 0;
+  const bool wide = wide_ok && ntiles <= 32 && K % 64 == 0;
+  const int mt = wide ? 32 : kMT;
+  const int ntb = (int)((ntiles + mt - 1) / mt), nkb = K / (wide ? 64 : kNC);
   SKP_CHECK_ARG((long long)ntb * nkb * nsplit <= 0x7fffffffLL, "grid too large");
   // one channel block's U slice is C·32·36·4 B; keep all of U on an L2 slice when it fits
   const long long ubytes = (long long)K * C * kP * 4;
@@ -423,9 +442,13 @@ extern "C" int skp_conv3x3_wino(const float* x, const float* U, const float* bia
   static const int dbg = getenv("SKP_WINO_DEBUG") ? atoi(getenv("SKP_WINO_DEBUG")) : 0;   // dev: 1 drop x loads, 2 drop U loads, 4 skip transforms, 8 skip MFMAs
   hipStream_t st = as_stream(stream);
   const dim3 grid((unsigned)(ntb * nkb * nsplit));
-#define SKP_WG(E)                                                                                                   \
-  hipLaunchKernelGGL((wino_f4_kernel<E>), grid, dim3(kThreads), 0, st, x, U, bias, residual, out, B, C, K, H, W, \
-                     tw, tpi, (int)ntiles, ntb, nkb, kb_major, C / nsplit, dbg)
+#define SKP_WG(E)                                                                                                    \
+  if (wide)                                                                                                          \
+    hipLaunchKernelGGL((wino_f4_kernel<E, 32>), grid, dim3(kThreads), 0, st, x, U, bias, residual, out, B, C, K, H, W, \
+                       tw, tpi, (int)ntiles, ntb, nkb, kb_major, C / nsplit, dbg);                                    \
+  else                                                                                                               \
+    hipLaunchKernelGGL((wino_f4_kernel<E, 64>), grid, dim3(kThreads), 0, st, x, U, bias, residual, out, B, C, K, H, W, \
+                       tw, tpi, (int)ntiles, ntb, nkb, kb_major, C / nsplit, dbg)
   switch (epi) {
     case 0: SKP_WG(0); break;
     case 1: SKP_WG(1); break;

@@ -756,6 +756,7 @@ WINO_MIN_WORKGROUPS = 128
 # "v1" forces the first kernel (A/B runs: SKP_WINO=v1).  SKP_WINO_SPLIT=0 disables split-K.
 WINO_KERNEL = os.environ.get("SKP_WINO", "auto")
 WINO_SPLIT = os.environ.get("SKP_WINO_SPLIT", "1") != "0"
+WINO_WIDE = os.environ.get("SKP_WINO_WIDE", "1") != "0"   # must match skp_conv3x3_wino's rule
 
 
 def _wino_v2(H, W, B=None):
@@ -794,6 +795,8 @@ def _wino_plan(B, C, K, H, W):
     v2 = _wino_v2(H, W, B)
     if v2:
         wgs = (B // 4 if H == 16 else B * (H // 32) * (W // 32)) * (K // 32)
+    elif WINO_WIDE and B * (H // 4) * (W // 4) <= 32 and K % 64 == 0:
+        wgs = K // 64   # one 32-tile × 64-channel block per channel block (libskp's rule, skp_conv.hip)
     else:
         wgs = -(-(B * (H // 4) * (W // 4)) // 64) * (K // 32)
     out_bytes = B * K * H * W * 4

@@ -145,6 +145,30 @@ def test_conv3x3_split_k_vs_fp64_and_unsplit(all_shapes, monkeypatch, B, C, K, H
     assert (outs[0][0] - outs[1][0]).abs().max().item() < 1e-5 * outs[1][0].abs().max().item()
 
 
+@pytest.mark.parametrize("B,C,K,H,W", [(8, 256, 128, 8, 8), (2, 128, 64, 8, 8), (3, 64, 192, 4, 12),
+                                       (8, 1280, 1280, 8, 8), (1, 96, 64, 4, 4)])
+def test_conv3x3_wide_blocks_vs_fp64(all_shapes, B, C, K, H, W):
+    """Grids of at most 32 tiles with K a multiple of 64 run as 32-tile × 64-channel workgroups
+    (skp_conv3x3_wino's wide blocks, the UNet's 8² layers): forward with bias + residual and the
+    input gradient (wide too when C is a multiple of 64) vs fp64, split-K included."""
+    ops = all_shapes
+    assert B * (H // 4) * (W // 4) <= 32 and K % 64 == 0
+    g = torch.Generator().manual_seed(C * 3 + K)
+    x = torch.randn(B, C, H, W, generator=g)
+    w = torch.randn(K, C, 3, 3, generator=g) / (3 * C ** 0.5)
+    b = torch.randn(K, generator=g)
+    r = torch.randn(B, K, H, W, generator=g)
+    dy = torch.randn(B, K, H, W, generator=g)
+    xd = x.to(DEV).requires_grad_(True)
+    y = ops.conv3x3(xd, w.to(DEV), b.to(DEV), r.to(DEV))
+    (y * dy.to(DEV)).sum().backward()
+    x64 = x.double().requires_grad_(True)
+    ref = F.conv2d(x64, w.double(), b.double(), 1, 1) + r.double()
+    (ref * dy.double()).sum().backward()
+    assert _rel(y.detach().cpu(), ref.detach()) < 3e-5
+    assert _rel(xd.grad.cpu(), x64.grad) < 3e-5
+
+
 def test_conv3x3_batch_above_2gib_runs_in_chunks(all_shapes):
     """An input above 2 GiB (the kernels' 32-bit buffer offsets; the SDXL VAE at 1024², batch 8)
     runs as batch chunks: same result as MIOpen (fp32) over the whole batch, bias and residual
