@@ -196,6 +196,14 @@ int skp_attn_fwd(const float* Q, const float* K, const float* V, float* O, float
 int skp_attn_bwd_flash(const float* Q, const float* K, const float* V, const float* dO, const float* stats,
                        const float* D, float* dS, float* dV, float* dK, int BH, int S, int L, int d, float scale,
                        void* stream);
+/* LayerNorm over the last dimension (the UNet transformer blocks' norm1/2/3; frozen γ, β):
+ * x, y (rows, C), C a multiple of 4 ≤ 2048; stats (rows, 2) = (mean, 1/sqrt(var + eps)) for the
+ * backward, which gives dx = rstd·(dy·γ − mean(dy·γ) − x̂·mean(dy·γ·x̂)).  Replaces
+ * torch.nn.LayerNorm inside diffusers' BasicTransformerBlock (attention.py).               */
+int skp_layernorm_fwd(const float* x, const float* gamma, const float* beta, long long rows, int C, float eps, float* y,
+                      float* stats, void* stream);
+int skp_layernorm_bwd(const float* x, const float* dy, const float* gamma, const float* stats, long long rows, int C,
+                      float* dx, void* stream);
 /* diffusers GEGLU (the UNet FeedForward's proj → chunk(2) → x·gelu(gate), exact-erf GELU):
  * h (rows, 2I) → out (rows, I), and its backward dh (rows, 2I) from dout (rows, I).
  * I % 4 == 0, 16-byte aligned.                                                 */

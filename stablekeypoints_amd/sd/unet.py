@@ -38,6 +38,7 @@ class CaptureComplete(Exception):
 # fused softmax backward run on libskp when True (HIP tensors, frozen parameters); False is the
 # plain-torch model (the tests compare the two).
 USE_FUSED_GROUPNORM = True
+USE_SKP_LAYERNORM = os.environ.get("SKP_LN", "1") != "0"   # A/B switch for the LayerNorm kernel
 
 
 def _fused(x, *modules):
@@ -52,6 +53,15 @@ def _conv_in(conv, x):
         from .. import ops
         return ops.conv3x3(x, conv.weight, conv.bias)
     return conv(x)
+
+
+def _ln(norm, x):
+    """nn.LayerNorm ``norm`` on x: the libskp kernel on the HIP device (frozen affine
+    parameters), elsewhere plain torch."""
+    if USE_SKP_LAYERNORM and _fused(x, norm):
+        from .. import ops
+        return ops.layer_norm(x, norm.weight, norm.bias, norm.eps)
+    return norm(x)
 
 
 def gn_act(norm, x, act, shift=None):
@@ -178,9 +188,9 @@ class BasicTransformerBlock(nn.Module):
         self.norm3 = nn.LayerNorm(dim)
 
     def forward(self, h, context=None):
-        h = self.attn1(self.norm1(h)) + h
-        h = self.attn2(self.norm2(h), context=context) + h
-        h = self.ff(self.norm3(h)) + h
+        h = self.attn1(_ln(self.norm1, h)) + h
+        h = self.attn2(_ln(self.norm2, h), context=context) + h
+        h = self.ff(_ln(self.norm3, h)) + h
         return h
 
 

@@ -547,6 +547,30 @@ def test_flash_attention_vs_math_and_fp64(monkeypatch, BH, S, L, D, q_grad):
         assert (res[True][i] - res[False][i]).abs().max().item() < tol
 
 
+@pytest.mark.parametrize("shape", [(8, 4096, 320), (8, 1024, 640), (3, 85, 1280), (5, 2048), (7, 12), (2, 3, 4),
+                                   (1, 1, 1024)])
+def test_layer_norm_vs_fp64(monkeypatch, shape):
+    """ops.layer_norm (skp_layernorm_fwd/bwd, one wave per row) vs fp64 autograd of
+    F.layer_norm: output within 2e-6 of its scale, input gradient within 1e-5 (rows of 4 to
+    2048 floats, row counts not a multiple of the 4 rows per block)."""
+    from stablekeypoints_amd import ops
+    monkeypatch.setattr(ops, "LN_MIN_ROWS", 1)
+    g = torch.Generator().manual_seed(sum(shape))
+    C = shape[-1]
+    x = (torch.randn(*shape, generator=g) * 3 + 1).to(DEV).requires_grad_(True)
+    w = torch.randn(C, generator=g).to(DEV)
+    b = torch.randn(C, generator=g).to(DEV)
+    dy = torch.randn(*shape, generator=g).to(DEV)
+    y = ops.layer_norm(x, w, b, 1e-5)
+    assert y.grad_fn.__class__.__name__ == "LayerNormFnBackward"
+    (y * dy).sum().backward()
+    xd = x.detach().double().requires_grad_(True)
+    ref = torch.nn.functional.layer_norm(xd, (C,), w.double(), b.double(), 1e-5)
+    (ref * dy.double()).sum().backward()
+    assert (y.double() - ref).abs().max().item() < 2e-6 * max(1.0, ref.abs().max().item())
+    assert (x.grad.double() - xd.grad).abs().max().item() < 1e-5 * max(1.0, xd.grad.abs().max().item())
+
+
 @pytest.mark.parametrize("rows,cols", [(64, 4096), (33, 500), (128, 1024), (7, 77), (5, 16384), (9, 12)])
 def test_softmax_fwd_in_place_vs_torch(rows, cols):
     """skp_softmax_fwd (in place) vs torch.softmax: within 2 ulp-level (1e-6 relative to the row
