@@ -279,7 +279,14 @@ class Downsample2D(nn.Module):
 
     def forward(self, x):
         if self.padding == 0:
-            x = F.pad(x, (0, 1, 0, 1), mode="constant", value=0)
+            # F.pad(x, (0, 1, 0, 1)) without F.pad's zero fill of the whole output (the VAE's
+            # 512² / 256² levels: a 1 GB fill per step): copy x, zero only the new row and column
+            B, C, H, W = x.shape
+            xp = x.new_empty(B, C, H + 1, W + 1)
+            xp[:, :, :H, :W] = x
+            xp[:, :, H, :].zero_()
+            xp[:, :, :H, W].zero_()
+            x = xp
         return self.conv(x)
 
 

@@ -48,3 +48,21 @@ def test_ops_refuse_cpu_tensors():
     from stablekeypoints_amd import ops
     with pytest.raises(ValueError, match="no CPU fallback"):
         ops.find_max_pixel(torch.zeros(2, 4, 4))
+
+
+def test_vae_downsample_edge_pad_equals_f_pad():
+    """Downsample2D(padding=0) pads with a copy + edge zeroing instead of F.pad's full fill:
+    same output and input gradient as F.pad(x, (0, 1, 0, 1)) + the stride-2 conv (host logic)."""
+    import torch
+    import torch.nn.functional as F
+    from stablekeypoints_amd.sd.unet import Downsample2D
+    torch.manual_seed(0)
+    m = Downsample2D(6, padding=0)
+    x = torch.randn(2, 6, 10, 12, requires_grad=True)
+    y = m(x)
+    y.sum().backward()
+    g = x.grad.clone()
+    x.grad = None
+    ref = m.conv(F.pad(x, (0, 1, 0, 1)))
+    ref.sum().backward()
+    assert torch.equal(y, ref) and torch.equal(g, x.grad)
