@@ -41,6 +41,15 @@ def test_bad_arguments_rejected_without_gpu():
     rc = L.skp_fps(ctypes.c_void_p(16), 10, 8, 8, ctypes.c_void_p(16), 1, 4, ctypes.c_void_p(16), None,
                    ctypes.c_void_p(16), None)
     assert rc == -1 and b"two candidates" in L.skp_last_error()
+    a = ctypes.c_void_p(256)   # aligned non-null dummies: every check below fails before any HIP call
+    rc = L.skp_layernorm_fwd(a, a, a, 4, 6, 1e-5, a, a, None)
+    assert rc == -1 and b"multiple of 4" in L.skp_last_error()
+    rc = L.skp_attn_bwd_flash(a, a, a, a, a, a, a, a, a, 2, 100, 64, 40, 0.1, None)
+    assert rc == -1 and b"multiple of 64" in L.skp_last_error()
+    rc = L.skp_attn_fwd(a, a, a, a, None, 2, 128, 77, 48, 0.1, None)
+    assert rc == -1 and b"head dim" in L.skp_last_error()
+    rc = L.skp_conv3x3_wino(a, a, None, None, a, 2, 64, 48, 8, 8, 1, None, None)
+    assert rc == -1 and b"multiple of 32" in L.skp_last_error()
 
 
 def test_ops_refuse_cpu_tensors():
