@@ -52,6 +52,18 @@ int skp_capture_bwd(const float* z_low, int BH, int s, int N, int R, const float
                     long long sp, long long sn, float gscale, const float* stats, float* dz_low, float* workspace,
                     void* stream);
 
+/* Fused capture + per-image aggregate: the capture branch (ptp_utils.py:508-538) of L
+ * layers followed by collect_maps' mean over layers and heads (optimize.py:27-79), per image,
+ * with no (B·H, R², N) attention in memory:
+ *   maps[b, n, p] = (1/(L·H)) Σ_l Σ_h softmax_n(bicubic_{s_l->R}(z_l[b·H + h, :, n])[p]).
+ * z_low: host array of L device pointers, layer l (B·H, s_l², N), 16-B aligned when N % 4 == 0;
+ * sizes: host array of the L s_l (1 <= s_l <= R); maps (B, N, R*R).
+ * stats: NULL or a host array of L device pointers (entries may be NULL), layer l
+ * (B·H, R*R, 2) receiving each pixel's softmax (max, 1/Σexp) exactly as skp_capture_fwd's
+ * `stats`, for skp_capture_bwd.                                                   */
+int skp_capture_maps_fwd(const float* const* z_low, const int* sizes, int L, int B, int H, int N, int R, float* maps,
+                         float* const* stats, void* stream);
+
 /* ---------------------------------------------------------------- A3 aggregate
  * optimize.collect_maps (optimize.py:27-79), token-major output:
  * out[m, p] = (1/(L·BH)) Σ_l Σ_b attn_l[b, p, idx(m)], idx = indices[m] or m.

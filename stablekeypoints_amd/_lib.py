@@ -19,6 +19,8 @@ _SIGS = {
     "skp_capture_fwd": [_p, _c_int, _c_int, _c_int, _c_int, _p, _p, _p],
     "skp_capture_bwd": [_p, _c_int, _c_int, _c_int, _c_int, _p, _c_int, _c_ll, _c_ll, _c_ll, _c_float, _p, _p, _p,
                         _p],
+    "skp_capture_maps_fwd": [ctypes.POINTER(_p), ctypes.POINTER(_c_int), _c_int, _c_int, _c_int, _c_int, _c_int, _p,
+                             ctypes.POINTER(_p), _p],
     "skp_aggregate": [ctypes.POINTER(_p), _c_int, _c_int, _c_int, _c_int, _p, _c_int, _p, _p],
     "skp_resize_bilinear": [_p, _c_int, _c_int, _c_int, _p, _p],
     "skp_resize_bilinear_bwd": [_p, _c_int, _c_int, _c_int, _p, _p],

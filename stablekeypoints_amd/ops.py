@@ -176,14 +176,25 @@ def aggregate(layers, indices=None, upsample_res=-1):
     return _Aggregate.apply(indices, int(upsample_res), *layers)
 
 
+FUSED_MAPS = os.environ.get("SKP_FUSED_MAPS", "1") != "0"   # A/B: 0 = skp_capture_fwd + skp_aggregate
+
+
+def capture_maps_bytes(B, H, N, R, sizes):
+    """Algorithmic HBM bytes of one skp_capture_maps_fwd launch: every z_low read once, the
+    (B, N, R²) maps and the (B·H, R², 2) per-layer stats written once."""
+    RR = R * R
+    return 4 * (sum(B * H * s * s * N for s in sizes) + B * N * RR + len(sizes) * B * H * RR * 2)
+
+
 class CaptureMaps(torch.autograd.Function):
     """Per-image maps straight from the captured layers' logits (fused capture + aggregate).
 
     zs[l]: (B·H, s_l², N) logits of captured layer l.  Output (B, N, R, R):
     map[b] = mean over layers and the H heads of image b of softmax(bicubic(z)).
-    The (B·H, R², N) attention is produced into scratch and reduced (skp_capture_fwd +
-    skp_aggregate), never saved; the backward hands each layer's kernel the per-image map
-    gradient as a broadcast (group = H), so no (B·H, R², N) gradient is materialised.
+    One launch of skp_capture_maps_fwd: the (B·H, R², N) attention is never written; only the
+    per-pixel softmax stats are kept for the backward, which hands each layer's kernel the
+    per-image map gradient as a broadcast (group = H), so no (B·H, R², N) gradient is
+    materialised either.
     """
 
     @staticmethod
@@ -194,20 +205,28 @@ class CaptureMaps(torch.autograd.Function):
         L = len(zs)
         dev = zs[0].device
         RR = R * R
-        attn = [torch.empty(BH, RR, N, device=dev, dtype=F32) for _ in range(L)]
         # per-pixel softmax (max, 1/Σ) of every layer, kept for the backward (8 B per pixel-head)
         stats = [torch.empty(BH, RR, 2, device=dev, dtype=F32) for _ in range(L)]
-        for z, a, st, s in zip(zs, attn, stats, sizes):
-            with _timed("skp_capture_fwd", (BH * RR * N + BH * s * s * N) * 4):
-                call("skp_capture_fwd", ptr(z), BH, s, N, R, ptr(a), ptr(st), stream(dev))
         out = torch.empty(B, N, R, R, device=dev, dtype=F32)
-        for b in range(B):
-            off = b * H * RR * N * 4
-            arr = (ctypes.c_void_p * L)(*[a.data_ptr() + off for a in attn])
-            with _timed("skp_aggregate", (L * H * RR * N + N * RR) * 4):
-                call("skp_aggregate", ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)), L, H, RR, N, None, N,
-                     ptr(out[b]), stream(dev))
-        del attn
+        if FUSED_MAPS:
+            zp = (ctypes.c_void_p * L)(*[z.data_ptr() for z in zs])
+            sp = (ctypes.c_int * L)(*[int(s) for s in sizes])
+            stp = (ctypes.c_void_p * L)(*[st.data_ptr() for st in stats])
+            with _timed("skp_capture_maps_fwd", capture_maps_bytes(B, H, N, R, sizes)):
+                call("skp_capture_maps_fwd", ctypes.cast(zp, ctypes.POINTER(ctypes.c_void_p)), sp, L, B, H, N, R,
+                     ptr(out), ctypes.cast(stp, ctypes.POINTER(ctypes.c_void_p)), stream(dev))
+        else:
+            attn = [torch.empty(BH, RR, N, device=dev, dtype=F32) for _ in range(L)]
+            for z, a, st, s in zip(zs, attn, stats, sizes):
+                with _timed("skp_capture_fwd", (BH * RR * N + BH * s * s * N) * 4):
+                    call("skp_capture_fwd", ptr(z), BH, s, N, R, ptr(a), ptr(st), stream(dev))
+            for b in range(B):
+                off = b * H * RR * N * 4
+                arr = (ctypes.c_void_p * L)(*[a.data_ptr() + off for a in attn])
+                with _timed("skp_aggregate", (L * H * RR * N + N * RR) * 4):
+                    call("skp_aggregate", ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)), L, H, RR, N, None, N,
+                         ptr(out[b]), stream(dev))
+            del attn
         ctx.save_for_backward(*zs, *stats)
         ctx.meta = (B, H, R, N, list(sizes))
         return out

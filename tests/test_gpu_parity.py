@@ -327,6 +327,86 @@ def test_capture_maps_per_image_fwd_bwd():
         assert np.abs(N(zt[i].grad) - ref).max() < 1e-4 * max(1.0, np.abs(ref).max())
 
 
+def _capture_maps_abi(zs, sizes, B, H, R, with_stats=True):
+    """skp_capture_maps_fwd through the C ABI: maps (B, N, R, R) and per-layer stats."""
+    import ctypes
+    from stablekeypoints_amd._lib import call, ptr, stream
+    L = len(zs)
+    Nn = zs[0].shape[-1]
+    maps = torch.full((B, Nn, R, R), float("nan"), device=DEV)
+    stats = [torch.full((B * H, R * R, 2), float("nan"), device=DEV) for _ in range(L)]
+    zp = (ctypes.c_void_p * L)(*[z.data_ptr() for z in zs])
+    sp = (ctypes.c_int * L)(*sizes)
+    stp = (ctypes.c_void_p * L)(*[st.data_ptr() for st in stats])
+    call("skp_capture_maps_fwd", ctypes.cast(zp, ctypes.POINTER(ctypes.c_void_p)), sp, L, B, H, Nn, R, ptr(maps),
+         ctypes.cast(stp, ctypes.POINTER(ctypes.c_void_p)) if with_stats else None, stream(zs[0].device))
+    torch.cuda.synchronize()
+    return maps, stats
+
+
+@pytest.mark.parametrize("B,H,sizes,R,Nn", [(2, 8, (4, 4, 4, 8), 32, 40), (1, 3, (5, 3), 40, 37), (2, 2, (16, 32), 128, 1),
+                                            (1, 2, (8,), 32, 1000), (3, 1, (1, 2), 8, 130), (1, 8, (16, 16, 16, 32), 128, 500),
+                                            (1, 4, (7, 13), 100, 256), (1, 2, (6,), 72, 129)])
+def test_capture_maps_fwd_vs_oracle(B, H, sizes, R, Nn):
+    """skp_capture_maps_fwd (fused capture + per-image layer/head mean) vs the oracle's
+    capture_fwd + collect_maps per image (ptp_utils.py:508-538, optimize.py:27-79): maps within
+    1e-6 absolute, every stats entry (row max, 1/Σ) within fp32 rounding of the oracle's row."""
+    zs = [recipes.random_logits(300 + 7 * i + Nn, (B * H, s * s, Nn), scale=2.0) for i, s in enumerate(sizes)]
+    maps, stats = _capture_maps_abi([T(z) for z in zs], list(sizes), B, H, R)
+    m = N(maps)
+    assert np.isfinite(m).all()
+    for b in range(B):
+        attn = [O.capture_fwd(z[b * H:(b + 1) * H], s, R) for z, s in zip(zs, sizes)]
+        ref = O.collect_maps(attn)
+        assert np.abs(m[b] - ref).max() < 1e-6, (b, np.abs(m[b] - ref).max())
+    for z, s, st in zip(zs, sizes, stats):
+        zu = O.resize(z.reshape(B * H, s, s, Nn).transpose(0, 3, 1, 2), R, "bicubic")
+        zu = zu.transpose(0, 2, 3, 1).reshape(B * H, R * R, Nn).astype(np.float64)
+        st = N(st).astype(np.float64)
+        zmax = zu.max(-1)
+        assert (np.abs(st[..., 0] - zmax) / np.maximum(1.0, np.abs(zmax))).max() < 4e-6   # fp32 rounding
+        assert np.abs(st[..., 1] * np.exp(zu - st[..., :1]).sum(-1) - 1).max() < 2e-5
+
+
+def test_capture_maps_fwd_equals_two_kernel_path_full_size():
+    """At the bench shape (B=8 images × 8 heads, s = 16,16,16,32, R=128, N=500) the fused launch
+    equals skp_capture_fwd + skp_aggregate per image (the r01 path, itself oracle-pinned) to
+    1e-7 on the maps and to fp32 rounding on the stats; the backward fed with either stats agrees."""
+    import ctypes
+    from stablekeypoints_amd import ops
+    from stablekeypoints_amd._lib import call, ptr, stream
+    B, H, R, Nn, sizes = 8, 8, 128, 500, (16, 16, 16, 32)
+    g = torch.Generator().manual_seed(5)
+    zs = [(torch.randn(B * H, s * s, Nn, generator=g) * 3).to(DEV) for s in sizes]
+    maps, stats = _capture_maps_abi(zs, list(sizes), B, H, R)
+    RR = R * R
+    ref = torch.empty(B, Nn, R, R, device=DEV)
+    attn = []
+    for z, s in zip(zs, sizes):
+        a = torch.empty(B * H, RR, Nn, device=DEV)
+        st = torch.empty(B * H, RR, 2, device=DEV)
+        call("skp_capture_fwd", ptr(z), B * H, s, Nn, R, ptr(a), ptr(st), stream(z.device))
+        attn.append((a, st))
+    for b in range(B):
+        arr = (ctypes.c_void_p * 4)(*[a.data_ptr() + b * H * RR * Nn * 4 for a, _ in attn])
+        call("skp_aggregate", ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)), 4, H, RR, Nn, None, Nn, ptr(ref[b]),
+             stream(DEV))
+    torch.cuda.synchronize()
+    d = (maps - ref).abs().max().item()
+    print(f"\nfused vs two-kernel maps: max|Δ| {d:.2e} (max {ref.max().item():.3e})")
+    assert d < 1e-7
+    for (a, st_ref), st in zip(attn, stats):
+        # the row max of the same bicubic values, summed with and without FMA contraction
+        assert ((st[..., 0] - st_ref[..., 0]).abs() / st_ref[..., 0].abs().clamp(min=1)).max().item() < 2e-6
+        assert ((st[..., 1] - st_ref[..., 1]).abs() / st_ref[..., 1]).max().item() < 1e-5   # exp2 vs __expf, Σ order
+    del attn
+    gmap = torch.randn(B, Nn, R, R, generator=g).to(DEV)
+    for z, s, st in zip(zs[:1], sizes, stats):
+        d0 = ops.capture_bwd(z, s, R, gmap, gscale=1 / 32, group=H, strides=(Nn * RR, 1, RR))
+        d1 = ops.capture_bwd(z, s, R, gmap, gscale=1 / 32, group=H, strides=(Nn * RR, 1, RR), stats=st)
+        assert (d1 - d0).abs().max().item() < 1e-5 * max(1.0, d0.abs().max().item())
+
+
 def test_batched_captures_match_sequential_tiny():
     """TokenOptimizer: one B=2 pass (LogitStore, fused maps) == the reference's two passes."""
     from stablekeypoints_amd import ptp_utils

@@ -67,6 +67,14 @@ def main():
                 call("skp_capture_fwd", ptr(zb2[sz]), 2 * H, sz, N, R, ptr(scratch), ptr(st), stream(dev))
                 del scratch
             res[name] = timed(lambda: ops.capture_bwd(zb2[sz], sz, R, gmap, 0.03125, H, bstr, stats=st), args.iters)
+        elif name in ("maps8", "maps8_old"):   # fused capture + per-image aggregate at the bench shape
+            sizes = (16, 16, 16, 32)
+            z8 = [torch.randn(8 * H, s * s, N, device=dev, generator=g) * 2 for s in sizes]
+            ops.FUSED_MAPS = name == "maps8"
+            with torch.no_grad():
+                res[name] = timed(lambda: ops.capture_maps(z8, sizes, 8, R), args.iters)
+            ops.FUSED_MAPS = True
+            del z8
         elif name == "sum1g":   # read-bandwidth reference: torch reduction over a fresh 1 GiB tensor
             big = torch.empty(256 * 1024 * 1024, device=dev).normal_()
             res[name] = timed(lambda: big.sum(), args.iters)
