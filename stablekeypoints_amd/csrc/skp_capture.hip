@@ -498,14 +498,15 @@ __global__ __launch_bounds__(kColThreads) void capture_bwd_cols_kernel(const flo
 // No (B·H, R², N) attention reaches HBM: HBM sees the z_low reads, the maps write and the
 // per-pixel (max, 1/Σ) stats the backward reuses.
 //
-// One 512-thread workgroup owns P consecutive pixels of output row y of image b and loops over
-// every (layer, head).  Per (l, h): the vertical bicubic pass of the chunk's low-res columns
-// into LDS (V, nc × Np, tokens padded with −1e30 so they exp to 0 with no masking), then each
-// half-wave takes one pixel (32 lanes × QPL token quads): horizontal taps from V, max and Σ by
-// five in-register DPP/permlane steps, and acc += exp(z − m)/Σ in registers.  A wave owns PXW
-// pixels, two at a time, so acc is PXW/2 × QPL float4 per lane.  After the last (l, h) the
-// (pixel, token) accumulators go token-major through an LDS tile, 128 tokens per round, as
-// coalesced runs of P pixels.
+// One workgroup (WAVES waves) owns P consecutive pixels of output row y of image b and loops
+// over every (layer, head).  Per (l, h): the vertical bicubic pass of the chunk's low-res
+// columns into LDS (V, nc × Np, tokens padded with −1e30 so they exp to 0 with no masking),
+// then each 16-lane row of a wave takes one pixel (lanes own QPL token quads): horizontal taps
+// from V (ds_read_b128; the four rows' quads fall in disjoint banks), max and Σ by four
+// single-instruction DPP steps inside the row, and acc += exp(z − m)·(1/Σ) in registers on
+// the packed f32 VALU.  A wave owns PXW pixels, four at a time, so acc is PXW/4 × QPL float4 per
+// lane.  After the last (l, h) the (pixel, token) accumulators go token-major through an LDS
+// tile, 128 tokens per round, as coalesced runs of P pixels.
 // Blocks are mapped XCD-major: block k runs on XCD k % 8 and takes job (k % 8)·⌈jobs/8⌉ + k / 8,
 // so each XCD walks consecutive rows of one image and its L2 serves their shared z_low rows.
 constexpr float kPadLogit = -1e30f;   // Σ taps ≈ 1, so padded tokens interpolate to ≈ −1e30
@@ -517,36 +518,53 @@ struct CapLayers {
   int s[SKP_MAX_LAYERS];
 };
 
-template <class Op>
-__device__ __forceinline__ float half_reduce(float v, Op op) {   // over each 32-lane half
-  v = op(v, dpp_read<0xB1>(v));
-  v = op(v, dpp_read<0x4E>(v));
-  v = op(v, dpp_read<0x141>(v));
-  v = op(v, dpp_read<0x140>(v));
-  float w = v;
-  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(v), "+v"(w));
-  return op(v, w);
+// max / sum over each 16-lane row: four DPP steps, each one VALU op with the DPP source
+// (no mov + canonicalise); `s_nop 1` covers the VALU-write -> DPP-read hazard of the chain.
+__device__ __forceinline__ float row16_max(float v) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_max_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_max_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_max_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_max_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf"
+      : "+v"(v));
+  return v;
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_add_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_add_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_add_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_add_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf"
+      : "+v"(v));
+  return v;
 }
 
-constexpr int maps_pxw(int qpl) {   // pixels per wave: acc = PXW/2 · QPL float4 = 32 VGPRs
-  return (16 / qpl) < 2 ? 2 : ((16 / qpl) > 16 ? 16 : 16 / qpl);
-}
+// pixels per wave (a multiple of 4): acc = PXW/4 · QPL float4 = 32 VGPRs where possible
+constexpr int maps_pxw(int qpl) { return (32 / qpl) < 4 ? 4 : ((32 / qpl) > 16 ? 16 : 32 / qpl); }
 
 template <int QPL, int WAVES>
 __global__ __launch_bounds__(WAVES * WAVE) __attribute__((amdgpu_waves_per_eu(4)))
-void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nchunks, float count,
+void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nchunks, int vstride, float count,
                          float* __restrict__ maps) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int kMapThreads = WAVES * WAVE;
   constexpr int PXW = maps_pxw(QPL);
-  constexpr int G = PXW / 2;                 // pixel pairs per wave
+  constexpr int G = PXW / 4;                 // pixel quadruples per wave
   constexpr int P = WAVES * PXW;             // pixels per workgroup
-  constexpr int Np = 128 * QPL;              // padded tokens
+  constexpr int Np = 64 * QPL;               // padded tokens (16 lanes × QPL quads)
   constexpr int Npq = Np / 4;
   constexpr float L2E = 1.4426950408889634f;
-  float4* TW = reinterpret_cast<float4*>(lds);             // P tap weights
-  int4* TI = reinterpret_cast<int4*>(lds + 4 * P);          // P tap columns relative to c0
-  float* V = lds + 8 * P;                                   // nc × Np (later: the store tile)
+  float4* TW = reinterpret_cast<float4*>(lds);             // [2][P] tap weights (by layer parity)
+  int4* TI = reinterpret_cast<int4*>(lds + 8 * P);          // [2][P] tap offsets (column − c0) · Npq
+  float* V = lds + 16 * P;                                  // [2][vstride] vertical passes (then the store tile)
 
   const int total = B * R * nchunks;
   const int per = (total + 7) / 8;
@@ -559,7 +577,7 @@ void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nc
   const int np = min(P, R - x0);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int half = lane >> 5, li = lane & 31;
+  const int row = lane >> 4, li = lane & 15;
   f4 acc[G][QPL];
 #pragma unroll
   for (int g = 0; g < G; ++g)
@@ -567,126 +585,168 @@ void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nc
     for (int c = 0; c < QPL; ++c) acc[g][c] = (f4)0.0f;
 
   const bool vec = (N & 3) == 0;
-  for (int l = 0; l < L; ++l) {
-    const int s = cl.s[l];
-    const Taps4 ty = bicubic_taps(y, s, R);
-    const int c0 = max(bicubic_taps(x0, s, R).lo, 0);
-    const int c1 = min(bicubic_taps(x0 + np - 1, s, R).lo + 3, s - 1);
-    const int nc = c1 - c0 + 1;
-    __syncthreads();   // previous layer's TW/TI and V consumed
-    for (int x = tid; x < P; x += kMapThreads) {
-      const Taps4 t = bicubic_taps(x0 + min(x, np - 1), s, R);
-      TW[x] = make_float4(t.w[0], t.w[1], t.w[2], t.w[3]);
-      TI[x] = make_int4(t.i[0] - c0, t.i[1] - c0, t.i[2] - c0, t.i[3] - c0);
+  // Per (layer, head) slab: stage the tap table (first head of a layer) and the vertical pass,
+  // then the pixel work; two workgroups per CU overlap one's staging with the other's pixels.
+  // (A software pipeline with double-buffered V measured slower: 1.03 vs 0.94 ms.)
+  auto layer_cols = [&](int l, int& s, int& c0, int& nc) {
+    s = cl.s[l];
+    c0 = max(bicubic_taps(x0, s, R).lo, 0);
+    nc = min(bicubic_taps(x0 + np - 1, s, R).lo + 3, s - 1) - c0 + 1;
+  };
+  auto stage = [&](int it) {   // tap table (first head of a layer) + vertical pass of slab it
+    const int l = it / H, h = it - l * H;
+    int s, c0, nc;
+    layer_cols(l, s, c0, nc);
+    const int buf = it & 1;
+    if (h == 0) {
+      float4* tw = TW + (l & 1) * P;
+      int4* tiw = TI + (l & 1) * P;
+      for (int x = tid; x < P; x += kMapThreads) {
+        const Taps4 t = bicubic_taps(x0 + min(x, np - 1), s, R);
+        tw[x] = make_float4(t.w[0], t.w[1], t.w[2], t.w[3]);
+        tiw[x] = make_int4((t.i[0] - c0) * Npq, (t.i[1] - c0) * Npq, (t.i[2] - c0) * Npq, (t.i[3] - c0) * Npq);
+      }
     }
-    for (int h = 0; h < H; ++h) {
-      const int bh = b * H + h;
-      const float* zb = cl.z[l] + (size_t)bh * s * s * N;
-      if (h > 0) __syncthreads();   // V of the previous head consumed
-      // vertical pass: V[jj][n] = Σ_k wy_k · z[iy_k][c0 + jj][n]
-      if (vec) {
-        const float4* r0 = reinterpret_cast<const float4*>(zb + ((size_t)ty.i[0] * s + c0) * N);
-        const float4* r1 = reinterpret_cast<const float4*>(zb + ((size_t)ty.i[1] * s + c0) * N);
-        const float4* r2 = reinterpret_cast<const float4*>(zb + ((size_t)ty.i[2] * s + c0) * N);
-        const float4* r3 = reinterpret_cast<const float4*>(zb + ((size_t)ty.i[3] * s + c0) * N);
-        const int nq = N >> 2;
-        float4* V4 = reinterpret_cast<float4*>(V);
-#pragma unroll 1
-        for (int e = tid; e < nc * Npq; e += kMapThreads) {
+    const Taps4 ty = bicubic_taps(y, s, R);
+    const float* zb = cl.z[l] + (size_t)(b * H + h) * s * s * N;
+    float* Vb = V + buf * vstride;
+    // V[jj][n] = Σ_k wy_k · z[iy_k][c0 + jj][n]
+    if (vec) {
+      const f4* r0 = reinterpret_cast<const f4*>(zb + ((size_t)ty.i[0] * s + c0) * N);
+      const f4* r1 = reinterpret_cast<const f4*>(zb + ((size_t)ty.i[1] * s + c0) * N);
+      const f4* r2 = reinterpret_cast<const f4*>(zb + ((size_t)ty.i[2] * s + c0) * N);
+      const f4* r3 = reinterpret_cast<const f4*>(zb + ((size_t)ty.i[3] * s + c0) * N);
+      const int nq = N >> 2;
+      f4* V4 = reinterpret_cast<f4*>(Vb);
+      // up to VPT outputs per thread with all 4·VPT loads in flight before the first FMA
+#ifndef SKP_MAPS_VPT
+#define SKP_MAPS_VPT 1   // vertical outputs per thread per batch (2, 3 measured 1-2% slower)
+#endif
+      constexpr int VPT = SKP_MAPS_VPT;
+      const int tot = nc * Npq;
+      for (int e0 = tid; e0 < tot; e0 += VPT * kMapThreads) {
+        f4 a[VPT][4];
+#pragma unroll
+        for (int k = 0; k < VPT; ++k) {
+          const int e = e0 + k * kMapThreads;
           const int jj = e / Npq, q = e - jj * Npq;
-          float4 v = make_float4(kPadLogit, kPadLogit, kPadLogit, kPadLogit);
-          if (q < nq) {
-            const size_t o = (size_t)jj * nq + q;
-            const float4 a0 = r0[o], a1 = r1[o], a2 = r2[o], a3 = r3[o];
-            v.x = ty.w[0] * a0.x + ty.w[1] * a1.x + ty.w[2] * a2.x + ty.w[3] * a3.x;
-            v.y = ty.w[0] * a0.y + ty.w[1] * a1.y + ty.w[2] * a2.y + ty.w[3] * a3.y;
-            v.z = ty.w[0] * a0.z + ty.w[1] * a1.z + ty.w[2] * a2.z + ty.w[3] * a3.z;
-            v.w = ty.w[0] * a0.w + ty.w[1] * a1.w + ty.w[2] * a2.w + ty.w[3] * a3.w;
+          if (e < tot && q < nq) {
+            const int o = jj * nq + q;
+            a[k][0] = r0[o];
+            a[k][1] = r1[o];
+            a[k][2] = r2[o];
+            a[k][3] = r3[o];
           }
-          V4[e] = v;
         }
-      } else {
+#pragma unroll
+        for (int k = 0; k < VPT; ++k) {
+          const int e = e0 + k * kMapThreads;
+          const int jj = e / Npq, q = e - jj * Npq;
+          if (e < tot) {
+            f4 v = (f4)kPadLogit;
+            if (q < nq) {
+              v = a[k][0] * ty.w[0];
+              v = __builtin_elementwise_fma(a[k][1], (f4)ty.w[1], v);
+              v = __builtin_elementwise_fma(a[k][2], (f4)ty.w[2], v);
+              v = __builtin_elementwise_fma(a[k][3], (f4)ty.w[3], v);
+            }
+            V4[e] = v;
+          }
+        }
+      }
+    } else {
 #pragma unroll 1
-        for (int e = tid; e < nc * Np; e += kMapThreads) {
-          const int jj = e / Np, n = e - jj * Np;
-          float v = kPadLogit;
-          if (n < N) {
-            const int j = c0 + jj;
-            v = ty.w[0] * zb[((size_t)ty.i[0] * s + j) * N + n];
-            v += ty.w[1] * zb[((size_t)ty.i[1] * s + j) * N + n];
-            v += ty.w[2] * zb[((size_t)ty.i[2] * s + j) * N + n];
-            v += ty.w[3] * zb[((size_t)ty.i[3] * s + j) * N + n];
-          }
-          V[e] = v;
+      for (int e = tid; e < nc * Np; e += kMapThreads) {
+        const int jj = e / Np, n = e - jj * Np;
+        float v = kPadLogit;
+        if (n < N) {
+          const int j = c0 + jj;
+          v = ty.w[0] * zb[((size_t)ty.i[0] * s + j) * N + n];
+          v += ty.w[1] * zb[((size_t)ty.i[1] * s + j) * N + n];
+          v += ty.w[2] * zb[((size_t)ty.i[2] * s + j) * N + n];
+          v += ty.w[3] * zb[((size_t)ty.i[3] * s + j) * N + n];
         }
+        Vb[e] = v;
       }
-      __syncthreads();
-      const f4* V4 = reinterpret_cast<const f4*>(V);
-      float2* st = cl.stats[l];
+    }
+  };
+  const int nslab = L * H;
+  for (int it = 0; it < nslab; ++it) {
+    if (it > 0) __syncthreads();   // V (and at a layer change the tap table) of slab it − 1 consumed
+    stage(it);
+    __syncthreads();
+    const int l = it / H, bh = b * H + (it - l * H);
+    const f4* V4 = reinterpret_cast<const f4*>(V + (it & 1) * vstride) + li;
+    const float4* tw = TW + (l & 1) * P;
+    const int4* tiw = TI + (l & 1) * P;
+    float2* st = cl.stats[l];
 #pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const int xl = wid * PXW + 2 * g + half;             // pixel of this half-wave
-        const int xr = min(xl, np - 1);                        // past-the-edge halves redo a valid one
-        const float4 w = TW[xr];
-        const int4 ti = TI[xr];
-        f4 zc[QPL];
-        f4 mv = {kPadLogit, kPadLogit, kPadLogit, kPadLogit};
+    for (int g = 0; g < G; ++g) {
+      const int xl = wid * PXW + 4 * g + row;              // pixel of this 16-lane row
+      const int xr = min(xl, np - 1);                        // past-the-edge rows redo a valid one
+      const float4 w = tw[xr];
+      const int4 ti = tiw[xr];
+      f4 zc[QPL];
+      float m = kPadLogit;
 #pragma unroll
-        for (int c = 0; c < QPL; ++c) {
-          const int q = c * 32 + li;
-          const f4 a0 = V4[ti.x * Npq + q], a1 = V4[ti.y * Npq + q];
-          const f4 a2 = V4[ti.z * Npq + q], a3 = V4[ti.w * Npq + q];
-          // token pairs on the packed f32 VALU: z = ((w0·a0 + w1·a1) + w2·a2) + w3·a3
-          f4 v = a0 * w.x;
-          v = __builtin_elementwise_fma(a1, (f4)w.y, v);
-          v = __builtin_elementwise_fma(a2, (f4)w.z, v);
-          v = __builtin_elementwise_fma(a3, (f4)w.w, v);
-          zc[c] = v;
-          mv = __builtin_elementwise_max(mv, v);
-          if (c & 1) __builtin_amdgcn_sched_barrier(0);   // two quads of LDS reads in flight (registers)
-        }
-        float m = fmaxf(fmaxf(mv.x, mv.y), fmaxf(mv.z, mv.w));
-        m = half_reduce(m, [](float a, float b2) { return fmaxf(a, b2); });
-        const f4 mb = (f4)(-m * L2E);
-        f4 sv = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int c = 0; c < QPL; ++c) {
-          f4 t = __builtin_elementwise_fma(zc[c], (f4)L2E, mb);
-          t.x = __builtin_amdgcn_exp2f(t.x);
-          t.y = __builtin_amdgcn_exp2f(t.y);
-          t.z = __builtin_amdgcn_exp2f(t.z);
-          t.w = __builtin_amdgcn_exp2f(t.w);
-          zc[c] = t;
-          sv += t;
-        }
-        float ssum = (sv.x + sv.y) + (sv.z + sv.w);
-        ssum = half_reduce(ssum, [](float a, float b2) { return a + b2; });
-        const float inv = 1.0f / ssum;
-#pragma unroll
-        for (int c = 0; c < QPL; ++c) acc[g][c] = __builtin_elementwise_fma(zc[c], (f4)inv, acc[g][c]);
-        if (st && li == 0 && xl < np) st[((size_t)bh * R + y) * R + x0 + xl] = make_float2(m, inv);
-        __builtin_amdgcn_sched_barrier(0);   // keep the next pixel's LDS reads from being hoisted (registers)
+      for (int c = 0; c < QPL; ++c) {
+        const f4 a0 = V4[ti.x + 16 * c], a1 = V4[ti.y + 16 * c];
+        const f4 a2 = V4[ti.z + 16 * c], a3 = V4[ti.w + 16 * c];
+        // token pairs on the packed f32 VALU: z = ((w0·a0 + w1·a1) + w2·a2) + w3·a3
+        f4 v = a0 * w.x;
+        v = __builtin_elementwise_fma(a1, (f4)w.y, v);
+        v = __builtin_elementwise_fma(a2, (f4)w.z, v);
+        v = __builtin_elementwise_fma(a3, (f4)w.w, v);
+        zc[c] = v;
+        m = __builtin_fmaxf(__builtin_fmaxf(m, v.x), v.y);
+        m = __builtin_fmaxf(__builtin_fmaxf(m, v.z), v.w);
+        if (QPL > 4 || (c & 1)) __builtin_amdgcn_sched_barrier(0);   // bound the LDS reads in flight (registers)
       }
+      m = row16_max(m);
+      const f4 mb = (f4)(-m * L2E);
+      f4 sv = (f4)0.0f;
+#pragma unroll
+      for (int c = 0; c < QPL; ++c) {
+        f4 t = __builtin_elementwise_fma(zc[c], (f4)L2E, mb);
+        t.x = __builtin_amdgcn_exp2f(t.x);
+        t.y = __builtin_amdgcn_exp2f(t.y);
+        t.z = __builtin_amdgcn_exp2f(t.z);
+        t.w = __builtin_amdgcn_exp2f(t.w);
+        zc[c] = t;
+        sv += t;
+      }
+      const float inv = __builtin_amdgcn_rcpf(row16_sum((sv.x + sv.y) + (sv.z + sv.w)));
+#pragma unroll
+      for (int c = 0; c < QPL; ++c) acc[g][c] = __builtin_elementwise_fma(zc[c], (f4)inv, acc[g][c]);
+      if (st && li == 0 && xl < np) st[((size_t)bh * R + y) * R + x0 + xl] = make_float2(m, inv);
+      __builtin_amdgcn_sched_barrier(0);   // keep the next pixels' LDS reads from being hoisted (registers)
     }
   }
-  // token-major store: round c stages tokens [128c, 128c + 128) of all P pixels in LDS
+  // token-major store: round r stages tokens [128r, 128r + 128) of all P pixels in LDS; lane li
+  // of a row holds quads li + 16c, so round r takes c = 2r and 2r + 1
   constexpr int TS = 128 + 4;   // tile row stride (floats): 16-B aligned, b128 reads conflict-free
   float* tile = V;
   float* ob = maps + (size_t)b * N * R * R + (size_t)y * R + x0;
+  const float rc = 1.0f / count;
 #pragma unroll
-  for (int c = 0; c < QPL; ++c) {
+  for (int r = 0; r < (QPL + 1) / 2; ++r) {
     __syncthreads();
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      const int xl = wid * PXW + 2 * g + half;
-      *reinterpret_cast<f4*>(tile + xl * TS + 4 * li) = acc[g][c] / count;
+      const int xl = wid * PXW + 4 * g + row;
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int c = 2 * r + h2;
+        if (c < QPL) *reinterpret_cast<f4*>(tile + xl * TS + 4 * (li + 16 * h2)) = acc[g][c] * rc;
+      }
     }
     __syncthreads();
-    for (int e = tid; e < P * 32; e += kMapThreads) {
+    const int nr = min(128, Np - 128 * r) / 4;   // quads staged this round
+    for (int e = tid; e < P * nr; e += kMapThreads) {
       const int xl = e % P, jq = e / P;
       if (xl >= np) continue;
-      const float4 v = *reinterpret_cast<const float4*>(tile + xl * TS + 4 * jq);
-      const int n = 128 * c + 4 * jq;
+      const f4 v = *reinterpret_cast<const f4*>(tile + xl * TS + 4 * jq);
+      const int n = 128 * r + 4 * jq;
       if (n < N) ob[(size_t)n * R * R + xl] = v.x;
       if (n + 1 < N) ob[(size_t)(n + 1) * R * R + xl] = v.y;
       if (n + 2 < N) ob[(size_t)(n + 2) * R * R + xl] = v.z;
@@ -934,24 +994,30 @@ extern "C" int skp_capture_bwd(const float* z_low, int BH, int s, int N, int R, 
 }
 
 namespace {
-int maps_qpl(int N) {   // float4 quads per lane (32 lanes per pixel): Np = 128·QPL >= N
-  if (N <= 128) return 1;
-  if (N <= 256) return 2;
-  if (N <= 512) return 4;
-  if (N <= 1024) return 8;
+int maps_qpl(int N) {   // float4 quads per lane (16 lanes per pixel): Np = 64·QPL >= N
+  if (N <= 64) return 1;
+  if (N <= 128) return 2;
+  if (N <= 256) return 4;
+  if (N <= 512) return 8;
+  if (N <= 1024) return 16;
   return -1;
 }
 
-size_t maps_lds(const int* sizes, int L, int R, int qpl, int waves) {
+// floats per V buffer: the widest layer's nc × Np, and at least half the store tile (P × 132)
+int maps_vstride(const int* sizes, int L, int R, int qpl, int waves) {
   const int P = waves * maps_pxw(qpl);
-  const int Np = 128 * qpl;
+  const int Np = 64 * qpl;
   int ncmax = 1;
   for (int l = 0; l < L; ++l) {   // columns one P-pixel chunk can touch: ⌈P·s/R⌉ + 4, at most s
     const int s = sizes[l];
     ncmax = std::max(ncmax, std::min(s, (int)(((long long)P * s + R - 1) / R) + 4));
   }
-  const size_t v = (size_t)ncmax * Np, tile = (size_t)P * (128 + 4);
-  return (8 * (size_t)P + std::max(v, tile)) * sizeof(float);
+  const int v = ncmax * Np, tile = P * (128 + 4);
+  return (std::max(v, (tile + 1) / 2) + 3) & ~3;
+}
+
+size_t maps_lds(int vstride, int qpl, int waves) {   // [2][P] taps ×2 + [2][vstride] V
+  return (16 * (size_t)waves * maps_pxw(qpl) + 2 * (size_t)vstride) * sizeof(float);
 }
 
 // workgroup size: 8 waves (two workgroups per CU) unless SKP_MAPS_WAVES=16 (A/B switch)
@@ -964,20 +1030,21 @@ int maps_waves() {
 }
 
 template <int QPL, int WAVES>
-void launch_maps(const CapLayers& cl, int L, int B, int H, int N, int R, size_t lds, float* maps, hipStream_t st) {
+void launch_maps(const CapLayers& cl, int L, int B, int H, int N, int R, int vstride, size_t lds, float* maps,
+                 hipStream_t st) {
   const int P = WAVES * maps_pxw(QPL);
   const int nchunks = (R + P - 1) / P;
   const int total = B * R * nchunks;
   const int grid = 8 * ((total + 7) / 8);
   hipLaunchKernelGGL((capture_maps_kernel<QPL, WAVES>), dim3(grid), dim3(WAVES * WAVE), lds, st, cl, L, B, H, N, R,
-                     nchunks, (float)L * (float)H, maps);
+                     nchunks, vstride, (float)L * (float)H, maps);
 }
 
 template <int QPL>
-void launch_maps_w(int waves, const CapLayers& cl, int L, int B, int H, int N, int R, size_t lds, float* maps,
-                   hipStream_t st) {
-  if (waves == 16) launch_maps<QPL, 16>(cl, L, B, H, N, R, lds, maps, st);
-  else launch_maps<QPL, 8>(cl, L, B, H, N, R, lds, maps, st);
+void launch_maps_w(int waves, const CapLayers& cl, int L, int B, int H, int N, int R, int vstride, size_t lds,
+                   float* maps, hipStream_t st) {
+  if (waves == 16) launch_maps<QPL, 16>(cl, L, B, H, N, R, vstride, lds, maps, st);
+  else launch_maps<QPL, 8>(cl, L, B, H, N, R, vstride, lds, maps, st);
 }
 }  // namespace
 
@@ -1001,14 +1068,16 @@ extern "C" int skp_capture_maps_fwd(const float* const* z_low, const int* sizes,
   }
   SKP_CHECK_ARG(aligned || (N % 4) != 0, "z_low pointers must be 16-B aligned");
   const int waves = maps_waves();
-  const size_t lds = maps_lds(sizes, L, R, qpl, waves);
+  const int vstride = maps_vstride(sizes, L, R, qpl, waves);
+  const size_t lds = maps_lds(vstride, qpl, waves);
   SKP_CHECK_ARG(lds <= 160 * 1024, "s*N too large for LDS");
   hipStream_t st = as_stream(stream);
   switch (qpl) {
-    case 1: launch_maps_w<1>(waves, cl, L, B, H, N, R, lds, maps, st); break;
-    case 2: launch_maps_w<2>(waves, cl, L, B, H, N, R, lds, maps, st); break;
-    case 4: launch_maps_w<4>(waves, cl, L, B, H, N, R, lds, maps, st); break;
-    default: launch_maps_w<8>(waves, cl, L, B, H, N, R, lds, maps, st); break;
+    case 1: launch_maps_w<1>(waves, cl, L, B, H, N, R, vstride, lds, maps, st); break;
+    case 2: launch_maps_w<2>(waves, cl, L, B, H, N, R, vstride, lds, maps, st); break;
+    case 4: launch_maps_w<4>(waves, cl, L, B, H, N, R, vstride, lds, maps, st); break;
+    case 8: launch_maps_w<8>(waves, cl, L, B, H, N, R, vstride, lds, maps, st); break;
+    default: launch_maps_w<16>(waves, cl, L, B, H, N, R, vstride, lds, maps, st); break;
   }
   SKP_LAUNCH_CHECK();
   return SKP_OK;
