@@ -64,6 +64,16 @@ int skp_capture_bwd(const float* z_low, int BH, int s, int N, int R, const float
 int skp_capture_maps_fwd(const float* const* z_low, const int* sizes, int L, int B, int H, int N, int R, float* maps,
                          float* const* stats, void* stream);
 
+/* Backward of skp_capture_maps_fwd for all L layers: dz_low[l] = bicubicᵀ(a ⊙ (g − Σ_n a g))
+ * per (b·H + h) with g = gscale · dmaps[b] (the per-image map gradient broadcast over heads,
+ * gscale = 1/(L·H) for the mean) and a rebuilt from the forward's stats (NULL: recomputed).
+ * dmaps (B, N, R*R) token-major; dz_low: host array of L device pointers, (B·H, s_l², N).
+ * N % 4 == 0.  workspace: B·R²·N + B·H·R·max(s_l)·N floats, 16-B aligned (pixel-major gradient
+ * copy + row partials).  Deterministic (no atomics).                                   */
+int skp_capture_maps_bwd(const float* const* z_low, const int* sizes, int L, int B, int H, int N, int R,
+                         const float* dmaps, float gscale, const float* const* stats, float* const* dz_low,
+                         float* workspace, void* stream);
+
 /* ---------------------------------------------------------------- A3 aggregate
  * optimize.collect_maps (optimize.py:27-79), token-major output:
  * out[m, p] = (1/(L·BH)) Σ_l Σ_b attn_l[b, p, idx(m)], idx = indices[m] or m.

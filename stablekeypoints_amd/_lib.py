@@ -21,6 +21,8 @@ _SIGS = {
                         _p],
     "skp_capture_maps_fwd": [ctypes.POINTER(_p), ctypes.POINTER(_c_int), _c_int, _c_int, _c_int, _c_int, _c_int, _p,
                              ctypes.POINTER(_p), _p],
+    "skp_capture_maps_bwd": [ctypes.POINTER(_p), ctypes.POINTER(_c_int), _c_int, _c_int, _c_int, _c_int, _c_int, _p,
+                             _c_float, ctypes.POINTER(_p), ctypes.POINTER(_p), _p, _p],
     "skp_aggregate": [ctypes.POINTER(_p), _c_int, _c_int, _c_int, _c_int, _p, _c_int, _p, _p],
     "skp_resize_bilinear": [_p, _c_int, _c_int, _c_int, _p, _p],
     "skp_resize_bilinear_bwd": [_p, _c_int, _c_int, _c_int, _p, _p],

@@ -755,6 +755,216 @@ void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nc
   }
 }
 
+// ------------------------------------------------------------------------------------ fused bwd
+// Backward of skp_capture_maps_fwd, one (layer, b·H + h, output row y) per WAVE, no LDS and no
+// barriers.  The per-image map gradient is first transposed to pixel-major gT (B, R², N)
+// (scaled by 1/(L·H)), so a pixel's token gradient is one coalesced 2-KiB run.  The wave walks
+// the R pixels of its row left to right with lanes owning NQ token quads and keeps in registers
+//   - the vertical bicubic pass of the 4 low-res columns lo(x) … lo(x)+3 the pixel taps (V
+//     window; a new column = 4 coalesced z_low row reads when lo advances, every R/s pixels),
+//   - the horizontal-adjoint accumulators of the same 4 virtual columns (W window).
+// Per pixel: z = Σ_k wx_k V_k, a = exp(z − m)·(1/Σ) from the forward's stats, dot = Σ_n a g
+// (one full-wave DPP reduction), dZ = a ⊙ (g − dot), W_k += wx_k dZ.  When lo advances the
+// lowest W column is complete and leaves as one coalesced store of the row partial
+// ws[bh][y][j][:] (virtual columns −2, −1 / s, s+1 fold into 0 / s−1 as torch's clamped taps
+// do).  Each value has one owner lane and a fixed order: deterministic, no atomics.  The
+// vertical adjoint is capture_bwd_cols_kernel over ws, as for skp_capture_bwd.
+constexpr int kRowThreads = 256;
+
+__device__ __forceinline__ float wave64_sum(float v) {
+  v = row16_sum(v);
+  float w = v;
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(v), "+v"(w));
+  v += w;
+  w = v;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(v), "+v"(w));
+  return v + w;
+}
+__device__ __forceinline__ float wave64_max(float v) {
+  v = row16_max(v);
+  float w = v;
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(v), "+v"(w));
+  v = __builtin_fmaxf(v, w);
+  w = v;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(v), "+v"(w));
+  return __builtin_fmaxf(v, w);
+}
+
+template <int NQ, bool STATS>
+__global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(4))) void capture_bwd_row_kernel(const float* __restrict__ z, int B, int H, int s,
+                                                                      int N, int R, const float* __restrict__ gT,
+                                                                      const float2* __restrict__ stats,
+                                                                      float* __restrict__ ws) {
+  constexpr float L2E = 1.4426950408889634f;
+  constexpr int W = kRowThreads / WAVE;
+  const int lane = threadIdx.x & 63;
+  // XCD-major job order: each XCD takes a contiguous range of (b, y, h), heads fastest, so the
+  // H waves reading one gT row run back to back on one L2
+  const long long total = (long long)B * H * R;
+  const long long blocks = (total + W - 1) / W;
+  const long long per = (blocks + 7) / 8;
+  const long long jb = (long long)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  const long long job = jb * W + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (jb >= blocks || job >= total) return;
+  const int h = (int)(job % H);
+  const int y = (int)((job / H) % R);
+  const int b = (int)(job / ((long long)H * R));
+  const int bh = b * H + h;
+  const int nq = N >> 2;
+  const Taps4 ty = bicubic_taps(y, s, R);
+  const f4* zr0 = reinterpret_cast<const f4*>(z + ((size_t)bh * s * s + (size_t)ty.i[0] * s) * N);
+  const f4* zr1 = reinterpret_cast<const f4*>(z + ((size_t)bh * s * s + (size_t)ty.i[1] * s) * N);
+  const f4* zr2 = reinterpret_cast<const f4*>(z + ((size_t)bh * s * s + (size_t)ty.i[2] * s) * N);
+  const f4* zr3 = reinterpret_cast<const f4*>(z + ((size_t)bh * s * s + (size_t)ty.i[3] * s) * N);
+  // lane quads lane + 64c; past-the-end quads read a valid quad (clamped) and are zeroed
+  int qo[NQ];
+  bool ok[NQ];
+#pragma unroll
+  for (int c = 0; c < NQ; ++c) {
+    ok[c] = lane + 64 * c < nq;
+    qo[c] = min(lane + 64 * c, nq - 1);
+  }
+  auto vcol = [&](int j, f4* out) {   // vertical pass of low-res column clamp(j)
+    const int o = min(max(j, 0), s - 1) * nq;
+#pragma unroll
+    for (int c = 0; c < NQ; ++c) {
+      f4 v = zr0[o + qo[c]] * ty.w[0];
+      v = __builtin_elementwise_fma(zr1[o + qo[c]], (f4)ty.w[1], v);
+      v = __builtin_elementwise_fma(zr2[o + qo[c]], (f4)ty.w[2], v);
+      v = __builtin_elementwise_fma(zr3[o + qo[c]], (f4)ty.w[3], v);
+      out[c] = v;
+    }
+  };
+  const f4* grow = reinterpret_cast<const f4*>(gT + ((size_t)b * R * R + (size_t)y * R) * N);
+  const float2* strow = STATS ? stats + ((size_t)bh * R + y) * R : nullptr;
+  f4* wrow = reinterpret_cast<f4*>(ws + ((size_t)bh * R + y) * (size_t)s * N);
+
+  f4 Vw[4][NQ], Ww[4][NQ], pend[NQ];
+  // virtual column held by window slot 0; lo advances by at most one per pixel (s <= R)
+  int base = bicubic_taps(0, s, R).lo;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) vcol(base + k, Vw[k]);
+#pragma unroll
+  for (int c = 0; c < NQ; ++c) {
+    pend[c] = (f4)0.0f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) Ww[k][c] = (f4)0.0f;
+  }
+  int pt = 0;   // clamped column pend belongs to
+  auto store_col = [&](int j, const f4* v) {
+#pragma unroll
+    for (int c = 0; c < NQ; ++c)
+      if (ok[c]) wrow[(size_t)j * nq + lane + 64 * c] = v[c];
+  };
+  // virtual column vc is complete; consecutive virtual columns clamp to non-decreasing
+  // columns that advance by at most one, so every column is stored exactly once
+  auto emit = [&](int vc, const f4* v) {
+    const int t = min(max(vc, 0), s - 1);
+    if (t != pt) {
+      store_col(pt, pend);
+      pt = t;
+#pragma unroll
+      for (int c = 0; c < NQ; ++c) pend[c] = v[c];
+    } else {
+#pragma unroll
+      for (int c = 0; c < NQ; ++c) pend[c] += v[c];
+    }
+  };
+  f4 g[NQ];
+#pragma unroll
+  for (int c = 0; c < NQ; ++c) g[c] = grow[qo[c]];
+  for (int x = 0; x < R; ++x) {
+    const Taps4 tx = bicubic_taps(x, s, R);
+    if (base < tx.lo) {   // wave-uniform: slot 0 is complete; slide both windows by one column
+      emit(base, Ww[0]);
+#pragma unroll
+      for (int c = 0; c < NQ; ++c) {
+        Ww[0][c] = Ww[1][c]; Ww[1][c] = Ww[2][c]; Ww[2][c] = Ww[3][c]; Ww[3][c] = (f4)0.0f;
+        Vw[0][c] = Vw[1][c]; Vw[1][c] = Vw[2][c]; Vw[2][c] = Vw[3][c];
+      }
+      ++base;
+      vcol(base + 3, Vw[3]);
+    }
+    f4 gn[NQ];   // next pixel's gradient, in flight during this pixel
+    const int xn = min(x + 1, R - 1);
+#pragma unroll
+    for (int c = 0; c < NQ; ++c) gn[c] = grow[(size_t)xn * nq + qo[c]];
+    f4 a[NQ];
+    float m = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < NQ; ++c) {
+      f4 v = Vw[0][c] * tx.w[0];
+      v = __builtin_elementwise_fma(Vw[1][c], (f4)tx.w[1], v);
+      v = __builtin_elementwise_fma(Vw[2][c], (f4)tx.w[2], v);
+      v = __builtin_elementwise_fma(Vw[3][c], (f4)tx.w[3], v);
+      a[c] = v;
+      if (!STATS) m = __builtin_fmaxf(__builtin_fmaxf(m, __builtin_fmaxf(v.x, v.y)), __builtin_fmaxf(v.z, v.w));
+    }
+    float inv;
+    if (STATS) {
+      const float2 st = strow[x];
+      m = st.x;
+      inv = st.y;
+    } else {
+      m = wave64_max(m);   // clamped quads duplicate valid tokens: the max is unchanged
+    }
+    const f4 mb = (f4)(-m * L2E);
+    f4 sv = (f4)0.0f;
+#pragma unroll
+    for (int c = 0; c < NQ; ++c) {
+      f4 t = __builtin_elementwise_fma(a[c], (f4)L2E, mb);
+      t.x = __builtin_amdgcn_exp2f(t.x);
+      t.y = __builtin_amdgcn_exp2f(t.y);
+      t.z = __builtin_amdgcn_exp2f(t.z);
+      t.w = __builtin_amdgcn_exp2f(t.w);
+      a[c] = ok[c] ? t : (f4)0.0f;
+      sv += a[c];
+    }
+    if (!STATS) inv = __builtin_amdgcn_rcpf(wave64_sum((sv.x + sv.y) + (sv.z + sv.w)));
+    f4 dv = (f4)0.0f;
+#pragma unroll
+    for (int c = 0; c < NQ; ++c) {
+      a[c] *= inv;
+      dv = __builtin_elementwise_fma(a[c], g[c], dv);
+    }
+    const float dot = wave64_sum((dv.x + dv.y) + (dv.z + dv.w));
+#pragma unroll
+    for (int c = 0; c < NQ; ++c) {
+      const f4 dz = a[c] * (g[c] - dot);
+      Ww[0][c] = __builtin_elementwise_fma(dz, (f4)tx.w[0], Ww[0][c]);
+      Ww[1][c] = __builtin_elementwise_fma(dz, (f4)tx.w[1], Ww[1][c]);
+      Ww[2][c] = __builtin_elementwise_fma(dz, (f4)tx.w[2], Ww[2][c]);
+      Ww[3][c] = __builtin_elementwise_fma(dz, (f4)tx.w[3], Ww[3][c]);
+      g[c] = gn[c];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) emit(base + k, Ww[k]);
+  store_col(pt, pend);
+}
+
+// gT[b][p][n] = scale · g[b][n][p]: 64 × 64 tiles through LDS (coalesced both ways)
+__global__ __launch_bounds__(256) void transpose_scale_kernel(const float* __restrict__ g, int N, int P, float scale,
+                                                              float* __restrict__ gT) {
+  __shared__ float tile[64][65];
+  const int b = blockIdx.z;
+  const int p0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
+  const float* gb = g + (size_t)b * N * P;
+  float* ob = gT + (size_t)b * N * P;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int n = n0 + ty + 4 * k, p = p0 + tx;
+    tile[ty + 4 * k][tx] = (n < N && p < P) ? gb[(size_t)n * P + p] * scale : 0.0f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int p = p0 + ty + 4 * k, n = n0 + tx;
+    if (n < N && p < P) ob[(size_t)p * N + n] = tile[tx][ty + 4 * k];
+  }
+}
+
 // ------------------------------------------------------------------------------------ aggregate
 struct LayerPtrs {
   const float* p[SKP_MAX_LAYERS];
@@ -1080,6 +1290,64 @@ extern "C" int skp_capture_maps_fwd(const float* const* z_low, const int* sizes,
     default: launch_maps_w<16>(waves, cl, L, B, H, N, R, vstride, lds, maps, st); break;
   }
   SKP_LAUNCH_CHECK();
+  return SKP_OK;
+}
+
+namespace {
+template <int NQ>
+void launch_bwd_row(const float* z, int B, int H, int s, int N, int R, const float* gT, const float* stats, float* ws,
+                    hipStream_t st) {
+  const long long total = (long long)B * H * R;
+  const long long blocks = (total + kRowThreads / WAVE - 1) / (kRowThreads / WAVE);
+  const long long grid = 8 * ((blocks + 7) / 8);
+  const float2* st2 = reinterpret_cast<const float2*>(stats);
+  if (stats)
+    hipLaunchKernelGGL((capture_bwd_row_kernel<NQ, true>), dim3((unsigned)grid), dim3(kRowThreads), 0, st, z, B, H, s, N,
+                       R, gT, st2, ws);
+  else
+    hipLaunchKernelGGL((capture_bwd_row_kernel<NQ, false>), dim3((unsigned)grid), dim3(kRowThreads), 0, st, z, B, H, s,
+                       N, R, gT, st2, ws);
+}
+}  // namespace
+
+extern "C" int skp_capture_maps_bwd(const float* const* z_low, const int* sizes, int L, int B, int H, int N, int R,
+                                    const float* dmaps, float gscale, const float* const* stats, float* const* dz_low,
+                                    float* workspace, void* stream) {
+  SKP_CHECK_ARG(z_low && sizes && dmaps && dz_low && workspace, "null pointer");
+  SKP_CHECK_ARG(L > 0 && L <= SKP_MAX_LAYERS, "L out of range");
+  SKP_CHECK_ARG(B > 0 && H > 0 && N > 0 && R > 0, "non-positive shape");
+  SKP_CHECK_ARG(N % 4 == 0, "N must be a multiple of 4 (use skp_capture_bwd)");
+  SKP_CHECK_ARG(N <= 1024, "N > 1024 tokens is not supported");
+  SKP_CHECK_ARG((long long)B * H <= 65535 && (long long)B * H * R < (1LL << 31), "shape too large");
+  SKP_CHECK_ARG((reinterpret_cast<uintptr_t>(workspace) & 15) == 0, "workspace must be 16-B aligned");
+  int smax = 0;
+  for (int l = 0; l < L; ++l) {
+    SKP_CHECK_ARG(z_low[l] && dz_low[l], "null layer pointer");
+    SKP_CHECK_ARG(sizes[l] > 0 && sizes[l] <= R && sizes[l] <= 1024, "layer size must be in [1, R]");
+    SKP_CHECK_ARG((reinterpret_cast<uintptr_t>(z_low[l]) & 15) == 0, "z_low pointers must be 16-B aligned");
+    smax = std::max(smax, sizes[l]);
+  }
+  hipStream_t st = as_stream(stream);
+  const int P = R * R;
+  float* gT = workspace;                                   // (B, R², N)
+  float* ws = workspace + (size_t)B * P * N;               // (B·H, R, s, N) row partials, reused per layer
+  hipLaunchKernelGGL(transpose_scale_kernel, dim3((P + 63) / 64, (N + 63) / 64, B), dim3(256), 0, st, dmaps, N, P, gscale,
+                     gT);
+  SKP_LAUNCH_CHECK();
+  const int nq = N / 4;
+  for (int l = 0; l < L; ++l) {
+    const int s = sizes[l];
+    const float* stl = stats ? stats[l] : nullptr;
+    if (nq <= 64) launch_bwd_row<1>(z_low[l], B, H, s, N, R, gT, stl, ws, st);
+    else if (nq <= 128) launch_bwd_row<2>(z_low[l], B, H, s, N, R, gT, stl, ws, st);
+    else launch_bwd_row<4>(z_low[l], B, H, s, N, R, gT, stl, ws, st);
+    SKP_LAUNCH_CHECK();
+    const int chunks = (int)(((long long)s * N + kColThreads - 1) / kColThreads);
+    hipLaunchKernelGGL(capture_bwd_cols_kernel, dim3(chunks, B * H), dim3(kColThreads), 0, st, ws, B * H, s, N, R,
+                       dz_low[l]);
+    SKP_LAUNCH_CHECK();
+  }
+  (void)smax;
   return SKP_OK;
 }
 

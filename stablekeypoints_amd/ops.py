@@ -186,6 +186,14 @@ def capture_maps_bytes(B, H, N, R, sizes):
     return 4 * (sum(B * H * s * s * N for s in sizes) + B * N * RR + len(sizes) * B * H * RR * 2)
 
 
+def capture_maps_bwd_bytes(B, H, N, R, sizes):
+    """Algorithmic HBM bytes of one skp_capture_maps_bwd call: the map gradient read once (and
+    its pixel-major copy written and read once), every z_low and stats read once, the row
+    partials written and read once, dz_low written once."""
+    RR = R * R
+    return 4 * (3 * B * N * RR + sum(2 * B * H * s * s * N + 2 * B * H * RR + 2 * B * H * R * s * N for s in sizes))
+
+
 class CaptureMaps(torch.autograd.Function):
     """Per-image maps straight from the captured layers' logits (fused capture + aggregate).
 
@@ -240,8 +248,21 @@ class CaptureMaps(torch.autograd.Function):
         dmaps = _c(dmaps)                       # (B, N, R, R)
         RR = R * R
         scale = 1.0 / float(len(zs) * H)
-        dzs = [capture_bwd(z, s, R, dmaps, gscale=scale, group=H, strides=(N * RR, 1, RR), stats=st)
-               for z, s, st in zip(zs, sizes, stats)]
+        if FUSED_MAPS and N % 4 == 0:
+            dzs = [torch.empty_like(z) for z in zs]
+            ws = torch.empty(B * RR * N + B * H * R * max(sizes) * N, device=dmaps.device, dtype=F32)
+            zp = (ctypes.c_void_p * L)(*[z.data_ptr() for z in zs])
+            sp = (ctypes.c_int * L)(*[int(s) for s in sizes])
+            stp = (ctypes.c_void_p * L)(*[st.data_ptr() for st in stats])
+            dp = (ctypes.c_void_p * L)(*[d.data_ptr() for d in dzs])
+            with _timed("skp_capture_maps_bwd", capture_maps_bwd_bytes(B, H, N, R, sizes)):
+                call("skp_capture_maps_bwd", ctypes.cast(zp, ctypes.POINTER(ctypes.c_void_p)), sp, L, B, H, N, R,
+                     ptr(dmaps), scale, ctypes.cast(stp, ctypes.POINTER(ctypes.c_void_p)),
+                     ctypes.cast(dp, ctypes.POINTER(ctypes.c_void_p)), ptr(ws), stream(dmaps.device))
+            del ws
+        else:
+            dzs = [capture_bwd(z, s, R, dmaps, gscale=scale, group=H, strides=(N * RR, 1, RR), stats=st)
+                   for z, s, st in zip(zs, sizes, stats)]
         return (None, None, None) + tuple(dzs)
 
 

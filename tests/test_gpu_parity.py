@@ -407,6 +407,63 @@ def test_capture_maps_fwd_equals_two_kernel_path_full_size():
         assert (d1 - d0).abs().max().item() < 1e-5 * max(1.0, d0.abs().max().item())
 
 
+def _capture_maps_bwd_abi(zs, sizes, B, H, R, dmaps, gscale, stats):
+    import ctypes
+    from stablekeypoints_amd._lib import call, ptr, stream
+    L = len(zs)
+    Nn = zs[0].shape[-1]
+    dzs = [torch.full_like(z, float("nan")) for z in zs]
+    ws = torch.empty(B * R * R * Nn + B * H * R * max(sizes) * Nn, device=DEV)
+    arr = lambda ts: ctypes.cast((ctypes.c_void_p * L)(*[t.data_ptr() for t in ts]), ctypes.POINTER(ctypes.c_void_p))
+    call("skp_capture_maps_bwd", arr(zs), (ctypes.c_int * L)(*sizes), L, B, H, Nn, R, ptr(dmaps), float(gscale),
+         arr(stats) if stats is not None else None, arr(dzs), ptr(ws), stream(DEV))
+    torch.cuda.synchronize()
+    return dzs
+
+
+@pytest.mark.parametrize("B,H,sizes,R,Nn,with_stats", [(2, 8, (4, 4, 4, 8), 32, 40, True), (1, 3, (5, 3), 40, 36, True),
+                                                       (2, 2, (16, 32), 128, 4, False), (1, 2, (8,), 32, 1000, True),
+                                                       (3, 1, (1, 2), 8, 128, False), (1, 4, (7, 13), 100, 256, True),
+                                                       (1, 2, (6, 64), 64, 260, True)])
+def test_capture_maps_bwd_vs_oracle(B, H, sizes, R, Nn, with_stats):
+    """skp_capture_maps_bwd (one wave per (layer, head, row), V/W windows in registers) vs the
+    oracle's capture_bwd of the per-image broadcast gradient (collect_maps_bwd, optimize.py:27-79,
+    then the capture branch's softmax + bicubic adjoint, ptp_utils.py:513-536): relative 1e-4."""
+    zs = [recipes.random_logits(400 + 5 * i + Nn, (B * H, s * s, Nn), scale=2.0) for i, s in enumerate(sizes)]
+    zt = [T(z) for z in zs]
+    _, stats = _capture_maps_abi(zt, list(sizes), B, H, R)
+    w = recipes.random_logits(77 + Nn, (B, Nn, R, R))
+    L = len(sizes)
+    dzs = _capture_maps_bwd_abi(zt, list(sizes), B, H, R, T(w), 1.0 / (L * H), stats if with_stats else None)
+    for i, (z, s) in enumerate(zip(zs, sizes)):
+        dattn = np.concatenate([O.collect_maps_bwd([(H, R * R, Nn)] * L, w[b], layers=tuple(range(L)))[i]
+                                for b in range(B)])
+        ref = O.capture_bwd(z, s, R, dattn)
+        got = N(dzs[i])
+        assert np.isfinite(got).all()
+        assert np.abs(got - ref).max() < 1e-4 * max(1e-3, np.abs(ref).max()), (i, np.abs(got - ref).max(), np.abs(ref).max())
+
+
+def test_capture_maps_bwd_equals_per_layer_kernel_full_size():
+    """Bench shape (B=8 × 8 heads, s = 16,16,16,32, R=128, N=500): the fused backward equals the
+    per-layer skp_capture_bwd (the r01 path, oracle-pinned) to fp32 rounding, and is
+    deterministic (bitwise equal on a second run)."""
+    from stablekeypoints_amd import ops
+    B, H, R, Nn, sizes = 8, 8, 128, 500, (16, 16, 16, 32)
+    g = torch.Generator().manual_seed(9)
+    zs = [(torch.randn(B * H, s * s, Nn, generator=g) * 3).to(DEV) for s in sizes]
+    _, stats = _capture_maps_abi(zs, list(sizes), B, H, R)
+    gmap = torch.randn(B, Nn, R, R, generator=g).to(DEV)
+    d1 = _capture_maps_bwd_abi(zs, list(sizes), B, H, R, gmap, 1 / 32, stats)
+    d2 = _capture_maps_bwd_abi(zs, list(sizes), B, H, R, gmap, 1 / 32, stats)
+    for z, s, st, a, a2 in zip(zs, sizes, stats, d1, d2):
+        ref = ops.capture_bwd(z, s, R, gmap, gscale=1 / 32, group=H, strides=(Nn * R * R, 1, R * R), stats=st)
+        err = (a - ref).abs().max().item() / ref.abs().max().item()
+        print(f"\ns={s}: fused bwd vs per-layer rel-max {err:.2e}")
+        assert err < 1e-5
+        assert torch.equal(a, a2)
+
+
 def test_batched_captures_match_sequential_tiny():
     """TokenOptimizer: one B=2 pass (LogitStore, fused maps) == the reference's two passes."""
     from stablekeypoints_amd import ptp_utils

@@ -75,6 +75,16 @@ def main():
                 res[name] = timed(lambda: ops.capture_maps(z8, sizes, 8, R), args.iters)
             ops.FUSED_MAPS = True
             del z8
+        elif name in ("mapsbwd8", "mapsbwd8_old"):   # fused backward vs per-layer capture_bwd, bench shape
+            sizes = (16, 16, 16, 32)
+            z8 = [(torch.randn(8 * H, s * s, N, device=dev, generator=g) * 2).requires_grad_(True) for s in sizes]
+            ops.FUSED_MAPS = True
+            maps = ops.capture_maps(z8, sizes, 8, R)
+            gm = torch.randn_like(maps)
+            ops.FUSED_MAPS = name == "mapsbwd8"
+            res[name] = timed(lambda: torch.autograd.grad(maps, z8, gm, retain_graph=True), args.iters)
+            ops.FUSED_MAPS = True
+            del z8, maps, gm
         elif name == "sum1g":   # read-bandwidth reference: torch reduction over a fresh 1 GiB tensor
             big = torch.empty(256 * 1024 * 1024, device=dev).normal_()
             res[name] = timed(lambda: big.sum(), args.iters)
