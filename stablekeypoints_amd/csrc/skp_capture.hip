@@ -791,20 +791,31 @@ __device__ __forceinline__ float wave64_max(float v) {
 }
 
 template <int NQ, bool STATS>
-__global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(4))) void capture_bwd_row_kernel(const float* __restrict__ z, int B, int H, int s,
-                                                                      int N, int R, const float* __restrict__ gT,
-                                                                      const float2* __restrict__ stats,
-                                                                      float* __restrict__ ws) {
+__global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(4)))
+void capture_bwd_row_kernel(const float* __restrict__ z, int B, int H, int s, int N, int R,
+                            const float* __restrict__ gT, const float2* __restrict__ stats, float* __restrict__ ws) {
   constexpr float L2E = 1.4426950408889634f;
   constexpr int W = kRowThreads / WAVE;
+  constexpr int Np = 256 * NQ;                      // padded tokens (64 lanes × NQ quads)
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float4* TWt = reinterpret_cast<float4*>(lds);                    // R tap weights (shared by the block)
+  int* TLt = reinterpret_cast<int*>(lds + 4 * R);                  // R first taps (before clamping)
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
+  f4* ring = reinterpret_cast<f4*>(lds + 5 * R + ((4 - (5 * R) % 4) % 4)) + (size_t)wid * 4 * (Np / 4);   // 4 V columns
+  for (int x = threadIdx.x; x < R; x += kRowThreads) {
+    const Taps4 t = bicubic_taps(x, s, R);
+    TWt[x] = make_float4(t.w[0], t.w[1], t.w[2], t.w[3]);
+    TLt[x] = t.lo;
+  }
+  __syncthreads();
   // XCD-major job order: each XCD takes a contiguous range of (b, y, h), heads fastest, so the
   // H waves reading one gT row run back to back on one L2
   const long long total = (long long)B * H * R;
   const long long blocks = (total + W - 1) / W;
   const long long per = (blocks + 7) / 8;
   const long long jb = (long long)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
-  const long long job = jb * W + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const long long job = jb * W + wid;
   if (jb >= blocks || job >= total) return;
   const int h = (int)(job % H);
   const int y = (int)((job / H) % R);
@@ -816,7 +827,7 @@ __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(4))
   const f4* zr1 = reinterpret_cast<const f4*>(z + ((size_t)bh * s * s + (size_t)ty.i[1] * s) * N);
   const f4* zr2 = reinterpret_cast<const f4*>(z + ((size_t)bh * s * s + (size_t)ty.i[2] * s) * N);
   const f4* zr3 = reinterpret_cast<const f4*>(z + ((size_t)bh * s * s + (size_t)ty.i[3] * s) * N);
-  // lane quads lane + 64c; past-the-end quads read a valid quad (clamped) and are zeroed
+  // lane quads lane + 64c; past-the-end quads read a valid quad (clamped)
   int qo[NQ];
   bool ok[NQ];
 #pragma unroll
@@ -824,89 +835,95 @@ __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(4))
     ok[c] = lane + 64 * c < nq;
     qo[c] = min(lane + 64 * c, nq - 1);
   }
-  auto vcol = [&](int j, f4* out) {   // vertical pass of low-res column clamp(j)
+  // vertical pass of virtual column j (clamped) into ring slot j & 3; padded quads get −1e30
+  auto vcol = [&](int j) {
     const int o = min(max(j, 0), s - 1) * nq;
+    f4* dst = ring + (j & 3) * (Np / 4) + lane;
 #pragma unroll
     for (int c = 0; c < NQ; ++c) {
       f4 v = zr0[o + qo[c]] * ty.w[0];
       v = __builtin_elementwise_fma(zr1[o + qo[c]], (f4)ty.w[1], v);
       v = __builtin_elementwise_fma(zr2[o + qo[c]], (f4)ty.w[2], v);
       v = __builtin_elementwise_fma(zr3[o + qo[c]], (f4)ty.w[3], v);
-      out[c] = v;
+      dst[64 * c] = ok[c] ? v : (f4)kPadLogit;
     }
   };
   const f4* grow = reinterpret_cast<const f4*>(gT + ((size_t)b * R * R + (size_t)y * R) * N);
-  const float2* strow = STATS ? stats + ((size_t)bh * R + y) * R : nullptr;
+  const float4* strow = STATS ? reinterpret_cast<const float4*>(stats + ((size_t)bh * R + y) * R) : nullptr;
   f4* wrow = reinterpret_cast<f4*>(ws + ((size_t)bh * R + y) * (size_t)s * N);
 
-  f4 Vw[4][NQ], Ww[4][NQ], pend[NQ];
-  // virtual column held by window slot 0; lo advances by at most one per pixel (s <= R)
-  int base = bicubic_taps(0, s, R).lo;
+  // W window: adjoint accumulators of virtual columns base … base + 3 (registers).  lo advances
+  // by at most one per pixel (s <= R) and stays <= s − 2, so in the loop a completed column is
+  // either virtual (< 0: folded into the next slot, which clamps to the same column 0) or a real
+  // column < s − 1 (stored once)
+  f4 Ww[4][NQ];
+  int base = TLt[0];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) vcol(base + k, Vw[k]);
+  for (int k = 0; k < 4; ++k) vcol(base + k);
 #pragma unroll
-  for (int c = 0; c < NQ; ++c) {
-    pend[c] = (f4)0.0f;
+  for (int c = 0; c < NQ; ++c)
 #pragma unroll
     for (int k = 0; k < 4; ++k) Ww[k][c] = (f4)0.0f;
-  }
-  int pt = 0;   // clamped column pend belongs to
   auto store_col = [&](int j, const f4* v) {
 #pragma unroll
     for (int c = 0; c < NQ; ++c)
       if (ok[c]) wrow[(size_t)j * nq + lane + 64 * c] = v[c];
   };
-  // virtual column vc is complete; consecutive virtual columns clamp to non-decreasing
-  // columns that advance by at most one, so every column is stored exactly once
-  auto emit = [&](int vc, const f4* v) {
-    const int t = min(max(vc, 0), s - 1);
-    if (t != pt) {
-      store_col(pt, pend);
-      pt = t;
+#ifndef SKP_BWD_GPF
+#define SKP_BWD_GPF 1   // pixels of gradient prefetched ahead (registers; 2 measured +1%)
+#endif
+  constexpr int GPF = SKP_BWD_GPF;
+  f4 g[GPF + 1][NQ];   // g[0]: this pixel, g[k]: pixel x + k in flight
 #pragma unroll
-      for (int c = 0; c < NQ; ++c) pend[c] = v[c];
-    } else {
+  for (int k = 0; k < GPF; ++k)
 #pragma unroll
-      for (int c = 0; c < NQ; ++c) pend[c] += v[c];
-    }
-  };
-  f4 g[NQ];
-#pragma unroll
-  for (int c = 0; c < NQ; ++c) g[c] = grow[qo[c]];
+    for (int c = 0; c < NQ; ++c) g[k][c] = grow[(size_t)min(k, R - 1) * nq + qo[c]];
+  float4 stq = make_float4(0.f, 0.f, 0.f, 0.f);   // stats of pixels x0 + 2·lane, x0 + 2·lane + 1
+  auto rl = [](float v, int i) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), i)); };
   for (int x = 0; x < R; ++x) {
-    const Taps4 tx = bicubic_taps(x, s, R);
-    if (base < tx.lo) {   // wave-uniform: slot 0 is complete; slide both windows by one column
-      emit(base, Ww[0]);
+    if (STATS && (x & 127) == 0) stq = strow[min((x >> 1) + lane, (R - 1) >> 1)];
+    const float4 w = TWt[x];
+    const int lo = TLt[x];
+    if (base < lo) {   // wave-uniform: W slot 0 is complete; slide by one column
+      if (base < 0) {
+#pragma unroll
+        for (int c = 0; c < NQ; ++c) Ww[1][c] += Ww[0][c];
+      } else {
+        store_col(base, Ww[0]);
+      }
 #pragma unroll
       for (int c = 0; c < NQ; ++c) {
         Ww[0][c] = Ww[1][c]; Ww[1][c] = Ww[2][c]; Ww[2][c] = Ww[3][c]; Ww[3][c] = (f4)0.0f;
-        Vw[0][c] = Vw[1][c]; Vw[1][c] = Vw[2][c]; Vw[2][c] = Vw[3][c];
       }
       ++base;
-      vcol(base + 3, Vw[3]);
+      vcol(base + 3);   // replaces the column that just left (ring slot (base − 1) & 3)
     }
-    f4 gn[NQ];   // next pixel's gradient, in flight during this pixel
-    const int xn = min(x + 1, R - 1);
+    const int xn = min(x + GPF, R - 1);
 #pragma unroll
-    for (int c = 0; c < NQ; ++c) gn[c] = grow[(size_t)xn * nq + qo[c]];
+    for (int c = 0; c < NQ; ++c) g[GPF][c] = grow[(size_t)xn * nq + qo[c]];
+    const f4* v0 = ring + ((base + 0) & 3) * (Np / 4) + lane;
+    const f4* v1 = ring + ((base + 1) & 3) * (Np / 4) + lane;
+    const f4* v2 = ring + ((base + 2) & 3) * (Np / 4) + lane;
+    const f4* v3 = ring + ((base + 3) & 3) * (Np / 4) + lane;
     f4 a[NQ];
     float m = -INFINITY;
 #pragma unroll
     for (int c = 0; c < NQ; ++c) {
-      f4 v = Vw[0][c] * tx.w[0];
-      v = __builtin_elementwise_fma(Vw[1][c], (f4)tx.w[1], v);
-      v = __builtin_elementwise_fma(Vw[2][c], (f4)tx.w[2], v);
-      v = __builtin_elementwise_fma(Vw[3][c], (f4)tx.w[3], v);
+      f4 v = v0[64 * c] * w.x;
+      v = __builtin_elementwise_fma(v1[64 * c], (f4)w.y, v);
+      v = __builtin_elementwise_fma(v2[64 * c], (f4)w.z, v);
+      v = __builtin_elementwise_fma(v3[64 * c], (f4)w.w, v);
       a[c] = v;
       if (!STATS) m = __builtin_fmaxf(__builtin_fmaxf(m, __builtin_fmaxf(v.x, v.y)), __builtin_fmaxf(v.z, v.w));
     }
     float inv;
     if (STATS) {
-      const float2 st = strow[x];
-      m = st.x;
-      inv = st.y;
+      const int src = (x & 127) >> 1;
+      const bool odd = x & 1;
+      m = rl(odd ? stq.z : stq.x, src);
+      inv = rl(odd ? stq.w : stq.y, src);
     } else {
-      m = wave64_max(m);   // clamped quads duplicate valid tokens: the max is unchanged
+      m = wave64_max(m);   // padded quads hold −1e30: the max is unchanged
     }
     const f4 mb = (f4)(-m * L2E);
     f4 sv = (f4)0.0f;
@@ -917,30 +934,50 @@ __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(4))
       t.y = __builtin_amdgcn_exp2f(t.y);
       t.z = __builtin_amdgcn_exp2f(t.z);
       t.w = __builtin_amdgcn_exp2f(t.w);
-      a[c] = ok[c] ? t : (f4)0.0f;
-      sv += a[c];
+      a[c] = t;
+      sv += t;
     }
     if (!STATS) inv = __builtin_amdgcn_rcpf(wave64_sum((sv.x + sv.y) + (sv.z + sv.w)));
-    f4 dv = (f4)0.0f;
+    f4 ag[NQ], dv = (f4)0.0f;
 #pragma unroll
     for (int c = 0; c < NQ; ++c) {
       a[c] *= inv;
-      dv = __builtin_elementwise_fma(a[c], g[c], dv);
+      ag[c] = a[c] * g[0][c];
+      dv += ag[c];
     }
     const float dot = wave64_sum((dv.x + dv.y) + (dv.z + dv.w));
 #pragma unroll
     for (int c = 0; c < NQ; ++c) {
-      const f4 dz = a[c] * (g[c] - dot);
-      Ww[0][c] = __builtin_elementwise_fma(dz, (f4)tx.w[0], Ww[0][c]);
-      Ww[1][c] = __builtin_elementwise_fma(dz, (f4)tx.w[1], Ww[1][c]);
-      Ww[2][c] = __builtin_elementwise_fma(dz, (f4)tx.w[2], Ww[2][c]);
-      Ww[3][c] = __builtin_elementwise_fma(dz, (f4)tx.w[3], Ww[3][c]);
-      g[c] = gn[c];
+      const f4 dz = __builtin_elementwise_fma(a[c], (f4)(-dot), ag[c]);   // a ⊙ (g − dot)
+      Ww[0][c] = __builtin_elementwise_fma(dz, (f4)w.x, Ww[0][c]);
+      Ww[1][c] = __builtin_elementwise_fma(dz, (f4)w.y, Ww[1][c]);
+      Ww[2][c] = __builtin_elementwise_fma(dz, (f4)w.z, Ww[2][c]);
+      Ww[3][c] = __builtin_elementwise_fma(dz, (f4)w.w, Ww[3][c]);
+#pragma unroll
+      for (int k = 0; k < GPF; ++k) g[k][c] = g[k + 1][c];
     }
   }
+  // the last window: virtual columns base … base + 3 (clamped runs summed, each column once)
+  f4 acc[NQ];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) emit(base + k, Ww[k]);
-  store_col(pt, pend);
+  for (int c = 0; c < NQ; ++c) acc[c] = Ww[0][c];
+#pragma unroll
+  for (int k = 1; k < 4; ++k) {
+    const int tp = min(max(base + k - 1, 0), s - 1), t = min(max(base + k, 0), s - 1);
+    if (t == tp) {
+#pragma unroll
+      for (int c = 0; c < NQ; ++c) acc[c] += Ww[k][c];
+    } else {
+      store_col(tp, acc);
+#pragma unroll
+      for (int c = 0; c < NQ; ++c) acc[c] = Ww[k][c];
+    }
+  }
+  store_col(min(max(base + 3, 0), s - 1), acc);
+}
+
+size_t bwd_row_lds(int R, int nqpl) {   // tap table + 4 waves × 4 ring columns × Np floats
+  return ((size_t)5 * R + 4 + (size_t)(kRowThreads / WAVE) * 4 * 256 * nqpl) * sizeof(float);
 }
 
 // gT[b][p][n] = scale · g[b][n][p]: 64 × 64 tiles through LDS (coalesced both ways)
@@ -1301,11 +1338,12 @@ void launch_bwd_row(const float* z, int B, int H, int s, int N, int R, const flo
   const long long blocks = (total + kRowThreads / WAVE - 1) / (kRowThreads / WAVE);
   const long long grid = 8 * ((blocks + 7) / 8);
   const float2* st2 = reinterpret_cast<const float2*>(stats);
+  const size_t lds = bwd_row_lds(R, NQ);
   if (stats)
-    hipLaunchKernelGGL((capture_bwd_row_kernel<NQ, true>), dim3((unsigned)grid), dim3(kRowThreads), 0, st, z, B, H, s, N,
-                       R, gT, st2, ws);
+    hipLaunchKernelGGL((capture_bwd_row_kernel<NQ, true>), dim3((unsigned)grid), dim3(kRowThreads), lds, st, z, B, H, s,
+                       N, R, gT, st2, ws);
   else
-    hipLaunchKernelGGL((capture_bwd_row_kernel<NQ, false>), dim3((unsigned)grid), dim3(kRowThreads), 0, st, z, B, H, s,
+    hipLaunchKernelGGL((capture_bwd_row_kernel<NQ, false>), dim3((unsigned)grid), dim3(kRowThreads), lds, st, z, B, H, s,
                        N, R, gT, st2, ws);
 }
 }  // namespace
@@ -1318,6 +1356,7 @@ extern "C" int skp_capture_maps_bwd(const float* const* z_low, const int* sizes,
   SKP_CHECK_ARG(B > 0 && H > 0 && N > 0 && R > 0, "non-positive shape");
   SKP_CHECK_ARG(N % 4 == 0, "N must be a multiple of 4 (use skp_capture_bwd)");
   SKP_CHECK_ARG(N <= 1024, "N > 1024 tokens is not supported");
+  SKP_CHECK_ARG(bwd_row_lds(R, N <= 256 ? 1 : (N <= 512 ? 2 : 4)) <= 160 * 1024, "R * N too large for LDS");
   SKP_CHECK_ARG((long long)B * H <= 65535 && (long long)B * H * R < (1LL << 31), "shape too large");
   SKP_CHECK_ARG((reinterpret_cast<uintptr_t>(workspace) & 15) == 0, "workspace must be 16-B aligned");
   int smax = 0;
