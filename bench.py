@@ -29,6 +29,7 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK = 8.0e12          # MI355X_MICROARCH.md: 8.0 TB/s spec
 HBM_MEASURED_COPY = 6.29e12
+VALU_F32_PEAK = 157.3e12   # MI355X_MICROARCH.md: f32 vector peak (packed v_pk_fma_f32), 256 CUs
 
 
 class KernelTimer:
@@ -68,6 +69,15 @@ class KernelTimer:
         return {"launches": len(ms), "avg_ms": float(np.mean(ms)), "bytes_per_launch": float(np.mean(self.nbytes[name]))}
 
 
+def _pmc_record(path, name, key, value):
+    """A PMC-derived figure for `name` from profiles/*.json, only if measured on this workload."""
+    try:
+        rec = json.load(open(path)).get(name, {})
+    except (OSError, ValueError):
+        return None
+    return rec.get(value) if rec.get(key[0]) == key[1] else None
+
+
 # ------------------------------------------------------------------------------ CPU baseline (port)
 def cpu_baseline(args):
     """One micro-iteration of the same workload on the host CPU: torch-CPU UNet/VAE
@@ -78,7 +88,14 @@ def cpu_baseline(args):
     from stablekeypoints_amd.sd.unet import CaptureComplete, attention_core
     from stablekeypoints_amd.datasets import SyntheticDataset
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    nproc = os.cpu_count() or 1
+    try:
+        allowed = len(os.sched_getaffinity(0))   # the CPUs this process may run on
+    except AttributeError:
+        allowed = nproc
+    # OMP_NUM_THREADS, when the host sets it, is the CPU share this job owns (a cgroup quota that
+    # neither nproc nor the affinity mask shows); oversubscribing a quota only slows the baseline
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or allowed
     torch.set_num_threads(threads)
     ldm = build_sd15(seed=0, device="cpu")
     R = args.res // 4
@@ -158,32 +175,45 @@ def cpu_baseline(args):
     context = torch.randn(1, args.tokens, 768).requires_grad_(True)
     img = SyntheticDataset(n=1, size=args.res, seed=0)[0]["img"][None]
 
-    def capture(image):
+    def capture(image, ctx):
         with torch.no_grad():
             lat = ldm.vae.encode(image * 2 - 1)["latent_dist"].mean * 0.18215
         t = ldm.scheduler.timesteps[-1]
         noisy = ldm.scheduler.add_noise(lat, torch.randn_like(lat), t)
         store.clear()
         try:
-            ldm.unet(noisy, t.repeat(1), context)
+            ldm.unet(noisy, t.repeat(1), ctx)
         except CaptureComplete:
             pass
         return OAggregate.apply(*store)
 
-    t0 = time.time()
-    m = capture(img)
-    u = torch.rand(1, 4).numpy()
-    theta = O.affine_params(u, 15.0, (0.8, 1.0), (0.25, 0.25))
-    timg = torch.from_numpy(O.affine_warp(img.numpy(), theta))
-    mt = capture(timg)
-    cand = O.find_top_k_gaussian(m.detach().numpy(), 25, sigma=2.0)
-    idx = torch.from_numpy(O.furthest_point_sampling(mt.detach().numpy(), 10, cand))
-    sh = OSharp.apply(m[idx], 2.0)
-    eq = OEquiv.apply(m[idx], mt[idx], theta)
-    loss = (eq * 1000.0 + sh * 100.0) / args.accum
-    loss.backward()
-    assert context.grad is not None and torch.isfinite(context.grad).all()
-    dt = time.time() - t0
+    def micro_iteration(ctx):
+        m = capture(img, ctx)
+        u = torch.rand(1, 4).numpy()
+        theta = O.affine_params(u, 15.0, (0.8, 1.0), (0.25, 0.25))
+        timg = torch.from_numpy(O.affine_warp(img.numpy(), theta))
+        mt = capture(timg, ctx)
+        cand = O.find_top_k_gaussian(m.detach().numpy(), min(25, m.shape[0]), sigma=2.0)
+        idx = torch.from_numpy(O.furthest_point_sampling(mt.detach().numpy(), min(10, m.shape[0]), cand))
+        sh = OSharp.apply(m[idx], 2.0)
+        eq = OEquiv.apply(m[idx], mt[idx], theta)
+        loss = (eq * 1000.0 + sh * 100.0) / args.accum
+        loss.backward()
+        assert ctx.grad is not None and torch.isfinite(ctx.grad).all()
+
+    def timed_rate(ctx, reps):
+        micro_iteration(ctx)                         # warm-up (allocator, thread pool, first-touch)
+        t0 = time.time()
+        for i in range(reps):
+            micro_iteration(ctx)
+            print(f"cpu_baseline: N={ctx.shape[1]} image {i + 1}/{reps} {time.time() - t0:.1f} s", file=sys.stderr,
+                  flush=True)
+        return reps / (time.time() - t0), time.time() - t0
+
+    rate, dt = timed_rate(context, 2)
+    # BASELINE.md's small figure: the same micro-iteration at N = 10 tokens (configs[0] scale)
+    ctx10 = torch.randn(1, 10, 768).requires_grad_(True)
+    rate10, dt10 = timed_rate(ctx10, 2)
     cpu = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
@@ -192,9 +222,13 @@ def cpu_baseline(args):
                 break
     except OSError:
         pass
-    return {"value": 1.0 / dt, "unit": "images/sec", "cores": threads, "kind": "port",
-            "sample": f"1 image = 1 token-opt micro-iteration (2 captures + select + losses + backward), "
-                      f"N={args.tokens}, {args.res}²; torch-CPU SD-1.5 UNet/VAE + numpy oracle; {dt:.1f} s on {cpu}"}
+    return {"value": rate, "unit": "images/sec", "cores": threads, "kind": "port", "nproc": nproc,
+            "cpu_model": cpu, "value_N10": rate10,
+            "sample": f"2 timed images after 1 warm-up, 1 image = 1 token-opt micro-iteration (2 captures + select + "
+                      f"losses + backward), N={args.tokens}, {args.res}²; torch-CPU SD-1.5 UNet/VAE + numpy oracle "
+                      f"({threads} threads: OMP_NUM_THREADS if set, else the CPUs this process may use; nproc "
+                      f"{nproc}, affinity {allowed}); {dt:.1f} s; "
+                      f"value_N10 = the same at N=10 tokens ({dt10:.1f} s)"}
 
 
 # ------------------------------------------------------------------------------ GPU bench
@@ -265,7 +299,8 @@ def main():
     opt = TokenOptimizer(ldm, controllers, context, accum=args.accum, device=dev)
     data = SyntheticDataset(n=16, size=args.res, seed=rank)
     imgs = [data[i]["img"][None].to(dev) for i in range(len(data))]
-    timer = KernelTimer(["skp_aggregate", "skp_capture_fwd", "skp_capture_bwd"])
+    timer = KernelTimer(["skp_aggregate", "skp_capture_fwd", "skp_capture_bwd", "skp_capture_maps_fwd",
+                         "skp_capture_maps_bwd"])
     ops.set_kernel_timer(timer)
 
     counter = [0]
@@ -313,30 +348,60 @@ def main():
     images = world * args.accum * args.steps
     value = images / elapsed
 
-    agg = timer.summary("skp_aggregate")
+    # roofline: the dominant hot-path kernel, skp_capture_maps_fwd (fused capture + per-image
+    # aggregate), is VALU-bound (bicubic taps + exp + normalise per (pixel, token, layer, head));
+    # its HBM traffic is reported beside it.  With SKP_FUSED_MAPS=0 the r01 path's HBM-bound
+    # skp_aggregate is reported instead.
+    from stablekeypoints_amd.ops import capture_maps_flops, capture_maps_bwd_flops
+    sizes = (16, 16, 16, 32) if args.model == "sd15" else None   # SD-1.5 captured layers (up_blocks 1, 2)
     roof = None
+    extra = {}
+    fw = timer.summary("skp_capture_maps_fwd")
+    bw = timer.summary("skp_capture_maps_bwd")
+    valu_json = os.path.join(REPO, "profiles", "pmc_valu.json")
+    if fw and sizes is not None:
+        B2 = 2 * mb   # each pass captures the images and their warps
+        flops = capture_maps_flops(B2, 8, args.tokens, args.upsample_res, sizes)
+        t = fw["avg_ms"] * 1e-3
+        traffic = _pmc_record(args.traffic, "skp_capture_maps_fwd", ("algorithmic_bytes_per_launch", fw["bytes_per_launch"]),
+                              "hbm_bytes_per_launch")
+        roof = {"kernel": "skp_capture_maps_fwd", "bound": "valu", "achieved": flops / t / 1e12,
+                "peak": VALU_F32_PEAK / 1e12, "unit": "TFLOP/s", "frac": flops / t / VALU_F32_PEAK,
+                "traffic": traffic, "avg_launch_ms": fw["avg_ms"], "launches": fw["launches"],
+                "algorithmic_flop_per_launch": flops, "algorithmic_bytes_per_launch": fw["bytes_per_launch"],
+                "hbm_achieved_GBps": fw["bytes_per_launch"] / t / 1e9,
+                "hbm_frac": fw["bytes_per_launch"] / t / HBM_PEAK,
+                "valu_busy_pmc": _pmc_record(valu_json, "skp_capture_maps_fwd", ("flop_per_launch", flops), "valu_busy"),
+                "flop_model": "15 FLOP per (image, head, layer, pixel, token) + 8 per (row, low-res column, token); "
+                              "ops.capture_maps_flops"}
+    elif fw:
+        extra["skp_capture_maps_fwd"] = {"avg_ms": fw["avg_ms"], "launches": fw["launches"]}
+    if bw and sizes is not None:
+        B2 = 2 * mb
+        flops = capture_maps_bwd_flops(B2, 8, args.tokens, args.upsample_res, sizes)
+        t = bw["avg_ms"] * 1e-3
+        extra["skp_capture_maps_bwd"] = {"avg_ms": bw["avg_ms"], "launches": bw["launches"],
+                                         "TFLOP/s": flops / t / 1e12, "valu_frac": flops / t / VALU_F32_PEAK,
+                                         "GB/s_algorithmic": bw["bytes_per_launch"] / t / 1e9}
+    agg = timer.summary("skp_aggregate")
     if agg:
         achieved = agg["bytes_per_launch"] / (agg["avg_ms"] * 1e-3)
-        traffic = None
-        if os.path.exists(args.traffic):
-            try:
-                rec_t = json.load(open(args.traffic)).get("skp_aggregate", {})
-                # PMC bytes apply only to the workload they were measured on
-                if rec_t.get("algorithmic_bytes_per_launch") == agg["bytes_per_launch"]:
-                    traffic = rec_t.get("hbm_bytes_per_launch")
-            except (OSError, ValueError):
-                traffic = None
-        roof = {"kernel": "skp_aggregate", "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
-                "unit": "GB/s", "frac": achieved / HBM_PEAK, "traffic": traffic,
-                "avg_launch_ms": agg["avg_ms"], "launches": agg["launches"],
-                "algorithmic_bytes_per_launch": agg["bytes_per_launch"],
-                "frac_of_measured_copy": achieved / HBM_MEASURED_COPY}
-    extra = {}
+        traffic = _pmc_record(args.traffic, "skp_aggregate", ("algorithmic_bytes_per_launch", agg["bytes_per_launch"]),
+                              "hbm_bytes_per_launch")
+        rec_a = {"kernel": "skp_aggregate", "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
+                 "unit": "GB/s", "frac": achieved / HBM_PEAK, "traffic": traffic,
+                 "avg_launch_ms": agg["avg_ms"], "launches": agg["launches"],
+                 "algorithmic_bytes_per_launch": agg["bytes_per_launch"],
+                 "frac_of_measured_copy": achieved / HBM_MEASURED_COPY}
+        if roof is None:
+            roof = rec_a
+        else:
+            extra["skp_aggregate"] = rec_a
     for k in ("skp_capture_fwd", "skp_capture_bwd"):
-        s = timer.summary(k)
-        if s:
-            extra[k] = {"avg_ms": s["avg_ms"], "launches": s["launches"],
-                        "GB/s_algorithmic": s["bytes_per_launch"] / (s["avg_ms"] * 1e-3) / 1e9}
+        s_ = timer.summary(k)
+        if s_:
+            extra[k] = {"avg_ms": s_["avg_ms"], "launches": s_["launches"],
+                        "GB/s_algorithmic": s_["bytes_per_launch"] / (s_["avg_ms"] * 1e-3) / 1e9}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.model == "sd15":

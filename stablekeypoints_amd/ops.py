@@ -186,6 +186,22 @@ def capture_maps_bytes(B, H, N, R, sizes):
     return 4 * (sum(B * H * s * s * N for s in sizes) + B * N * RR + len(sizes) * B * H * RR * 2)
 
 
+def capture_maps_flops(B, H, N, R, sizes):
+    """Algorithmic fp32 VALU work of one skp_capture_maps_fwd launch: per
+    (image, head, layer, pixel, token) 15 FLOP — horizontal bicubic 4 multiply-adds (8), softmax
+    max 1 + (z − m)·log2e as an FMA 2 + exp 1 + Σ 1, normalise-and-accumulate FMA 2 — and per
+    (image, head, layer, output row, low-res column, token) 8 for the vertical bicubic pass."""
+    return sum(B * H * N * (15 * R * R + 8 * R * s) for s in sizes)
+
+
+def capture_maps_bwd_flops(B, H, N, R, sizes):
+    """Algorithmic fp32 VALU work of one skp_capture_maps_bwd call: per (image, head, layer,
+    pixel, token) 24 FLOP — rebuild the softmax row (taps 8, exp argument 2, exp 1, ×1/Σ 1), a·g 1,
+    Σ a·g 1, dZ = a·g − a·dot 2, horizontal adjoint 4 multiply-adds (8) — and per (row, low-res
+    column, token) 8 each for the vertical pass and the vertical adjoint."""
+    return sum(B * H * N * (24 * R * R + 16 * R * s) for s in sizes)
+
+
 def capture_maps_bwd_bytes(B, H, N, R, sizes):
     """Algorithmic HBM bytes of one skp_capture_maps_bwd call: the map gradient read once (and
     its pixel-major copy written and read once), every z_low and stats read once, the row

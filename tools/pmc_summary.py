@@ -23,7 +23,8 @@ def main():
             k = r["Kernel_Name"]
             if args.match and args.match not in k:
                 continue
-            vals[k.split("(")[0][:90]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            name = k.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0][:90]
+            vals[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for k, cs in vals.items():
         m = {c: sum(v) / len(v) for c, v in cs.items()}
         print(k)

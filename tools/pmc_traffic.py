@@ -30,7 +30,8 @@ def main():
     ap.add_argument("--kernel", default="aggregate_kernel")
     ap.add_argument("--name", default="skp_aggregate")
     ap.add_argument("--algorithmic", type=int, default=1081344000)
-    ap.add_argument("--out", default=None)
+    ap.add_argument("--out", default=None, help="JSON file to update (other kernels' entries are kept)")
+    ap.add_argument("--workload", default="tools/kbench.py --only agg (N=500, R=128, 4 distinct layers x 8 heads)")
     args = ap.parse_args()
     f = values(args.fetch, args.kernel, "FETCH_SIZE")
     w = values(args.write, args.kernel, "WRITE_SIZE")
@@ -45,16 +46,20 @@ def main():
         "write_size_kb_raw_median": wm,
         "algorithmic_bytes_per_launch": args.algorithmic,
         "traffic_over_algorithmic": (fetch + write) / args.algorithmic,
-        "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes (tools/gpu_prof.sh) on "
-                  "tools/kbench.py --only agg (N=500, R=128, 4 distinct layers x 8 heads); FETCH_SIZE (KB) x1024 x2 "
+        "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes on "
+                  f"{args.workload}; FETCH_SIZE (KB) x1024 x2 "
                   "(gfx950: FETCH_SIZE reports half of wide coalesced reads, MI355X_MICROARCH.md HBM section), "
                   "WRITE_SIZE (KB) x1024; median over launches (tools/pmc_traffic.py)",
         "launches": min(len(f), len(w)),
     }}
-    text = json.dumps(res, indent=1)
-    print(text)
+    print(json.dumps(res, indent=1))
     if args.out:
-        open(args.out, "w").write(text + "\n")
+        try:
+            allrec = json.load(open(args.out))
+        except (OSError, ValueError):
+            allrec = {}
+        allrec.update(res)
+        open(args.out, "w").write(json.dumps(allrec, indent=1) + "\n")
 
 
 if __name__ == "__main__":

@@ -1,0 +1,49 @@
+"""VALU-busy of one kernel from a rocprofv3 PMC pass (SQ_ACTIVE_INST_VALU, GRBM_GUI_ACTIVE), merged
+into a JSON record keyed by kernel (dev tool; bench.py reports it beside the VALU roofline).
+
+VALU busy = 4·SQ_ACTIVE_INST_VALU (quad-cycles, summed over the chip) / (1024 SIMDs · GRBM_GUI_ACTIVE/8)
+(GRBM_GUI_ACTIVE is summed over the 8 XCDs); median over launches.
+
+usage: python tools/pmc_valu.py COUNTERS.csv --kernel capture_maps_kernel --name skp_capture_maps_fwd \
+           --flop 34078720000 --out profiles/pmc_valu.json
+"""
+import argparse
+import csv
+import collections
+import json
+import statistics
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("csv")
+    ap.add_argument("--kernel", required=True)
+    ap.add_argument("--name", required=True)
+    ap.add_argument("--flop", type=int, required=True, help="algorithmic FLOP per launch (ops.capture_maps_flops)")
+    ap.add_argument("--workload", default="")
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    per = collections.defaultdict(dict)
+    for r in csv.DictReader(open(args.csv)):
+        if args.kernel in r["Kernel_Name"]:
+            per[r["Dispatch_Id"]][r["Counter_Name"]] = float(r["Counter_Value"])
+    busy = [4 * d["SQ_ACTIVE_INST_VALU"] / (1024 * d["GRBM_GUI_ACTIVE"] / 8) for d in per.values()
+            if "SQ_ACTIVE_INST_VALU" in d and d.get("GRBM_GUI_ACTIVE")]
+    if not busy:
+        raise SystemExit(f"no counters for {args.kernel}")
+    rec = {args.name: {"valu_busy": statistics.median(busy), "launches": len(busy), "flop_per_launch": args.flop,
+                       "method": "rocprofv3 --pmc SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE; 4*ACTIVE_INST_VALU / "
+                                 "(1024 SIMDs * GRBM_GUI_ACTIVE/8), median over launches (tools/pmc_valu.py)",
+                       "workload": args.workload}}
+    print(json.dumps(rec, indent=1))
+    if args.out:
+        try:
+            allrec = json.load(open(args.out))
+        except (OSError, ValueError):
+            allrec = {}
+        allrec.update(rec)
+        open(args.out, "w").write(json.dumps(allrec, indent=1) + "\n")
+
+
+if __name__ == "__main__":
+    main()
