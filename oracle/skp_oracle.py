@@ -370,35 +370,50 @@ def theta_inverse(theta):
     return np.linalg.inv(aug)[:, :2, :].astype(np.float32)
 
 
+def _fma32(a, b, c):
+    """float32 fused multiply-add (the product is exact in float64)."""
+    return (np.asarray(a, np.float64) * np.asarray(b, np.float64) + np.asarray(c, np.float64)).astype(np.float32)
+
+
 def _base_coords(n):
     """affine_grid base coordinates, align_corners=False: linspace(-1,1,n)·(n-1)/n."""
     if n == 1:
         return np.zeros(1, np.float32)
-    step = np.float32(2.0 / (n - 1))
+    # torch-CPU linspace rounding (bit-equal to torch.linspace, tests/test_oracle_golden.py):
+    # fma(i, step, -1) for the first half, fma(-(n-1-i), step, 1) for the second
+    step = np.float32(np.float32(2.0) / np.float32(n - 1))
     i = np.arange(n)
-    lin = np.where(i < n // 2, np.float32(-1.0) + i.astype(np.float32) * step,
-                   np.float32(1.0) - (n - 1 - i).astype(np.float32) * step).astype(np.float32)
+    lin = np.where(i < n // 2, _fma32(i, step, -1.0), _fma32(-(n - 1 - i), step, 1.0)).astype(np.float32)
     return ((lin * np.float32(n - 1)) / np.float32(n)).astype(np.float32)
 
 
 def _grid(theta, H, W):
+    """Sampling coordinates of F.affine_grid + grid_sample as torch-CPU rounds them (the reference
+    warps images on the CPU, optimize.py:386): the affine_grid bmm of [x, y, 1] by θᵀ as
+    fma(y, θ1, x·θ0) + θ2 (bit-equal to F.affine_grid, checked in tests/test_oracle_golden.py) and
+    the CPU grid sampler's unnormalisation fma(g + 1, n/2, −0.5)."""
     xs = _base_coords(W)[None, None, :]
     ys = _base_coords(H)[None, :, None]
     t = theta.astype(np.float32)
-    gx = xs * t[:, 0, 0, None, None] + ys * t[:, 0, 1, None, None] + t[:, 0, 2, None, None]
-    gy = xs * t[:, 1, 0, None, None] + ys * t[:, 1, 1, None, None] + t[:, 1, 2, None, None]
-    ix = ((gx + F32(1.0)) * F32(W) - F32(1.0)) / F32(2.0)
-    iy = ((gy + F32(1.0)) * F32(H) - F32(1.0)) / F32(2.0)
+    gx = _fma32(ys, t[:, 0, 1, None, None], xs * t[:, 0, 0, None, None]) + t[:, 0, 2, None, None]
+    gy = _fma32(ys, t[:, 1, 1, None, None], xs * t[:, 1, 0, None, None]) + t[:, 1, 2, None, None]
+    ix = _fma32(gx + F32(1.0), F32(W / 2), -0.5)
+    iy = _fma32(gy + F32(1.0), F32(H / 2), -0.5)
     return ix.astype(np.float32), iy.astype(np.float32)
 
 
 def _taps(ix, iy, H, W):
-    """grid_sample bilinear taps (nw, ne, sw, se) with ATen's weight formulas."""
+    """grid_sample bilinear taps (nw, ne, sw, se) with the CPU sampler's weight formulas:
+    w = ix − floor(ix), e = 1 − w, n = iy − floor(iy), s = 1 − n; nw = s·e, ne = s·w, sw = n·e,
+    se = n·w (summed in that order by the callers)."""
     x0f = np.floor(ix).astype(np.float32)
     y0f = np.floor(iy).astype(np.float32)
     x1f, y1f = x0f + F32(1.0), y0f + F32(1.0)
-    wts = [((y0f, x0f), (x1f - ix) * (y1f - iy)), ((y0f, x1f), (ix - x0f) * (y1f - iy)),
-           ((y1f, x0f), (x1f - ix) * (iy - y0f)), ((y1f, x1f), (ix - x0f) * (iy - y0f))]
+    we = (ix - x0f).astype(np.float32)
+    ee = (F32(1.0) - we).astype(np.float32)
+    wn = (iy - y0f).astype(np.float32)
+    ws = (F32(1.0) - wn).astype(np.float32)
+    wts = [((y0f, x0f), ws * ee), ((y0f, x1f), ws * we), ((y1f, x0f), wn * ee), ((y1f, x1f), wn * we)]
     out = []
     for (yf, xf), w in wts:
         yy, xx = yf.astype(np.int64), xf.astype(np.int64)

@@ -186,14 +186,14 @@ __device__ __forceinline__ Taps2 bilinear_taps(int dst, int n_in, int n_out) {
   return r;
 }
 
-// affine_grid base coordinate (align_corners=False): linspace(-1, 1, n)[i] * (n-1)/n,
-// with linspace evaluated as ATen does (from the start for the first half, from the end
-// for the second half).
+// affine_grid base coordinate (align_corners=False): linspace(-1, 1, n)[i] * (n-1)/n, with
+// linspace rounded as torch-CPU's kernel does (measured bit-equal against torch.linspace for
+// n = 100, 128, 512): fma(i, step, −1) for the first half, fma(−(n−1−i), step, 1) for the second.
 __device__ __forceinline__ float affine_base(int i, int n) {
   if (n <= 1) return 0.0f;
-  const float step = 2.0f / (float)(n - 1);
-  const float lin = (i < n / 2) ? (-1.0f + step * (float)i) : (1.0f - step * (float)(n - 1 - i));
-  return (lin * (float)(n - 1)) / (float)n;  // ATen: range * (n - 1) / n
+  const float step = __fdiv_rn(2.0f, (float)(n - 1));
+  const float lin = (i < n / 2) ? __fmaf_rn((float)i, step, -1.0f) : __fmaf_rn(-(float)(n - 1 - i), step, 1.0f);
+  return __fdiv_rn(__fmul_rn(lin, (float)(n - 1)), (float)n);  // ATen: range * (n - 1) / n
 }
 
 // Correctly rounded float sqrt via double (exact for finite floats).

@@ -16,21 +16,28 @@ struct Bilin {
   float w[4];  // nw, ne, sw, se
 };
 
+// Rounding follows torch-CPU exactly (the reference warps images on the CPU, optimize.py:386, and
+// its goldens are CPU runs): affine_grid's bmm of [x, y, 1] by θᵀ rounds as
+// fma(y, θ1, x·θ0) + θ2 (measured against F.affine_grid: bit-equal on every grid point), the CPU
+// grid sampler unnormalises as fma(g + 1, n/2, −0.5) and forms the bilinear weights from
+// w = ix − floor(ix), e = 1 − w (nw = s·e, ne = s·w, sw = n·e, se = n·w), and the sample as
+// ((v_nw·nw + v_ne·ne) + v_sw·sw) + v_se·se without fused multiply-adds.
 __device__ __forceinline__ Bilin grid_point(const float* th, int y, int x, int H, int W) {
   const float bx = affine_base(x, W), by = affine_base(y, H);
-  const float gx = bx * th[0] + by * th[1] + th[2];
-  const float gy = bx * th[3] + by * th[4] + th[5];
-  const float ix = ((gx + 1.0f) * (float)W - 1.0f) / 2.0f;
-  const float iy = ((gy + 1.0f) * (float)H - 1.0f) / 2.0f;
+  const float gx = __fadd_rn(__fmaf_rn(by, th[1], __fmul_rn(bx, th[0])), th[2]);
+  const float gy = __fadd_rn(__fmaf_rn(by, th[4], __fmul_rn(bx, th[3])), th[5]);
+  const float ix = __fmaf_rn(__fadd_rn(gx, 1.0f), (float)W * 0.5f, -0.5f);
+  const float iy = __fmaf_rn(__fadd_rn(gy, 1.0f), (float)H * 0.5f, -0.5f);
   const float x0 = floorf(ix), y0 = floorf(iy);
-  const float x1 = x0 + 1.0f, y1 = y0 + 1.0f;
+  const float we = __fsub_rn(ix, x0), ee = __fsub_rn(1.0f, we);   // distance to the west / east side
+  const float wn = __fsub_rn(iy, y0), ws = __fsub_rn(1.0f, wn);   // distance to the north / south side
   Bilin b;
   b.x0 = (int)x0;
   b.y0 = (int)y0;
-  b.w[0] = (x1 - ix) * (y1 - iy);
-  b.w[1] = (ix - x0) * (y1 - iy);
-  b.w[2] = (x1 - ix) * (iy - y0);
-  b.w[3] = (ix - x0) * (iy - y0);
+  b.w[0] = __fmul_rn(ws, ee);
+  b.w[1] = __fmul_rn(ws, we);
+  b.w[2] = __fmul_rn(wn, ee);
+  b.w[3] = __fmul_rn(wn, we);
   return b;
 }
 
@@ -39,7 +46,8 @@ __device__ __forceinline__ float sample(const float* __restrict__ p, const Bilin
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int xx = b.x0 + (k & 1), yy = b.y0 + (k >> 1);
-    if (xx >= 0 && xx < W && yy >= 0 && yy < H) out += p[yy * W + xx] * b.w[k];
+    const float v = (xx >= 0 && xx < W && yy >= 0 && yy < H) ? p[yy * W + xx] : 0.0f;
+    out = k == 0 ? __fmul_rn(v, b.w[0]) : __fadd_rn(out, __fmul_rn(v, b.w[k]));
   }
   return out;
 }

@@ -197,15 +197,17 @@ def test_losses_vs_golden():
         l.backward()
         assert np.allclose(N(l), g[f"sharp_ns{ns}"], rtol=1e-5)
         assert np.allclose(N(A.grad), g[f"dA_sharp_ns{ns}"], atol=1e-9, rtol=1e-4)
-    assert np.allclose(N(ops.affine_warp(T(g["img"]), T(g["theta"]))), g["warped"], atol=1e-5)
+    dw = float(np.abs(N(ops.affine_warp(T(g["img"]), T(g["theta"]))) - g["warped"]).max())
+    assert dw <= 1e-6, dw   # torch-CPU grid rounding reproduced (tests/test_oracle_golden.py)
     ti = O.theta_inverse(g["theta"])
     A = T(g["A"]).requires_grad_(True)
     At = T(g["At"]).requires_grad_(True)
     l = ops.equivariance_loss_single(A, At, T(ti[1]))
     l.backward()
-    assert np.allclose(N(l), g["equiv"], rtol=1e-4)
-    assert np.allclose(N(A.grad), g["dA_equiv"], atol=1e-8, rtol=1e-3)
-    assert np.allclose(N(At.grad), g["dAt_equiv"], atol=1e-8, rtol=1e-3)
+    print(f"\nwarp max|Δ| {dw:.1e}, equivariance loss rel {abs(float(l) / float(g['equiv']) - 1):.1e}")
+    assert np.allclose(N(l), g["equiv"], rtol=1e-5)
+    assert np.allclose(N(A.grad), g["dA_equiv"], atol=1e-8, rtol=1e-4)
+    assert np.allclose(N(At.grad), g["dAt_equiv"], atol=1e-8, rtol=1e-4)
 
 
 def test_affine_warp_adjoint():
@@ -286,9 +288,10 @@ def test_token_opt_step_tiny_vs_reference():
     assert np.allclose(N(lat0), g["latent0"], atol=1e-4)
     Tr = RandomAffineWithInverse(degrees=15, scale=(0.8, 1.0), translate=(0.25, 0.25))
     timg = Tr(T(g["img"]), theta=torch.from_numpy(g["theta"]))
-    # grid coordinates differ from torch-CPU's bmm by rounding (~1e-6 px); on a random
-    # image that moves a few samples by ~1e-5 (the numpy oracle differs by 1.4e-5 too)
-    assert np.allclose(N(timg), g["timg"], atol=1e-4)
+    # skp_affine_warp rounds the grid as torch-CPU does (fma(y, θ1, x·θ0) + θ2, the CPU sampler's
+    # fma(g + 1, n/2, −0.5)): the reference's warp to 2 ulp
+    dtimg = float(np.abs(N(timg) - g["timg"]).max())
+    assert dtimg <= 1e-6, dtimg
     # The UNet passes start from the reference's latents (identical inputs): the VAE's conv
     # algorithms differ from torch-CPU's at ~1e-6, which is checked just above.
     maps = ptp_utils.run_and_find_attn(ldm, T(g["latent0"]), ctx, **kw)
@@ -302,8 +305,14 @@ def test_token_opt_step_tiny_vs_reference():
     eq = optimize.equivariance_loss(maps[0][idx], maps_t[0][idx][None], Tr, 0)
     loss = (eq * 1000.0 + sharp * 100.0) / 4
     loss.backward()
-    assert np.allclose(N(sharp), g["sharp"], rtol=1e-4) and np.allclose(N(eq), g["eq"], rtol=1e-3)
-    assert np.allclose(N(ctx.grad), g["dctx"], rtol=1e-3, atol=1e-7)
+    rs, re = abs(float(sharp) / float(g["sharp"]) - 1), abs(float(eq) / float(g["eq"]) - 1)
+    dc = N(ctx.grad)
+    rg = float(np.linalg.norm(dc - g["dctx"]) / np.linalg.norm(g["dctx"]))
+    print(f"\nstep vs reference: timg max|Δ| {dtimg:.1e}, sharp rel {rs:.1e}, eq rel {re:.1e}, "
+          f"context.grad rel-L2 {rg:.1e}")
+    assert rs <= 1e-4 and re <= 1e-4, (rs, re)   # north_star: losses within 1e-4
+    assert rg <= 1e-4, rg
+    assert np.allclose(dc, g["dctx"], rtol=1e-4, atol=1e-7)
 
 
 # ----------------------------------------------------------------------------- fused per-image path
