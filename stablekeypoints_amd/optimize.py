@@ -128,6 +128,12 @@ class TokenOptimizer:
         self.transform = RandomAffineWithInverse(degrees=augment_degrees, scale=augment_scale,
                                                  translate=augment_translate)
         self.world, self.rank = _world()
+        if self.world > 1:
+            # every rank must start from rank 0's embedding: the ranks apply identical Adam
+            # steps to identical all-reduced gradients, so one broadcast keeps them in lockstep
+            import torch.distributed as dist
+            with torch.no_grad():
+                dist.broadcast(self.context, src=0)
         self._prefetched = []      # FIFO of (key, thetas, latents, event) from prefetch()
         self._side = None
         self.reset_running()
@@ -144,7 +150,7 @@ class TokenOptimizer:
         if self._side is None:
             self._side = torch.cuda.Stream(device=self.device)
         batch = torch.cat(list(images))
-        thetas = self.transform.draw_theta(len(images))
+        thetas = self.draw_thetas(len(images))
         main = torch.cuda.current_stream(self.device)
         self._side.wait_stream(main)
         with torch.cuda.stream(self._side), torch.no_grad():
@@ -154,6 +160,19 @@ class TokenOptimizer:
             ev = torch.cuda.Event()
             ev.record(self._side)
         self._prefetched.append((key, thetas, lat, ev))
+
+    def draw_thetas(self, k):
+        """Warps for this rank's next ``k`` micro-iterations, drawn as the reference draws them.
+
+        The reference applies the transform to each micro-iteration's DataParallel batch of
+        ``num_gpus`` images (optimize.py:386), so its CPU generator yields, per micro-iteration,
+        one theta per replica in replica order; replica r uses theta r (optimize.py:420-424).
+        Every rank draws the whole sequence (k·world thetas, same CPU seed on every rank) and keeps
+        its own column, so the run is the same augmentation stream at any world size."""
+        if self.world == 1:
+            return self.transform.draw_theta(k)
+        th = self.transform.draw_theta(k * self.world)
+        return th.reshape(k, self.world, 2, 3)[:, self.rank].contiguous()
 
     def _take_prefetched(self, images):
         key = tuple(id(t) for t in images)
@@ -207,7 +226,7 @@ class TokenOptimizer:
             self.transform.last_params = {"theta": thetas.detach().cpu().float()}
         else:
             batch = torch.cat(list(images))
-            transformed = self.transform(batch)          # draws k thetas, image order
+            transformed = self.transform(batch, theta=self.draw_thetas(k))   # k thetas, image order
             inputs = torch.cat([batch, transformed])
         maps = ptp_utils.run_and_find_attn_per_image(
             self.ldm, inputs, self.context, noise_level=self.kw["noise_level"],
@@ -232,13 +251,13 @@ class TokenOptimizer:
     def image_loss(self, image):
         """optimize.py:372-437 for one image: (weighted loss, equivariance, sharpening, indices)."""
         if self.batch_captures:
-            transformed_img = self.transform(image)
+            transformed_img = self.transform(image, theta=self.draw_thetas(1))
             attn_map, attention_map_transformed = ptp_utils.run_and_find_attn_per_image(
                 self.ldm, torch.cat([image, transformed_img]), self.context, noise_level=self.kw["noise_level"],
                 device=self.device, layers=self.kw["layers"], controllers=self.controllers)[0]
         else:
             attn_map = ptp_utils.run_and_find_attn(self.ldm, image, self.context, **self.kw)[0]
-            transformed_img = self.transform(image)
+            transformed_img = self.transform(image, theta=self.draw_thetas(1))
             attention_map_transformed = ptp_utils.run_and_find_attn(self.ldm, transformed_img, self.context,
                                                                      **self.kw)[0]
         return self._map_loss(attn_map, attention_map_transformed, 0)
@@ -289,6 +308,40 @@ class TokenOptimizer:
         return rec
 
 
+class ReplicaSampler:
+    """The reference's ``DataLoader(dataset, batch_size=num_gpus, shuffle=True, drop_last=True)``
+    (optimize.py:356-368) split over ranks: each epoch is one permutation shared by every rank
+    (one seed, broadcast from rank 0 when not given), cut into groups of ``num_gpus`` with the
+    remainder dropped; micro-iteration j gives rank r element r of group j, i.e. exactly the image
+    DataParallel replica r receives.  The ranks' images are therefore a partition of each group."""
+
+    def __init__(self, n, num_gpus, rank, seed=None):
+        if n < num_gpus:
+            raise ValueError(f"dataset of {n} images cannot fill a group of num_gpus={num_gpus} (drop_last)")
+        if seed is None:
+            seed = int(torch.randint(0, 2 ** 31 - 1, (1,)))
+            if num_gpus > 1:
+                import torch.distributed as dist
+                t = torch.tensor([seed], dtype=torch.int64)
+                if dist.get_backend() == "nccl":
+                    t = t.cuda()
+                dist.broadcast(t, src=0)
+                seed = int(t.item())
+        self.n, self.g, self.rank = n, num_gpus, rank
+        self.gen = torch.Generator().manual_seed(int(seed))
+        self.groups = 0
+        self.pos = 0
+
+    def next(self):
+        if self.pos >= self.groups:
+            self.order = torch.randperm(self.n, generator=self.gen)
+            self.groups = self.n // self.g
+            self.pos = 0
+        i = int(self.order[self.pos * self.g + self.rank])
+        self.pos += 1
+        return i
+
+
 def optimize_embedding(ldm, top_k_strategy="entropy", wandb_log=True, context=None, device="cuda", num_steps=2000,
                        from_where=("down_cross", "mid_cross", "up_cross"), upsample_res=256, layers=(0, 1, 2, 3, 4, 5),
                        lr=5e-3, noise_level=-1, num_tokens=1000, top_k=10, augment_degrees=30,
@@ -298,7 +351,9 @@ def optimize_embedding(ldm, top_k_strategy="entropy", wandb_log=True, context=No
                        controllers=None, validation=False, num_subjects=1, dataset=None, log=None, seed=None):
     """optimize.py:269-475.  Extra keyword conveniences: ``dataset`` (object yielding
     {"img": (3,H,W)}; overrides dataset_name), ``log`` (callable receiving each
-    optimiser step's metrics instead of print), ``seed`` (sampler seed; rank added)."""
+    optimiser step's metrics instead of print), ``seed`` (shuffle seed, the same on every rank;
+    default: drawn on rank 0 and broadcast).  Rank r processes replica r's images
+    (``ReplicaSampler``) with replica r's warps (``TokenOptimizer.draw_thetas``)."""
     world, rank = _world()
     num_gpus = world   # one process per GPU: the replica count is the world size
     if dataset is None:
@@ -315,18 +370,10 @@ def optimize_embedding(ldm, top_k_strategy="entropy", wandb_log=True, context=No
                          augment_degrees=augment_degrees, augment_scale=augment_scale,
                          augment_translate=augment_translate, device=device)
     n_iter = int(num_steps * accum)   # batch_size < num_gpus gives 0 iterations, as in the reference
-    base = seed if seed is not None else int(torch.randint(0, 2 ** 31 - 1, (1,)))
-    sampler_gen = torch.Generator().manual_seed(base + rank)
-    order = torch.randperm(len(dataset), generator=sampler_gen)
-    state = {"order": order, "pos": 0}
+    sampler = ReplicaSampler(len(dataset), num_gpus, rank, seed)
 
     def next_image():
-        if state["pos"] >= len(state["order"]):
-            state["order"] = torch.randperm(len(dataset), generator=sampler_gen)
-            state["pos"] = 0
-        img = dataset[int(state["order"][state["pos"]])]["img"][None].to(device, non_blocking=True)
-        state["pos"] += 1
-        return img
+        return dataset[sampler.next()]["img"][None].to(device, non_blocking=True)
 
     def next_batch(n):
         return [next_image() for _ in range(n)]

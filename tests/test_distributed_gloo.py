@@ -197,3 +197,142 @@ def test_two_rank_eval_stages_equal_two_replicas_in_one_process(monkeypatch):
         idx, tta = torch.from_numpy(idx), torch.from_numpy(tta)
         assert torch.equal(idx, ref_idx), (rank, idx, ref_idx)
         assert torch.allclose(tta, ref_tta, rtol=1e-6, atol=1e-7), rank
+
+
+# ---------------------------------------------------------------------------- data order + warps
+# optimize.py:356-368 draws each micro-iteration's num_gpus images from ONE shuffled
+# DataLoader(batch_size=num_gpus, drop_last=True); replica r gets image r and warp r of that
+# batch.  ReplicaSampler / TokenOptimizer.draw_thetas must give rank r exactly those.
+def _order_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from stablekeypoints_amd.optimize import ReplicaSampler, TokenOptimizer
+        from stablekeypoints_amd.invertable_transform import RandomAffineWithInverse
+        torch.manual_seed(1234 + 17 * rank)   # different CPU states: the seed must come from rank 0
+        s = ReplicaSampler(7, world, rank)     # seed drawn on rank 0 and broadcast
+        picks = [s.next() for _ in range(9)]  # 3 groups per epoch (drop_last), 3 epochs
+        torch.manual_seed(99)                  # draws from the shared CPU stream, as main.py seeds
+        opt = TokenOptimizer.__new__(TokenOptimizer)
+        opt.world, opt.rank = world, rank
+        opt.transform = RandomAffineWithInverse(degrees=15, scale=(0.8, 1.0), translate=(0.25, 0.25))
+        th = torch.cat([opt.draw_thetas(2), opt.draw_thetas(1)])
+        seed = s.gen.initial_seed()
+        q.put((rank, picks, th.numpy().copy(), seed))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_sampler_partitions_each_replica_batch_and_warps_follow_replicas():
+    from stablekeypoints_amd.optimize import ReplicaSampler
+    from stablekeypoints_amd.invertable_transform import RandomAffineWithInverse
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_order_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=120) for _ in range(world)])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    seeds = {o[3] for o in out}
+    assert len(seeds) == 1, "ranks shuffled with different seeds"
+    # the single-process DataLoader view: one permutation per epoch, groups of 2, remainder dropped
+    gen = torch.Generator().manual_seed(seeds.pop())
+    groups = []
+    for _ in range(3):
+        perm = torch.randperm(7, generator=gen).tolist()
+        groups += [perm[2 * i:2 * i + 2] for i in range(3)]
+    for rank, picks, _, _ in out:
+        assert picks == [g[rank] for g in groups], (rank, picks, groups)
+    for j in range(9):   # each group is split, never duplicated, across the ranks
+        assert {out[0][1][j], out[1][1][j]} == set(groups[j])
+    # warps: the reference draws num_gpus thetas per micro-iteration; replica r uses theta r
+    torch.manual_seed(99)
+    ref = RandomAffineWithInverse(degrees=15, scale=(0.8, 1.0), translate=(0.25, 0.25)).draw_theta(3 * world)
+    ref = ref.reshape(3, world, 2, 3)
+    for rank, _, th, _ in out:
+        assert torch.equal(torch.from_numpy(th), ref[:, rank]), rank
+    assert ReplicaSampler(5, 1, 0, seed=3).next() == int(torch.randperm(5, generator=torch.Generator().manual_seed(3))[0])
+
+
+# ---------------------------------------------------------------------------- real step, 2 ranks on one GPU
+def _tiny_opt(accum, dev, ctx_shift=0.0):
+    """TokenOptimizer on the toy-width SD-1.5 with batching-independent noise (a function of the
+    latent), so one image's pass gives the same maps whatever else shares the batch."""
+    import recipes
+    from stablekeypoints_amd.optimize import TokenOptimizer
+    from stablekeypoints_amd.optimize_token import load_ldm
+    from stablekeypoints_amd.sd import TINY_CONFIG
+    ldm, ctls, _ = load_ldm(dev, "random", feature_upsample_res=32, config=TINY_CONFIG)
+    inner = ldm.scheduler
+
+    class Sched:
+        timesteps = inner.timesteps
+
+        def add_noise(self, x, noise, t):
+            return inner.add_noise(x, torch.sin(7.0 * x), t)
+    ldm.scheduler = Sched()
+    ctx = torch.from_numpy(recipes.random_logits(52, (1, 16, 32))).to(dev) + ctx_shift
+    return TokenOptimizer(ldm, ctls, ctx, top_k=4, furthest_point_num_samples=8, accum=accum, device=dev)
+
+
+def _tiny_images(dev):
+    import recipes
+    from stablekeypoints_amd.sd import TINY_IMAGE
+    return [torch.from_numpy(recipes.uniform(60 + i, (1, 3, TINY_IMAGE, TINY_IMAGE))).to(dev) for i in range(2)]
+
+
+def _real_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = "cuda:0"
+        torch.cuda.set_device(0)
+        torch.manual_seed(5)
+        # rank 1 starts from a different embedding: TokenOptimizer must replace it by rank 0's
+        opt = _tiny_opt(1, dev, ctx_shift=float(rank))
+        img = _tiny_images(dev)[rank]
+        idx = opt.micro_steps([img])[0]
+        rec = {k: float(v) for k, v in opt.optimizer_step().items()}
+        q.put((rank, idx.cpu().numpy().copy(), opt.context.detach().cpu().numpy().copy(), rec))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_ranks_real_token_opt_step_equals_one_process():
+    """TokenOptimizer.micro_steps + optimizer_step on 2 gloo ranks (both on cuda:0, one image
+    each) == one process running both images' micro-iterations then Adam (optimize.py:362-448
+    with num_gpus=2 vs 1): selected indices exact, loss statistics and the context after Adam
+    within 1e-6."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    dev = "cuda:0"
+    torch.manual_seed(5)
+    ref = _tiny_opt(2, dev)
+    imgs = _tiny_images(dev)
+    ref_idx = [ref.micro_step(imgs[0]), ref.micro_step(imgs[1])]
+    ref_rec = {k: float(v) for k, v in ref.optimizer_step().items()}
+    ref_ctx = ref.context.detach().cpu()
+    del ref
+    torch.cuda.empty_cache()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_real_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=300) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, idx, c, rec in out:
+        assert (idx == ref_idx[rank].cpu().numpy()).all(), (rank, idx, ref_idx[rank])
+        d = float((torch.from_numpy(c) - ref_ctx).abs().max())
+        print(f"\nrank {rank}: context after Adam max|Δ| vs one process {d:.1e}")
+        assert d <= 1e-6, d
+        for k in rec:
+            assert abs(rec[k] - ref_rec[k]) <= 1e-6 * max(1.0, abs(ref_rec[k])), (k, rec[k], ref_rec[k])
