@@ -386,6 +386,7 @@ def find_top_k_gaussian(maps, top_k, sigma=3, epsilon=1e-5, num_subjects=1, retu
     _lib.require_device(maps)
     maps = _c(maps)
     T, h, w = maps.shape
+    top_k = min(int(top_k), T)   # argsort(kl)[:top_k] (ptp_utils.py:110): at most T candidates
     out = torch.empty(top_k, device=maps.device, dtype=torch.int64)
     kl = torch.empty(T, device=maps.device, dtype=torch.float64)
     call("skp_topk_gaussian", ptr(maps), T, h, w, int(top_k), float(sigma), float(epsilon), int(num_subjects),
@@ -397,6 +398,7 @@ def entropy_sort(maps, top_k, return_entropy=False):
     _lib.require_device(maps)
     maps = _c(maps)
     T, h, w = maps.shape
+    top_k = min(int(top_k), T)   # argsort(entropy)[:top_k] (ptp_utils.py:185): at most T candidates
     out = torch.empty(top_k, device=maps.device, dtype=torch.int64)
     ent = torch.empty(T, device=maps.device, dtype=torch.float64)
     call("skp_entropy_sort", ptr(maps), T, h, w, int(top_k), ptr(out), ptr(ent), ptr(ent), stream(maps.device))

@@ -1,0 +1,107 @@
+"""BASELINE.json configs[0]: the custom-image workload (4 images of 512², N=10 tokens, 5
+optimisation steps) through the reference's optimize stage on the GPU.
+
+Reference: ``datasets/custom_images.py:7-28`` (sorted folder, RGB, resize, [0, 1] CHW),
+``optimize.py:269-475`` (``optimize_embedding``; batch_size 4 → 4 micro-iterations per Adam
+step), ``main.py:212-241`` (``embedding.pt``).  The custom dataset stops after the optimize /
+find_indices stages in the reference (``keypoint_regressor.py:169-170``).
+N = 10 is not a multiple of 4, so this also runs the small-N kernel variants: the fused
+forward with one token quad per lane (QPL = 1) and the per-layer capture backward (NT = 1).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+class _Calls:
+    """Kernel-timer stand-in that records which hot-path entry points ran."""
+
+    def __init__(self):
+        self.names = []
+
+    def record(self, name, nbytes):
+        self.names.append(name)
+
+        class _Ctx:
+            def __enter__(self_):
+                return self_
+
+            def __exit__(self_, *a):
+                return False
+        return _Ctx()
+
+
+def test_configs0_custom_images_n10_five_steps(tmp_path):
+    from PIL import Image
+    from stablekeypoints_amd import main as skp_main, ops
+    from stablekeypoints_amd.optimize import optimize_embedding
+    from stablekeypoints_amd.optimize_token import load_ldm
+    folder = tmp_path / "images"
+    folder.mkdir()
+    rng = np.random.default_rng(0)
+    for i in range(4):   # smooth synthetic scenes: a few Gaussian blobs on a gradient
+        yy, xx = np.mgrid[0:512, 0:512] / 512.0
+        img = np.stack([xx, yy, 1 - xx], -1) * 0.5
+        for _ in range(3):
+            cy, cx, r = rng.random(3) * [1, 1, 0.1] + [0, 0, 0.05]
+            img += np.exp(-((yy - cy) ** 2 + (xx - cx) ** 2) / (2 * r * r))[..., None] * rng.random(3)
+        Image.fromarray((np.clip(img, 0, 1) * 255).astype(np.uint8)).save(folder / f"img_{i}.png")
+    torch.manual_seed(0)
+    torch.cuda.manual_seed(0)
+    ldm, controllers, num_gpus = load_ldm(DEV, "random", feature_upsample_res=128)
+    calls = _Calls()
+    ops.set_kernel_timer(calls)
+    from stablekeypoints_amd import ptp_utils
+    from stablekeypoints_amd.datasets import CustomDataset
+    from stablekeypoints_amd.optimize import TokenOptimizer
+    ctx0 = ptp_utils.init_random_noise(DEV, num_words=10, dim=768)
+    images = [CustomDataset(str(folder))[i]["img"][None].to(DEV) for i in range(4)]
+
+    def fixed_loss(ctx):
+        """The objective on the 4 images with fixed warps and noise (seeded), no update."""
+        torch.manual_seed(123)
+        torch.cuda.manual_seed(123)
+        opt = TokenOptimizer(ldm, controllers, ctx.detach().clone(), top_k=10, furthest_point_num_samples=25,
+                             sigma=2.0, accum=1, device=DEV)
+        with torch.no_grad():
+            total = sum(float(opt.image_loss(img)[0]) for img in images)
+        opt.restore_hooks()
+        return total
+
+    before = fixed_loss(ctx0)
+    losses = []
+    try:
+        emb = optimize_embedding(ldm, top_k_strategy="gaussian", wandb_log=False, lr=5e-3, num_steps=5, num_tokens=10,
+                                 context=ctx0.clone(),
+                                 top_k=10, sigma=2.0, sharpening_loss_weight=100, equivariance_attn_loss_weight=1000.0,
+                                 batch_size=4, furthest_point_num_samples=25, layers=[0, 1, 2, 3], device=DEV,
+                                 dataset_loc=str(folder), dataset_name="custom", controllers=controllers,
+                                 num_gpus=num_gpus, augment_degrees=15.0, augment_scale=(0.8, 1.0),
+                                 augment_translate=(0.25, 0.25), log=lambda rec: losses.append(rec["loss"]), seed=0)
+    finally:
+        ops.set_kernel_timer(None)
+    torch.save(emb, tmp_path / "embedding.pt")   # main.py:241
+    saved = torch.load(tmp_path / "embedding.pt", weights_only=True)
+    after = fixed_loss(saved.to(DEV))
+    print(f"\nconfigs[0]: running loss per Adam step {['%.4f' % v for v in losses]} (each step its own random "
+          f"warps); fixed-warp objective {before:.4f} -> {after:.4f}; kernels {sorted(set(calls.names))}")
+    assert tuple(saved.shape) == (1, 10, 768) and torch.isfinite(saved).all()
+    assert len(losses) == 5 and all(np.isfinite(losses))
+    assert after < before, (before, after)   # the same objective, before and after the 5 Adam steps
+    assert "skp_capture_maps_fwd" in calls.names        # QPL = 1 fused forward (N = 10 <= 64)
+    assert not torch.equal(saved.cpu(), ctx0.cpu())
+    assert "skp_capture_bwd" in calls.names             # per-layer backward, NT = 1 (N % 4 != 0)
+    assert "skp_capture_maps_bwd" not in calls.names
+    assert skp_main.build_parser().parse_args(["--dataset_name", "custom"]).dataset_name == "custom"
