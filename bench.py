@@ -39,9 +39,10 @@ class KernelTimer:
         self.names = set(names)
         self.events = {n: [] for n in names}
         self.nbytes = {n: [] for n in names}
+        self.flops = {n: [] for n in names}
         self.enabled = False
 
-    def record(self, name, nbytes):
+    def record(self, name, nbytes, flops=0):
         timer = self
 
         class _Ctx:
@@ -58,6 +59,7 @@ class KernelTimer:
                     self_.ev[1].record()
                     timer.events[name].append(self_.ev)
                     timer.nbytes[name].append(nbytes)
+                    timer.flops[name].append(flops)
                 return False
         return _Ctx()
 
@@ -66,7 +68,8 @@ class KernelTimer:
         if not ev:
             return None
         ms = [a.elapsed_time(b) for a, b in ev]
-        return {"launches": len(ms), "avg_ms": float(np.mean(ms)), "bytes_per_launch": float(np.mean(self.nbytes[name]))}
+        return {"launches": len(ms), "avg_ms": float(np.mean(ms)), "bytes_per_launch": float(np.mean(self.nbytes[name])),
+                "flop_per_launch": float(np.mean(self.flops[name]))}
 
 
 def _pmc_record(path, name, key, value):
@@ -352,16 +355,13 @@ def main():
     # aggregate), is VALU-bound (bicubic taps + exp + normalise per (pixel, token, layer, head));
     # its HBM traffic is reported beside it.  With SKP_FUSED_MAPS=0 the r01 path's HBM-bound
     # skp_aggregate is reported instead.
-    from stablekeypoints_amd.ops import capture_maps_flops, capture_maps_bwd_flops
-    sizes = (16, 16, 16, 32) if args.model == "sd15" else None   # SD-1.5 captured layers (up_blocks 1, 2)
     roof = None
     extra = {}
     fw = timer.summary("skp_capture_maps_fwd")
     bw = timer.summary("skp_capture_maps_bwd")
     valu_json = os.path.join(REPO, "profiles", "pmc_valu.json")
-    if fw and sizes is not None:
-        B2 = 2 * mb   # each pass captures the images and their warps
-        flops = capture_maps_flops(B2, 8, args.tokens, args.upsample_res, sizes)
+    if fw:
+        flops = fw["flop_per_launch"]   # ops.capture_maps_flops of the launch's (B, H, N, R, sizes)
         t = fw["avg_ms"] * 1e-3
         traffic = _pmc_record(args.traffic, "skp_capture_maps_fwd", ("algorithmic_bytes_per_launch", fw["bytes_per_launch"]),
                               "hbm_bytes_per_launch")
@@ -374,14 +374,11 @@ def main():
                 "valu_busy_pmc": _pmc_record(valu_json, "skp_capture_maps_fwd", ("flop_per_launch", flops), "valu_busy"),
                 "flop_model": "15 FLOP per (image, head, layer, pixel, token) + 8 per (row, low-res column, token); "
                               "ops.capture_maps_flops"}
-    elif fw:
-        extra["skp_capture_maps_fwd"] = {"avg_ms": fw["avg_ms"], "launches": fw["launches"]}
-    if bw and sizes is not None:
-        B2 = 2 * mb
-        flops = capture_maps_bwd_flops(B2, 8, args.tokens, args.upsample_res, sizes)
+    if bw:
         t = bw["avg_ms"] * 1e-3
         extra["skp_capture_maps_bwd"] = {"avg_ms": bw["avg_ms"], "launches": bw["launches"],
-                                         "TFLOP/s": flops / t / 1e12, "valu_frac": flops / t / VALU_F32_PEAK,
+                                         "TFLOP/s": bw["flop_per_launch"] / t / 1e12,
+                                         "valu_frac": bw["flop_per_launch"] / t / VALU_F32_PEAK,
                                          "GB/s_algorithmic": bw["bytes_per_launch"] / t / 1e9}
     agg = timer.summary("skp_aggregate")
     if agg:

@@ -31,8 +31,8 @@ class _NoTimer:
         return False
 
 
-def _timed(name, nbytes=0):
-    return _TIMER.record(name, nbytes) if _TIMER is not None else _NoTimer()
+def _timed(name, nbytes=0, flops=0):
+    return _TIMER.record(name, nbytes, flops) if _TIMER is not None else _NoTimer()
 
 
 def _c(t, dtype=F32):
@@ -236,7 +236,7 @@ class CaptureMaps(torch.autograd.Function):
             zp = (ctypes.c_void_p * L)(*[z.data_ptr() for z in zs])
             sp = (ctypes.c_int * L)(*[int(s) for s in sizes])
             stp = (ctypes.c_void_p * L)(*[st.data_ptr() for st in stats])
-            with _timed("skp_capture_maps_fwd", capture_maps_bytes(B, H, N, R, sizes)):
+            with _timed("skp_capture_maps_fwd", capture_maps_bytes(B, H, N, R, sizes), capture_maps_flops(B, H, N, R, sizes)):
                 call("skp_capture_maps_fwd", ctypes.cast(zp, ctypes.POINTER(ctypes.c_void_p)), sp, L, B, H, N, R,
                      ptr(out), ctypes.cast(stp, ctypes.POINTER(ctypes.c_void_p)), stream(dev))
         else:
@@ -271,7 +271,8 @@ class CaptureMaps(torch.autograd.Function):
             sp = (ctypes.c_int * L)(*[int(s) for s in sizes])
             stp = (ctypes.c_void_p * L)(*[st.data_ptr() for st in stats])
             dp = (ctypes.c_void_p * L)(*[d.data_ptr() for d in dzs])
-            with _timed("skp_capture_maps_bwd", capture_maps_bwd_bytes(B, H, N, R, sizes)):
+            with _timed("skp_capture_maps_bwd", capture_maps_bwd_bytes(B, H, N, R, sizes),
+                        capture_maps_bwd_flops(B, H, N, R, sizes)):
                 call("skp_capture_maps_bwd", ctypes.cast(zp, ctypes.POINTER(ctypes.c_void_p)), sp, L, B, H, N, R,
                      ptr(dmaps), scale, ctypes.cast(stp, ctypes.POINTER(ctypes.c_void_p)),
                      ctypes.cast(dp, ctypes.POINTER(ctypes.c_void_p)), ptr(ws), stream(dmaps.device))
