@@ -45,6 +45,41 @@ def test_bgemm_matches_fp64(Z, M, Nn, K):
     assert torch.allclose(out2.cpu().double(), ref * 2, atol=1e-4, rtol=1e-5)
 
 
+def _layouts(x):
+    """x (Z, R, C) as three device views with equal values: contiguous, transposed storage
+    (unit stride along the other axis) and a generic strided view (no unit stride)."""
+    d = x.to(DEV)
+    t = x.transpose(1, 2).contiguous().to(DEV).transpose(1, 2)
+    big = torch.zeros(x.shape[0], x.shape[1], 2 * x.shape[2], device=DEV)
+    big[:, :, ::2] = d
+    return {"contig": d, "trans": t, "strided": big[:, :, ::2]}
+
+
+@pytest.mark.parametrize("Z,M,Nn,K", [(2, 70, 45, 37), (64, 256, 500, 160)])
+def test_bgemm_all_operand_layouts_accumulate_shared_batch(Z, M, Nn, K):
+    """Every operand layout pair the loader distinguishes (k unit stride, m/n unit stride,
+    generic), accumulate=True, and a stride-0 batch operand (the shared token embedding's
+    projected keys); (64, 256, 500, 160) is the bench's q kᵀ, 2048 tiles over a persistent
+    grid of 1024 workgroups (several tiles per workgroup, pipeline across tile boundaries)."""
+    from stablekeypoints_amd import ops
+    g = torch.Generator().manual_seed(Z + M + K)
+    a = torch.randn(Z, M, K, generator=g)
+    b = torch.randn(Z, K, Nn, generator=g)
+    ref = (a.double() @ b.double())
+    for na, av in _layouts(a).items():
+        for nb, bv in _layouts(b).items():
+            out = ops.bgemm(av, bv, alpha=0.25)
+            err = (out.cpu().double() - 0.25 * ref).abs().max().item()
+            assert err < 1e-4, (na, nb, err)
+    c0 = torch.randn(Z, M, Nn, generator=g)
+    out = c0.to(DEV)
+    ops.bgemm(a.to(DEV), b.to(DEV), alpha=2.0, out=out, accumulate=True)
+    assert torch.allclose(out.cpu().double(), c0.double() + 2 * ref, atol=2e-4, rtol=1e-5)
+    b1 = b[:1]
+    shared = ops.bgemm(a.to(DEV), b1.to(DEV).expand(Z, K, Nn))
+    assert torch.allclose(shared.cpu().double(), a.double() @ b1.double(), atol=1e-4, rtol=1e-5)
+
+
 def test_bgemm_layout_identity_asymmetric():
     from stablekeypoints_amd import ops
     a = torch.eye(40).unsqueeze(0)
