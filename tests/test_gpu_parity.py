@@ -421,7 +421,7 @@ def _capture_maps_abi(zs, sizes, B, H, R, with_stats=True):
 @pytest.mark.parametrize("B,H,sizes,R,Nn", [(2, 8, (4, 4, 4, 8), 32, 40), (1, 3, (5, 3), 40, 37), (2, 2, (16, 32), 128, 1),
                                             (1, 2, (8,), 32, 1000), (3, 1, (1, 2), 8, 130), (1, 8, (16, 16, 16, 32), 128, 500),
                                             (1, 4, (7, 13), 100, 256), (1, 2, (6,), 72, 129), (1, 1, (12,), 24, 8),
-                                            (1, 2, (32, 64), 128, 500)])
+                                            (1, 2, (32, 64), 128, 500), (1, 2, (9, 20), 31, 64)])
 def test_capture_maps_fwd_vs_oracle(B, H, sizes, R, Nn):
     """skp_capture_maps_fwd (fused capture + per-image layer/head mean) vs the oracle's
     capture_fwd + collect_maps per image (ptp_utils.py:508-538, optimize.py:27-79): maps within
@@ -499,7 +499,7 @@ def _capture_maps_bwd_abi(zs, sizes, B, H, R, dmaps, gscale, stats):
 @pytest.mark.parametrize("B,H,sizes,R,Nn,with_stats", [(2, 8, (4, 4, 4, 8), 32, 40, True), (1, 3, (5, 3), 40, 36, True),
                                                        (2, 2, (16, 32), 128, 4, False), (1, 2, (8,), 32, 1000, True),
                                                        (3, 1, (1, 2), 8, 128, False), (1, 4, (7, 13), 100, 256, True),
-                                                       (1, 2, (6, 64), 64, 260, True)])
+                                                       (1, 2, (6, 64), 64, 260, True), (2, 4, (16, 32), 128, 500, True)])
 def test_capture_maps_bwd_vs_oracle(B, H, sizes, R, Nn, with_stats):
     """skp_capture_maps_bwd (one wave per (layer, head, row), V/W windows in registers) vs the
     oracle's capture_bwd of the per-image broadcast gradient (collect_maps_bwd, optimize.py:27-79,
