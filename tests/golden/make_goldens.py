@@ -477,6 +477,57 @@ def gen_celeba_reader():
     np.savez_compressed(os.path.join(HERE, "celeba_reader.npz"), **out)
 
 
+def gen_cub_reader():
+    """datasets/cub_parts.py:242-440 (CUBDataset) on a seeded 6-image tree (recipes.write_mini_cub):
+    train (jitter + mirror, np.random seeded per item) and test splits, cub_001 / cub_all.  The
+    reference reader needs cv2.resize and torchvision's ToTensor, both absent here: they are
+    supplied as restatements (cv2 INTER_LINEAR half-pixel bilinear / INTER_NEAREST floor, from
+    stablekeypoints_amd.datasets; ToTensor = HWC uint8 -> CHW / 255), so the image pixels pin
+    the crop, bbox padding/jitter, squaring and mirroring but not cv2's own resampling; the
+    keypoints, visibility and sfm poses involve no resampling and are pinned outright."""
+    import tempfile
+    from datasets import cub_parts
+    from stablekeypoints_amd import datasets as mine
+    cv2 = sys.modules["cv2"]
+    cv2.INTER_NEAREST = "nearest"
+
+    def resize(img, size, interpolation=None):
+        w, h = size
+        if interpolation == "nearest":
+            out = mine._resize_nearest(img[:, :, 0] if img.ndim == 3 else img, h, w)
+        else:
+            out = mine._resize_linear(img, h, w)
+        return out
+
+    cv2.resize = resize
+
+    class _ToTensor:
+        def __call__(self, im):
+            a = np.asarray(im)
+            return torch.from_numpy(a.transpose(2, 0, 1).copy()).float() / 255.0
+
+    cub_parts.transforms = types.SimpleNamespace(Compose=lambda ts: ts[0], ToTensor=_ToTensor)
+    out = {}
+    with tempfile.TemporaryDirectory() as root:
+        recipes.write_mini_cub(root)
+        for split in ("train", "test"):
+            for name, cls in (("001", 1), ("all", None)):
+                ds = cub_parts.CUBDataset(dataset_root=root, split=split, single_class=cls)
+                key = f"{split}_{name}"
+                out[key + "_len"] = len(ds)
+                out[key + "_labels"] = np.array(ds.labels)
+                for i in range(len(ds)):
+                    np.random.seed(100 + i)
+                    e = ds[i]
+                    out[f"{key}_{i}_img_sha"] = recipes.sha256(_np(e["img"]).astype(np.float32))
+                    out[f"{key}_{i}_img_shape"] = np.array(e["img"].shape)
+                    out[f"{key}_{i}_kpts"] = _np(e["kpts"])
+                    out[f"{key}_{i}_vis"] = _np(e["visibility"])
+                    out[f"{key}_{i}_mask_sha"] = recipes.sha256(np.asarray(e["mask"], np.float32))
+                    out[f"{key}_{i}_sfm"] = np.asarray(e["sfm_pose"], np.float64)
+    np.savez_compressed(os.path.join(HERE, "cub_reader.npz"), **out)
+
+
 def gen_evaluate_tiny():
     """eval.evaluate (eval.py:374-539) on the tiny model, all five metrics, CPU.
 
@@ -571,7 +622,8 @@ if __name__ == "__main__":
     REFM = import_reference()
     torch.set_num_threads(8)
     which = sys.argv[1:] or ["capture_small", "capture_sd15", "argmax", "gaussian", "select", "losses",
-                             "step_tiny", "interp", "eval_tiny", "best_indices_tiny", "regressor", "celeba_reader", "evaluate_tiny"]
+                             "step_tiny", "interp", "eval_tiny", "best_indices_tiny", "regressor", "celeba_reader", "evaluate_tiny",
+                             "cub_reader"]
     for w in which:
         print("generating", w, flush=True)
         globals()["gen_" + w]()

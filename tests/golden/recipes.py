@@ -114,3 +114,54 @@ def write_mini_celeba(root, seed=0):
     open(os.path.join(root, "MAFL/training.txt"), "w").writelines(["000001.jpg\n", "000003.jpg\n", "000004.jpg\n",
                                                                    "000006.jpg\n"])
     open(os.path.join(root, "MAFL/testing.txt"), "w").writelines(["000002.jpg\n", "000005.jpg\n"])
+
+
+def write_mini_cub(root, seed=0):
+    """A 6-image CUB tree in the layout datasets/cub_parts.py reads: PNG images (lossless, so the
+    bytes the readers see are the seeded pixels; the reader only joins rel_path) under
+    CUB_200_2011/images/<class dir>/, CMR-style train/test .mat annotations (struct array
+    ``images``: rel_path, bbox x1..y2 1-based, parts 3 × 15 (x, y, visibility, 1-based), mask)
+    and .../sfm/anno_<split>.mat (``sfm_anno``: scale, trans (2,), rot 3 × 3).  Classes 001 ×3,
+    002 ×2, 003 ×1; image 1 is grayscale; image 4's box runs past the image (background fill)."""
+    import os
+    import scipy.io as sio
+    from PIL import Image
+    rng = np.random.default_rng(seed)
+    classes = [1, 1, 2, 1, 2, 3]
+    base = os.path.join(root, "CUB_200_2011")
+    recs, sfms = [], []
+    for k, c in enumerate(classes):
+        d = f"{c:03d}.Bird_{c}"
+        os.makedirs(os.path.join(base, "images", d), exist_ok=True)
+        h, w = int(rng.integers(60, 100)), int(rng.integers(60, 100))
+        shape = (h, w) if k == 1 else (h, w, 3)
+        rel = f"{d}/Bird_{c}_{k:04d}.png"
+        Image.fromarray(rng.integers(0, 256, shape, dtype=np.uint8)).save(os.path.join(base, "images", rel))
+        x1, y1 = int(rng.integers(2, w // 3)), int(rng.integers(2, h // 3))
+        x2 = w + 5 if k == 4 else int(rng.integers(2 * w // 3, w))
+        y2 = int(rng.integers(2 * h // 3, h))
+        parts = np.zeros((3, 15))
+        parts[0] = rng.uniform(x1, min(x2, w), 15).round()
+        parts[1] = rng.uniform(y1, y2, 15).round()
+        parts[2] = (rng.uniform(0, 1, 15) > 0.3).astype(float)
+        parts[:2, parts[2] == 0] = 0.0
+        mask = (rng.uniform(0, 1, (h, w)) > 0.5).astype(np.uint8)
+        recs.append((rel, {"x1": float(x1), "y1": float(y1), "x2": float(x2), "y2": float(y2)}, parts, mask))
+        q = rng.normal(size=4)
+        q /= np.linalg.norm(q)
+        a, b_, c_, d_ = q
+        rot = np.array([[1 - 2 * (c_ * c_ + d_ * d_), 2 * (b_ * c_ - a * d_), 2 * (b_ * d_ + a * c_)],
+                        [2 * (b_ * c_ + a * d_), 1 - 2 * (b_ * b_ + d_ * d_), 2 * (c_ * d_ - a * b_)],
+                        [2 * (b_ * d_ - a * c_), 2 * (c_ * d_ + a * b_), 1 - 2 * (b_ * b_ + c_ * c_)]])
+        sfms.append((float(rng.uniform(50, 150)), rng.uniform(20, 60, 2), rot))
+    cache = os.path.join(base, "cachedir", "cub")
+    os.makedirs(os.path.join(cache, "data"), exist_ok=True)
+    os.makedirs(os.path.join(cache, "sfm"), exist_ok=True)
+    for split, idx in (("train", [0, 1, 2, 3, 4, 5]), ("test", [5, 2, 0, 4])):
+        imgs = np.zeros((len(idx),), dtype=[("rel_path", "O"), ("bbox", "O"), ("parts", "O"), ("mask", "O")])
+        sfm = np.zeros((len(idx),), dtype=[("scale", "O"), ("trans", "O"), ("rot", "O")])
+        for j, k in enumerate(idx):
+            imgs[j]["rel_path"], imgs[j]["bbox"], imgs[j]["parts"], imgs[j]["mask"] = recs[k]
+            sfm[j]["scale"], sfm[j]["trans"], sfm[j]["rot"] = sfms[k]
+        sio.savemat(os.path.join(cache, "data", f"{split}_cub_cleaned.mat"), {"images": imgs})
+        sio.savemat(os.path.join(cache, "sfm", f"anno_{split}.mat"), {"sfm_anno": sfm})
