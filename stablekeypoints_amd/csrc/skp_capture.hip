@@ -869,18 +869,15 @@ void capture_bwd_row_kernel(const float* __restrict__ z, int B, int H, int s, in
     for (int c = 0; c < NQ; ++c)
       if (ok[c]) wrow[(size_t)j * nq + lane + 64 * c] = v[c];
   };
-#ifndef SKP_BWD_GPF
-#define SKP_BWD_GPF 1   // pixels of gradient prefetched ahead (registers; 2 measured +1%)
-#endif
-  constexpr int GPF = SKP_BWD_GPF;
-  f4 g[GPF + 1][NQ];   // g[0]: this pixel, g[k]: pixel x + k in flight
+  // Gradient rows ping-pong between two register sets (the pixel loop is unrolled by 2), so the
+  // prefetch of pixel x + 1 needs no copy; with the forward's stats, 1/Σ folds into the exp's
+  // offset (a = exp2(z·log2e − m·log2e + log2(1/Σ))), one v_log per pixel instead of NQ·2 v_pk_mul.
+  f4 gA[NQ], gB[NQ];
 #pragma unroll
-  for (int k = 0; k < GPF; ++k)
-#pragma unroll
-    for (int c = 0; c < NQ; ++c) g[k][c] = grow[(size_t)min(k, R - 1) * nq + qo[c]];
+  for (int c = 0; c < NQ; ++c) gA[c] = grow[qo[c]];
   float4 stq = make_float4(0.f, 0.f, 0.f, 0.f);   // stats of pixels x0 + 2·lane, x0 + 2·lane + 1
   auto rl = [](float v, int i) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), i)); };
-  for (int x = 0; x < R; ++x) {
+  auto pixel = [&](int x, const f4 (&g)[NQ], f4 (&gn)[NQ]) {
     if (STATS && (x & 127) == 0) stq = strow[min((x >> 1) + lane, (R - 1) >> 1)];
     const float4 w = TWt[x];
     const int lo = TLt[x];
@@ -898,9 +895,9 @@ void capture_bwd_row_kernel(const float* __restrict__ z, int B, int H, int s, in
       ++base;
       vcol(base + 3);   // replaces the column that just left (ring slot (base − 1) & 3)
     }
-    const int xn = min(x + GPF, R - 1);
+    const int xn = min(x + 1, R - 1);
 #pragma unroll
-    for (int c = 0; c < NQ; ++c) g[GPF][c] = grow[(size_t)xn * nq + qo[c]];
+    for (int c = 0; c < NQ; ++c) gn[c] = grow[(size_t)xn * nq + qo[c]];
     const f4* v0 = ring + ((base + 0) & 3) * (Np / 4) + lane;
     const f4* v1 = ring + ((base + 1) & 3) * (Np / 4) + lane;
     const f4* v2 = ring + ((base + 2) & 3) * (Np / 4) + lane;
@@ -916,16 +913,17 @@ void capture_bwd_row_kernel(const float* __restrict__ z, int B, int H, int s, in
       a[c] = v;
       if (!STATS) m = __builtin_fmaxf(__builtin_fmaxf(m, __builtin_fmaxf(v.x, v.y)), __builtin_fmaxf(v.z, v.w));
     }
-    float inv;
+    f4 mb;
     if (STATS) {
       const int src = (x & 127) >> 1;
       const bool odd = x & 1;
       m = rl(odd ? stq.z : stq.x, src);
-      inv = rl(odd ? stq.w : stq.y, src);
+      const float inv = rl(odd ? stq.w : stq.y, src);
+      mb = (f4)(__builtin_amdgcn_logf(inv) - m * L2E);   // v_log_f32 is log2
     } else {
       m = wave64_max(m);   // padded quads hold −1e30: the max is unchanged
+      mb = (f4)(-m * L2E);
     }
-    const f4 mb = (f4)(-m * L2E);
     f4 sv = (f4)0.0f;
 #pragma unroll
     for (int c = 0; c < NQ; ++c) {
@@ -935,14 +933,17 @@ void capture_bwd_row_kernel(const float* __restrict__ z, int B, int H, int s, in
       t.z = __builtin_amdgcn_exp2f(t.z);
       t.w = __builtin_amdgcn_exp2f(t.w);
       a[c] = t;
-      sv += t;
+      if (!STATS) sv += t;
     }
-    if (!STATS) inv = __builtin_amdgcn_rcpf(wave64_sum((sv.x + sv.y) + (sv.z + sv.w)));
+    if (!STATS) {
+      const float inv = __builtin_amdgcn_rcpf(wave64_sum((sv.x + sv.y) + (sv.z + sv.w)));
+#pragma unroll
+      for (int c = 0; c < NQ; ++c) a[c] *= inv;
+    }
     f4 ag[NQ], dv = (f4)0.0f;
 #pragma unroll
     for (int c = 0; c < NQ; ++c) {
-      a[c] *= inv;
-      ag[c] = a[c] * g[0][c];
+      ag[c] = a[c] * g[c];
       dv += ag[c];
     }
     const float dot = wave64_sum((dv.x + dv.y) + (dv.z + dv.w));
@@ -953,9 +954,11 @@ void capture_bwd_row_kernel(const float* __restrict__ z, int B, int H, int s, in
       Ww[1][c] = __builtin_elementwise_fma(dz, (f4)w.y, Ww[1][c]);
       Ww[2][c] = __builtin_elementwise_fma(dz, (f4)w.z, Ww[2][c]);
       Ww[3][c] = __builtin_elementwise_fma(dz, (f4)w.w, Ww[3][c]);
-#pragma unroll
-      for (int k = 0; k < GPF; ++k) g[k][c] = g[k + 1][c];
     }
+  };
+  for (int x = 0; x < R; x += 2) {
+    pixel(x, gA, gB);
+    if (x + 1 < R) pixel(x + 1, gB, gA);
   }
   // the last window: virtual columns base … base + 3 (clamped runs summed, each column once)
   f4 acc[NQ];
