@@ -271,10 +271,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal of the multi-GPU path on a one-GPU box (not the measured configuration):
+    # SKP_BENCH_ONE_DEVICE=1 puts every rank on cuda:0, SKP_BENCH_DIST_BACKEND=gloo replaces RCCL
+    # (which refuses two ranks on one device).  The driver's N-GPU runs use neither.
+    if os.environ.get("SKP_BENCH_ONE_DEVICE") == "1":
+        local = 0
+    backend = os.environ.get("SKP_BENCH_DIST_BACKEND", "nccl")
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
