@@ -533,6 +533,15 @@ __device__ constexpr float kAt[4][6] = {{1.f, 1.f, 1.f, 1.f, 1.f, 0.f},
                                         {0.f, 1.f, 1.f, 0.25f, 4.f, 0.f},
                                         {0.f, 1.f, -1.f, 0.125f, -8.f, 1.f}};
 
+#ifndef SKP_W2_PACKED
+#define SKP_W2_PACKED 1   // 0: the scalar half_transform (A/B build)
+#endif
+#if SKP_W2_PACKED
+#define W2_TRANSFORM half_transform_pk
+#else
+#define W2_TRANSFORM half_transform
+#endif
+
 // s_waitcnt vmcnt(n) with expcnt / lgkmcnt left alone (gfx9 encoding)
 #define W2_VMCNT(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (((n) >> 4) << 14) | (7 << 4) | (15 << 8))
 
@@ -565,6 +574,83 @@ __device__ __forceinline__ void half_transform(const float* raw, float* a) {
   }
 #pragma unroll
   for (int ii = 0; ii < 3; ++ii) bt6(t[ii][0], t[ii][1], t[ii][2], t[ii][3], t[ii][4], t[ii][5], a + 6 * ii, 1);
+}
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// y = Bᵀ x with shared differences: 16 operations instead of 20 (e, f, g, h reused)
+template <typename T>
+__device__ __forceinline__ void bt6_shared(T a0, T a1, T a2, T a3, T a4, T a5, T* y) {
+  const T e = a4 - a2, f = a3 - a1, g = a2 + a3, h = a3 - a2;
+  y[0] = __builtin_elementwise_fma((T)1.5f, f, (a0 + e) - a2);
+  y[1] = __builtin_elementwise_fma((T)1.5f, g, e + f);
+  y[2] = __builtin_elementwise_fma((T)1.5f, h, e - f);
+  y[3] = __builtin_elementwise_fma((T)2.0f, f, e);
+  y[4] = __builtin_elementwise_fma((T)-0.5f, f, e);
+  y[5] = __builtin_elementwise_fma((T)1.5f, e, __builtin_elementwise_fma((T)-2.0f, f, a5 - a1));
+}
+
+// Packed form of half_transform (v_pk_* f32): the column pass runs on column pairs
+// (1,2), (3,4), (0,5) — the first two are halves of the middle 16-B chunk, the third one
+// v_pk_mov per row — with each output row's first two terms in one FMA; the row pass packs
+// transform rows 3H and 3H+1 (pairs re-formed by one v_pk_mov per column) and runs row
+// 3H+2 unpacked, both with the shared-difference Bᵀ.  ≈76 VALU instructions per patch half
+// instead of ≈108.
+template <int H, int RF>
+__device__ __forceinline__ void half_transform_pk(const float* raw, float* a) {
+  f2 t[3][3];        // t[ii][p]: column pair p of transform row 3H+ii
+  f2 first[3][3];    // the first nonzero term's input pair, until the second term arrives
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    const f32x4 c0 = *reinterpret_cast<const f32x4*>(raw + r * RF);
+    const f32x4 c1 = *reinterpret_cast<const f32x4*>(raw + r * RF + 4);
+    const f32x4 c2 = *reinterpret_cast<const f32x4*>(raw + r * RF + 8);
+    const f2 d[3] = {__builtin_shufflevector(c1, c1, 0, 1), __builtin_shufflevector(c1, c1, 2, 3),
+                     __builtin_shufflevector(c0, c2, 3, 4)};
+#pragma unroll
+    for (int ii = 0; ii < 3; ++ii) {
+      const float c = kBt[3 * H + ii][r];
+      if (c == 0.0f) continue;
+      int seen = 0, r0 = 0;   // nonzero terms of row 3H+ii before r (compile time)
+#pragma unroll
+      for (int rp = 0; rp < r; ++rp)
+        if (kBt[3 * H + ii][rp] != 0.0f) {
+          if (seen == 0) r0 = rp;
+          ++seen;
+        }
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        if (seen == 0) {
+          first[ii][p] = d[p];
+        } else if (seen == 1) {   // c0·x0 + c·x: one FMA when either coefficient is ±1
+          const float c0f = kBt[3 * H + ii][r0];
+          if (c0f == 1.0f || c0f == -1.0f)
+            t[ii][p] = __builtin_elementwise_fma((f2)c, d[p], c0f == 1.0f ? first[ii][p] : -first[ii][p]);
+          else if (c == 1.0f || c == -1.0f)
+            t[ii][p] = __builtin_elementwise_fma((f2)c0f, first[ii][p], c == 1.0f ? d[p] : -d[p]);
+          else
+            t[ii][p] = __builtin_elementwise_fma((f2)c, d[p], (f2)c0f * first[ii][p]);
+        } else {
+          t[ii][p] = (c == 1.0f) ? t[ii][p] + d[p] : __builtin_elementwise_fma((f2)c, d[p], t[ii][p]);
+        }
+      }
+    }
+    asm volatile("" ::"v"(c0.x), "v"(c0.y), "v"(c0.z), "v"(c2.y), "v"(c2.z), "v"(c2.w));
+  }
+  // row pass: column b of row ii is t[ii][0] = (b1, b2), t[ii][1] = (b3, b4), t[ii][2] = (b0, b5)
+  const f2 u0 = __builtin_shufflevector(t[0][2], t[1][2], 0, 2), u1 = __builtin_shufflevector(t[0][0], t[1][0], 0, 2);
+  const f2 u2 = __builtin_shufflevector(t[0][0], t[1][0], 1, 3), u3 = __builtin_shufflevector(t[0][1], t[1][1], 0, 2);
+  const f2 u4 = __builtin_shufflevector(t[0][1], t[1][1], 1, 3), u5 = __builtin_shufflevector(t[0][2], t[1][2], 1, 3);
+  f2 y01[6];
+  bt6_shared<f2>(u0, u1, u2, u3, u4, u5, y01);
+  float y2[6];
+  bt6_shared<float>(t[2][2].x, t[2][0].x, t[2][0].y, t[2][1].x, t[2][1].y, t[2][2].y, y2);
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    a[j] = y01[j].x;
+    a[6 + j] = y01[j].y;
+    a[12 + j] = y2[j];
+  }
 }
 
 // partial output tile of rows 3H..3H+2 of M (m[18] = M[3H+ii][j]) → y[16] (row-major 4×4)
@@ -714,7 +800,7 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
     W2_VMCNT(0);
   }
   __syncthreads();
-  w2::half_transform<HH, kRowF>(R0 + roff, a0);
+  w2::W2_TRANSFORM<HH, kRowF>(R0 + roff, a0);
 
   // stage s: wait for group s (raw(s+1), U(s)); barrier; issue group s+2 into the slots freed by
   // stage s-1; transform raw(s+1) (slot (s+1)%3) and run the MFMAs on U(s) (slot s%3).  The SIMD
@@ -731,11 +817,11 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
     if (s + 2 < nst) issue_group(s + 2, Ri, Ui);
     const bool tr = s + 1 < nst && !(dbg & 1);
     if (HH == 0) {
-      if (tr) w2::half_transform<HH, kRowF>(Rn + roff, anext);
+      if (tr) w2::W2_TRANSFORM<HH, kRowF>(Rn + roff, anext);
       if (!(dbg & 2)) mfmas(Us, acur);
     } else {
       if (!(dbg & 2)) mfmas(Us, acur);
-      if (tr) w2::half_transform<HH, kRowF>(Rn + roff, anext);
+      if (tr) w2::W2_TRANSFORM<HH, kRowF>(Rn + roff, anext);
     }
   };
   // unrolled by 6: ring slot s%3, A-operand buffer s%2
