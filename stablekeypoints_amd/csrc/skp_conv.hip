@@ -592,47 +592,48 @@ __device__ __forceinline__ void bt6_shared(T a0, T a1, T a2, T a3, T a4, T a5, T
 
 // Packed form of half_transform (v_pk_* f32): the column pass runs on column pairs
 // (1,2), (3,4), (0,5) — the first two are halves of the middle 16-B chunk, the third one
-// v_pk_mov per row — with each output row's first two terms in one FMA; the row pass packs
-// transform rows 3H and 3H+1 (pairs re-formed by one v_pk_mov per column) and runs row
-// 3H+2 unpacked, both with the shared-difference Bᵀ.  ≈76 VALU instructions per patch half
-// instead of ≈108.
+// v_pk_mov per row — streaming the patch rows through shared differences (9 / 7 operations
+// per pair for rows 0-2 / 3-5 instead of 10); the row pass packs transform rows 3H and 3H+1
+// (pairs re-formed per column) and runs row 3H+2 unpacked, both with the shared-difference
+// Bᵀ.  ≈80 VALU instructions per patch half and stage instead of ≈109.
 template <int H, int RF>
 __device__ __forceinline__ void half_transform_pk(const float* raw, float* a) {
-  f2 t[3][3];        // t[ii][p]: column pair p of transform row 3H+ii
-  f2 first[3][3];    // the first nonzero term's input pair, until the second term arrives
+  f2 t[3][3];   // t[ii][p]: column pair p of transform row 3H+ii
+  f2 k0[3], k1[3], k2[3], k3[3];   // streamed partial terms (per column pair)
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
+    if (H == 1 && r == 0) continue;   // Bᵀ rows 3-5 do not read patch row 0
     const f32x4 c0 = *reinterpret_cast<const f32x4*>(raw + r * RF);
     const f32x4 c1 = *reinterpret_cast<const f32x4*>(raw + r * RF + 4);
     const f32x4 c2 = *reinterpret_cast<const f32x4*>(raw + r * RF + 8);
     const f2 d[3] = {__builtin_shufflevector(c1, c1, 0, 1), __builtin_shufflevector(c1, c1, 2, 3),
                      __builtin_shufflevector(c0, c2, 3, 4)};
 #pragma unroll
-    for (int ii = 0; ii < 3; ++ii) {
-      const float c = kBt[3 * H + ii][r];
-      if (c == 0.0f) continue;
-      int seen = 0, r0 = 0;   // nonzero terms of row 3H+ii before r (compile time)
-#pragma unroll
-      for (int rp = 0; rp < r; ++rp)
-        if (kBt[3 * H + ii][rp] != 0.0f) {
-          if (seen == 0) r0 = rp;
-          ++seen;
+    for (int p = 0; p < 3; ++p) {
+      if (H == 0) {
+        // s = −a2 + 1.5a3 + a4, q = −a1 + 1.5a2 + a3: rows 1, 2 = s ± q, row 0 = a0 − 1.5a1 + (s − a2)
+        if (r == 0) k0[p] = d[p];
+        if (r == 1) { k1[p] = d[p]; k0[p] = __builtin_elementwise_fma((f2)-1.5f, d[p], k0[p]); }
+        if (r == 2) { k2[p] = d[p]; k3[p] = __builtin_elementwise_fma((f2)1.5f, d[p], -k1[p]); }
+        if (r == 3) { k1[p] = __builtin_elementwise_fma((f2)1.5f, d[p], -k2[p]); k3[p] = k3[p] + d[p]; }
+        if (r == 4) {
+          const f2 sv = k1[p] + d[p];
+          t[0][p] = k0[p] + (sv - k2[p]);
+          t[1][p] = sv + k3[p];
+          t[2][p] = sv - k3[p];
         }
-#pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        if (seen == 0) {
-          first[ii][p] = d[p];
-        } else if (seen == 1) {   // c0·x0 + c·x: one FMA when either coefficient is ±1
-          const float c0f = kBt[3 * H + ii][r0];
-          if (c0f == 1.0f || c0f == -1.0f)
-            t[ii][p] = __builtin_elementwise_fma((f2)c, d[p], c0f == 1.0f ? first[ii][p] : -first[ii][p]);
-          else if (c == 1.0f || c == -1.0f)
-            t[ii][p] = __builtin_elementwise_fma((f2)c0f, first[ii][p], c == 1.0f ? d[p] : -d[p]);
-          else
-            t[ii][p] = __builtin_elementwise_fma((f2)c, d[p], (f2)c0f * first[ii][p]);
-        } else {
-          t[ii][p] = (c == 1.0f) ? t[ii][p] + d[p] : __builtin_elementwise_fma((f2)c, d[p], t[ii][p]);
+      } else {
+        // e = a4 − a2, f = a3 − a1: row 3 = e + 2f, row 4 = e − f/2, row 5 = 1.5e − 2f − a1 + a5
+        if (r == 1) k0[p] = d[p];
+        if (r == 2) k1[p] = d[p];
+        if (r == 3) { k2[p] = d[p] - k0[p]; k3[p] = __builtin_elementwise_fma((f2)-2.0f, k2[p], -k0[p]); }
+        if (r == 4) {
+          const f2 e = d[p] - k1[p];
+          t[0][p] = __builtin_elementwise_fma((f2)2.0f, k2[p], e);
+          t[1][p] = __builtin_elementwise_fma((f2)-0.5f, k2[p], e);
+          k3[p] = __builtin_elementwise_fma((f2)1.5f, e, k3[p]);
         }
+        if (r == 5) t[2][p] = k3[p] + d[p];
       }
     }
     asm volatile("" ::"v"(c0.x), "v"(c0.y), "v"(c0.z), "v"(c2.y), "v"(c2.z), "v"(c2.w));
