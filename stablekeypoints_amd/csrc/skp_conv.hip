@@ -520,7 +520,7 @@ constexpr int kUInstr = kUF / 256;         // 20
 constexpr int kThreads = 512;
 constexpr unsigned kOOB = 0x80000000u;     // buffer offset past any num_records (< 2 GiB): loads 0
 static_assert(kUF % 256 == 0, "whole 1-KB chunks");
-static_assert(3 * (GeoT<8>::RAWF + kUF) * 4 <= 160 * 1024 && 3 * (GeoT<4>::RAWF + kUF) * 4 <= 160 * 1024, "LDS");
+static_assert((4 * GeoT<8>::RAWF + 3 * kUF) * 4 <= 160 * 1024 && 3 * (GeoT<4>::RAWF + kUF) * 4 <= 160 * 1024, "LDS");
 static_assert(2 * 8 * 1024 <= kUF * 4, "epilogue exchange: two waves' 8 KB per ring buffer");
 
 // Bᵀ (rows i = transform row, columns a = patch row) for the points (0, 1, -1, 1/2, -2, ∞)
@@ -680,8 +680,31 @@ __device__ __forceinline__ void half_output(const float* m, float* y) {
 }  // namespace w2
 
 struct W2Smem {
-  float *R0, *R1, *R2, *U0, *U1, *U2;
+  float *R0, *R1, *R2, *R3, *U0, *U1, *U2;
 };
+
+// s_waitcnt vmcnt(n) for a wave-uniform n (the per-wave DMA instruction counts differ)
+__device__ __forceinline__ void w2_vmcnt(int n) {
+  switch (n) {
+    case 0: W2_VMCNT(0); break;
+    case 5: W2_VMCNT(5); break;
+    case 6: W2_VMCNT(6); break;
+    case 7: W2_VMCNT(7); break;
+    case 8: W2_VMCNT(8); break;
+    case 9: W2_VMCNT(9); break;
+    case 10: W2_VMCNT(10); break;
+    case 11: W2_VMCNT(11); break;
+    case 12: W2_VMCNT(12); break;
+    case 13: W2_VMCNT(13); break;
+    case 14: W2_VMCNT(14); break;
+    case 15: W2_VMCNT(15); break;
+    default: W2_VMCNT(0); break;
+  }
+}
+
+#ifndef SKP_W2_RS4
+#define SKP_W2_RS4 0   // 1: four raw-input slots for the 32×32 geometry (lead 3; measured 1-2% slower)
+#endif
 
 // One wave's whole program for transform half HH (rows 3HH..3HH+2); the kernel branches once
 // on the wave's half so the stage loop is straight-line code for each.
@@ -697,6 +720,9 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
   constexpr int kMaxRaw = (kRawInstr + 7) / 8;
   using w2::kUF;
   using w2::kUP;
+  // raw-input ring of RS slots (lead RS − 1 stages: the input streams from HBM), weight ring
+  // of 3 (lead 2: the weights are re-read by every tile block and hit L2)
+  constexpr int RS = (TXB == 8 && SKP_W2_RS4) ? 4 : 3;
   float *R0 = sm.R0, *R1 = sm.R1, *R2 = sm.R2, *U0 = sm.U0, *U1 = sm.U1, *U2 = sm.U2;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wm = wv & 3;
@@ -725,12 +751,15 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
   }
   const int nuw = (kInstr - 1 - wv) / 8 + 1 - nraw;   // U chunks of this wave
   const int ufirst = wv + 8 * nraw - kRawInstr;       // its first U chunk
-  const bool six = nraw + nuw == 6;                   // DMA instructions per stage group: 6 or 5
+  // vmcnt allowances (in-order counter; per step the wave issues U(s+2) then raw(s+RS)):
+  // top of step s needs U(s) and raw(s+1) landed; the prologue needs raw(0)
+  const int allow_step = RS == 4 ? nuw + 2 * nraw : nuw + nraw;
+  const int allow_pro = RS == 4 ? 2 * nuw + 3 * nraw : 2 * nuw + 2 * nraw;
   const size_t xend = (size_t)(img + NI) * C * plane; // the buffer ends with the block's last image
   const float* Ub = U + ((size_t)kb * C + c0) * w2::kNC * kUP;
   const int nst = csplit / w2::kCK;
 
-  // group t = {raw(t+1) → raw slot (t+1)%3, U(t) → U slot t%3}
+  // raw(t) → raw slot t % RS, U(t) → U slot t % 3
   auto issue_raw = [&](int t, float* rs_lds) {
     const bool ok = t < nst;
     const size_t off = ((size_t)c0 + (size_t)(ok ? t : 0) * w2::kCK) * plane;
@@ -741,8 +770,7 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
       if (m < nraw && !(dbg & 4))
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)(rs_lds + 256 * (wv + 8 * m)), 16, voff[m], 0, 0, 0);
   };
-  auto issue_group = [&](int t, float* rs_lds, float* us_lds) {
-    issue_raw(t + 1, rs_lds);
+  auto issue_u = [&](int t, float* us_lds) {
     const __amdgpu_buffer_rsrc_t ru =
         __builtin_amdgcn_make_buffer_rsrc((void*)(Ub + (size_t)t * kUF), (short)0, kUF * 4, 0x00020000);
 #pragma unroll
@@ -790,32 +818,26 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
     }
   };
 
-  // prologue: raw(0), groups 0 and 1; wait for raw(0) and transform it
+  // prologue: the DMAs of "steps" −RS..−1 (raw(0..RS−1), U(0), U(1)) in step order; wait for
+  // raw(0) and transform it
   issue_raw(0, R0);
-  issue_group(0, R1, U0);
-  if (nst > 1) issue_group(1, R2, U1);
-  if (nst > 1) {
-    if (six) W2_VMCNT(12);
-    else W2_VMCNT(10);
-  } else {
-    W2_VMCNT(0);
-  }
+  if (RS == 4) issue_raw(1, R1);
+  issue_u(0, U0);
+  issue_raw(RS - 2, RS == 4 ? R2 : R1);
+  if (nst > 1) issue_u(1, U1);
+  issue_raw(RS - 1, RS == 4 ? sm.R3 : R2);
+  w2_vmcnt(nst > 1 ? allow_pro : 0);
   __syncthreads();
   w2::W2_TRANSFORM<HH, kRowF>(R0 + roff, a0);
 
-  // stage s: wait for group s (raw(s+1), U(s)); barrier; issue group s+2 into the slots freed by
-  // stage s-1; transform raw(s+1) (slot (s+1)%3) and run the MFMAs on U(s) (slot s%3).  The SIMD
-  // partners (waves w, w+4: the two halves) do these in opposite orders, so one's transform
-  // (VALU) runs beside the other's MFMAs.
+  // stage s: wait for U(s) and raw(s+1); barrier; issue U(s+2) and raw(s+RS) into the slots
+  // freed by stage s-1; transform raw(s+1) (slot (s+1)%RS) and run the MFMAs on U(s) (slot
+  // s%3).  The SIMD partners (waves w, w+4: the two halves) do these in opposite orders.
   auto step = [&](int s, float* Rn, float* Us, float* Ri, float* Ui, const float (&acur)[18], float (&anext)[18]) {
-    if (s + 1 < nst) {
-      if (six) W2_VMCNT(6);
-      else W2_VMCNT(5);
-    } else {
-      W2_VMCNT(0);
-    }
+    w2_vmcnt(s + 1 < nst ? allow_step : 0);
     __syncthreads();
-    if (s + 2 < nst) issue_group(s + 2, Ri, Ui);
+    if (s + 2 < nst) issue_u(s + 2, Ui);
+    issue_raw(s + RS, Ri);   // past the last stage: empty (zero-length) loads keep the counts
     const bool tr = s + 1 < nst && !(dbg & 1);
     if (HH == 0) {
       if (tr) w2::W2_TRANSFORM<HH, kRowF>(Rn + roff, anext);
@@ -825,14 +847,19 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
       if (tr) w2::W2_TRANSFORM<HH, kRowF>(Rn + roff, anext);
     }
   };
-  // unrolled by 6: ring slot s%3, A-operand buffer s%2
-  for (int s = 0; s < ((dbg & 16) ? 0 : nst); s += 6) {
-    step(s, R1, U0, R0, U2, a0, a1);
-    if (s + 1 < nst) step(s + 1, R2, U1, R1, U0, a1, a0);
-    if (s + 2 < nst) step(s + 2, R0, U2, R2, U1, a0, a1);
-    if (s + 3 < nst) step(s + 3, R1, U0, R0, U2, a1, a0);
-    if (s + 4 < nst) step(s + 4, R2, U1, R1, U0, a0, a1);
-    if (s + 5 < nst) step(s + 5, R0, U2, R2, U1, a1, a0);
+  // unrolled by lcm(RS, 3, 2): raw slot s%RS, U slot s%3, A-operand buffer s%2
+  constexpr int PER = RS == 4 ? 12 : 6;
+  float* const Rsl[4] = {R0, R1, R2, sm.R3};
+  float* const Usl[3] = {U0, U1, U2};
+  for (int s0 = 0; s0 < ((dbg & 16) ? 0 : nst); s0 += PER) {
+    step(s0, Rsl[1 % RS], Usl[0], Rsl[0], Usl[2], a0, a1);
+#pragma unroll
+    for (int j = 1; j < PER; ++j) {
+      if (s0 + j < nst) {
+        if ((j & 1) == 0) step(s0 + j, Rsl[(j + 1) % RS], Usl[j % 3], Rsl[j % RS], Usl[(j + 2) % 3], a0, a1);
+        else step(s0 + j, Rsl[(j + 1) % RS], Usl[j % 3], Rsl[j % RS], Usl[(j + 2) % 3], a1, a0);
+      }
+    }
   }
 
   // epilogue: lane holds tiles 4(lane>>4)+r of the wave's 16 (ty = 2wm + (lane>>5),
@@ -924,7 +951,7 @@ __global__ __launch_bounds__(w2::kThreads) __attribute__((amdgpu_waves_per_eu(2,
   // separate LDS objects per ring slot: the compiler tells a DMA into one slot from a ds_read of
   // another and does not wait for outstanding DMAs before every LDS read
   __shared__ __attribute__((aligned(16))) float R0[w2::GeoT<TXB>::RAWF], R1[w2::GeoT<TXB>::RAWF],
-      R2[w2::GeoT<TXB>::RAWF];
+      R2[w2::GeoT<TXB>::RAWF], R3[(TXB == 8 && SKP_W2_RS4) ? w2::GeoT<TXB>::RAWF : 4];
   __shared__ __attribute__((aligned(16))) float U0[w2::kUF], U1[w2::kUF], U2[w2::kUF];
   // workgroup → (input-channel split, 32×32-pixel block, channel block); consecutive logical ids
   // share one XCD.  A split sums its csplit input channels into slab sp of y (the workspace).
@@ -954,7 +981,7 @@ __global__ __launch_bounds__(w2::kThreads) __attribute__((amdgpu_waves_per_eu(2,
     img = 4 * tb;
   }
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const W2Smem sm{R0, R1, R2, U0, U1, U2};
+  const W2Smem sm{R0, R1, R2, R3, U0, U1, U2};
   const int c0 = sp * csplit;
   if (wv < 4) wino2_body<EPI, 0, TXB>(sm, x, U, bias, res, y, C, K, H, W, img, x0, y0, kb, c0, csplit, wv, dbg);
   else wino2_body<EPI, 1, TXB>(sm, x, U, bias, res, y, C, K, H, W, img, x0, y0, kb, c0, csplit, wv, dbg);
