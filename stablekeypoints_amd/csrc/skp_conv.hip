@@ -937,7 +937,7 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
         v.z += rv.z;
         v.w += rv.w;
       }
-      *reinterpret_cast<float4*>(y + o) = v;
+      if (!(dbg & 64)) *reinterpret_cast<float4*>(y + o) = v;
     }
     if (blk == 0) __syncthreads();
   }
@@ -1048,7 +1048,7 @@ extern "C" int skp_conv3x3_wino2(const float* x, const float* U, const float* bi
   const int nkb = K / w2::kNC;
   SKP_CHECK_ARG(nblk * nkb * nsplit <= 0x7fffffffLL, "grid too large");
   // dev switches (SKP_WINO2_DEBUG): 1 skip transforms, 2 skip MFMAs, 4 skip input DMA, 8 skip weight DMA,
-  // 16 skip the stage loop, 32 skip the epilogue; SKP_WINO2_ORDER 1 tile-major, 2 channel-block-major
+  // 16 skip the stage loop, 32 skip the epilogue, 64 skip its global stores; SKP_WINO2_ORDER 1 tile-major, 2 channel-block-major
   static const int dbg = getenv("SKP_WINO2_DEBUG") ? atoi(getenv("SKP_WINO2_DEBUG")) : 0;
   static const int order = getenv("SKP_WINO2_ORDER") ? atoi(getenv("SKP_WINO2_ORDER")) : 0;
   // tile-major (the channel blocks of one pixel block back to back, sharing its input region in
