@@ -34,7 +34,10 @@ def _rel(a, b):
 @pytest.mark.parametrize("B,C,K,H,W", [(2, 64, 64, 32, 32), (2, 4, 32, 20, 20), (1, 32, 96, 12, 28),
                                        (3, 128, 64, 16, 8), (1, 512, 64, 8, 8), (2, 36, 32, 4, 4),
                                        (1, 8, 32, 32, 32), (2, 12, 64, 64, 96), (1, 40, 32, 96, 32),
-                                       (3, 4, 32, 32, 64), (4, 8, 32, 16, 16), (8, 36, 64, 16, 16)])
+                                       (3, 4, 32, 32, 64), (4, 8, 32, 16, 16), (8, 36, 64, 16, 16),
+                                       # region-kernel stage counts C/4 of 5, 7 and 11: every tail of
+                                       # its 6-step unrolled ring (zero-length raw loads past the end)
+                                       (1, 20, 32, 32, 32), (2, 28, 32, 32, 64), (4, 44, 32, 16, 16)])
 @pytest.mark.parametrize("bias,res", [(False, False), (True, False), (True, True)])
 def test_conv3x3_forward_vs_fp64(all_shapes, B, C, K, H, W, bias, res):
     ops = all_shapes
