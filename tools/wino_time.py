@@ -13,12 +13,15 @@ from stablekeypoints_amd import ops
 ap = argparse.ArgumentParser()
 ap.add_argument("--shapes", default="8,128,128,512;8,512,512,128;8,512,512,64;8,320,320,64;8,640,640,32;8,1280,1280,16")
 ap.add_argument("--iters", type=int, default=10)
+ap.add_argument("--residual", action="store_true", help="bias + residual epilogue (the resnet conv2 form)")
 a = ap.parse_args()
 for s in a.shapes.split(";"):
     B, C, K, HW = map(int, s.split(","))
     x = torch.randn(B, C, HW, HW, device="cuda:0")
     w = torch.randn(K, C, 3, 3, device="cuda:0") / (3 * C ** 0.5)
-    f = lambda: ops._wino_conv(x, w, False, None, None, K)
+    b = torch.randn(K, device="cuda:0") if a.residual else None
+    r = torch.randn(B, K, HW, HW, device="cuda:0") if a.residual else None
+    f = lambda: ops._wino_conv(x, w, False, b, r, K)
     f()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
