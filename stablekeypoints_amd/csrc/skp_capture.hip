@@ -550,6 +550,9 @@ __device__ __forceinline__ float row16_sum(float v) {
 // pixels per wave (a multiple of 4): acc = PXW/4 · QPL float4 = 32 VGPRs where possible
 constexpr int maps_pxw(int qpl) { return (32 / qpl) < 4 ? 4 : ((32 / qpl) > 16 ? 16 : 32 / qpl); }
 
+#ifndef SKP_MAPS_PRIO
+#define SKP_MAPS_PRIO 1   // s_setprio level of the staging phase (0: off; 1, 2, 3 measured 972, 983, 982 vs 1003 us)
+#endif
 template <int QPL, int WAVES>
 __global__ __launch_bounds__(WAVES * WAVE) __attribute__((amdgpu_waves_per_eu(4)))
 void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nchunks, int vstride, float count,
@@ -673,7 +676,13 @@ void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nc
   const int nslab = L * H;
   for (int it = 0; it < nslab; ++it) {
     if (it > 0) __syncthreads();   // V (and at a layer change the tap table) of slab it − 1 consumed
+#if SKP_MAPS_PRIO
+    __builtin_amdgcn_s_setprio(SKP_MAPS_PRIO);   // the staging's loads ahead of the other workgroup's pixels
+#endif
     stage(it);
+#if SKP_MAPS_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
     __syncthreads();
     const int l = it / H, bh = b * H + (it - l * H);
     const f4* V4 = reinterpret_cast<const f4*>(V + (it & 1) * vstride) + li;
