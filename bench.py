@@ -73,12 +73,18 @@ class KernelTimer:
 
 
 def _pmc_record(path, name, key, value):
-    """A PMC-derived figure for `name` from profiles/*.json, only if measured on this workload."""
+    """(figure, source) for `name` from a profiles/*.json PMC record, only if that record was
+    measured on this launch shape (key = (field, expected value)); source names the file, the
+    profiled workload and the counter method — the figure is NOT measured in this process."""
     try:
         rec = json.load(open(path)).get(name, {})
     except (OSError, ValueError):
-        return None
-    return rec.get(value) if rec.get(key[0]) == key[1] else None
+        return None, None
+    if rec.get(key[0]) != key[1] or rec.get(value) is None:
+        return None, None
+    src = {"file": os.path.relpath(path, REPO), "workload": rec.get("workload"), "method": rec.get("method"),
+           "measured_in_this_process": False}
+    return rec.get(value), src
 
 
 # ------------------------------------------------------------------------------ CPU baseline (port)
@@ -299,8 +305,9 @@ def main():
 
     if args.model == "sdxl" and args.res == 512:
         args.res = 1024
-    name = "stabilityai/stable-diffusion-xl-base-1.0" if args.model == "sdxl" else "runwayml/stable-diffusion-v1-5"
-    ldm, controllers, num_gpus = load_ldm(dev, name, feature_upsample_res=args.upsample_res)
+    # explicit seeded random weights (load_ldm raises for a hub name it cannot load offline)
+    ldm, controllers, num_gpus = load_ldm(dev, "random-xl" if args.model == "sdxl" else "random",
+                                          feature_upsample_res=args.upsample_res)
     if args.gc_freeze:
         import gc
         gc.collect()
@@ -312,7 +319,7 @@ def main():
     data = SyntheticDataset(n=16, size=args.res, seed=rank)
     imgs = [data[i]["img"][None].to(dev) for i in range(len(data))]
     timer = KernelTimer(["skp_aggregate", "skp_capture_fwd", "skp_capture_bwd", "skp_capture_maps_fwd",
-                         "skp_capture_maps_bwd"])
+                         "skp_capture_maps_bwd", "skp_capture_maps_bwd_sel"])
     ops.set_kernel_timer(timer)
 
     counter = [0]
@@ -367,35 +374,50 @@ def main():
     roof = None
     extra = {}
     fw = timer.summary("skp_capture_maps_fwd")
-    bw = timer.summary("skp_capture_maps_bwd")
     valu_json = os.path.join(REPO, "profiles", "pmc_valu.json")
+    timing_src = ("HIP events around every launch in the timed region, on the launching stream "
+                  "(bench.py KernelTimer)")
     if fw:
         flops = fw["flop_per_launch"]   # ops.capture_maps_flops of the launch's (B, H, N, R, sizes)
         t = fw["avg_ms"] * 1e-3
-        traffic = _pmc_record(args.traffic, "skp_capture_maps_fwd", ("algorithmic_bytes_per_launch", fw["bytes_per_launch"]),
-                              "hbm_bytes_per_launch")
+        traffic, traffic_src = _pmc_record(args.traffic, "skp_capture_maps_fwd",
+                                           ("algorithmic_bytes_per_launch", fw["bytes_per_launch"]),
+                                           "hbm_bytes_per_launch")
+        vb, vb_src = _pmc_record(valu_json, "skp_capture_maps_fwd", ("flop_per_launch", flops), "valu_busy")
         roof = {"kernel": "skp_capture_maps_fwd", "bound": "valu", "achieved": flops / t / 1e12,
                 "peak": VALU_F32_PEAK / 1e12, "unit": "TFLOP/s", "frac": flops / t / VALU_F32_PEAK,
-                "traffic": traffic, "avg_launch_ms": fw["avg_ms"], "launches": fw["launches"],
+                "traffic": traffic, "traffic_source": traffic_src, "avg_launch_ms": fw["avg_ms"],
+                "launches": fw["launches"], "timing_source": timing_src,
                 "algorithmic_flop_per_launch": flops, "algorithmic_bytes_per_launch": fw["bytes_per_launch"],
                 "hbm_achieved_GBps": fw["bytes_per_launch"] / t / 1e9,
                 "hbm_frac": fw["bytes_per_launch"] / t / HBM_PEAK,
-                "valu_busy_pmc": _pmc_record(valu_json, "skp_capture_maps_fwd", ("flop_per_launch", flops), "valu_busy"),
+                "valu_busy_pmc": vb, "valu_busy_source": vb_src,
                 "flop_model": "15 FLOP per (image, head, layer, pixel, token) + 8 per (row, low-res column, token); "
                               "ops.capture_maps_flops"}
-    if bw:
-        t = bw["avg_ms"] * 1e-3
-        extra["skp_capture_maps_bwd"] = {"avg_ms": bw["avg_ms"], "launches": bw["launches"],
-                                         "TFLOP/s": bw["flop_per_launch"] / t / 1e12,
-                                         "valu_frac": bw["flop_per_launch"] / t / VALU_F32_PEAK,
-                                         "GB/s_algorithmic": bw["bytes_per_launch"] / t / 1e9}
+    for name, model in (("skp_capture_maps_bwd_sel", "20 FLOP per (image, head, layer, pixel, token) + 16 per (row, "
+                         "low-res column, token): the dense part; ops.capture_maps_sel_bwd_flops"),
+                        ("skp_capture_maps_bwd", "24 FLOP per (image, head, layer, pixel, token) + 16 per (row, "
+                         "low-res column, token); ops.capture_maps_bwd_flops")):
+        bw = timer.summary(name)
+        if bw:
+            t = bw["avg_ms"] * 1e-3
+            vb, vb_src = _pmc_record(valu_json, name, ("flop_per_launch", bw["flop_per_launch"]), "valu_busy")
+            extra[name] = {"bound": "valu", "avg_ms": bw["avg_ms"], "launches": bw["launches"],
+                           "timing_source": timing_src, "achieved": bw["flop_per_launch"] / t / 1e12,
+                           "peak": VALU_F32_PEAK / 1e12, "unit": "TFLOP/s",
+                           "frac": bw["flop_per_launch"] / t / VALU_F32_PEAK,
+                           "algorithmic_flop_per_call": bw["flop_per_launch"], "flop_model": model,
+                           "GB/s_algorithmic": bw["bytes_per_launch"] / t / 1e9,
+                           "algorithmic_bytes_per_call": bw["bytes_per_launch"],
+                           "valu_busy_pmc": vb, "valu_busy_source": vb_src}
     agg = timer.summary("skp_aggregate")
     if agg:
         achieved = agg["bytes_per_launch"] / (agg["avg_ms"] * 1e-3)
-        traffic = _pmc_record(args.traffic, "skp_aggregate", ("algorithmic_bytes_per_launch", agg["bytes_per_launch"]),
-                              "hbm_bytes_per_launch")
+        traffic, traffic_src = _pmc_record(args.traffic, "skp_aggregate",
+                                           ("algorithmic_bytes_per_launch", agg["bytes_per_launch"]),
+                                           "hbm_bytes_per_launch")
         rec_a = {"kernel": "skp_aggregate", "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
-                 "unit": "GB/s", "frac": achieved / HBM_PEAK, "traffic": traffic,
+                 "unit": "GB/s", "frac": achieved / HBM_PEAK, "traffic": traffic, "traffic_source": traffic_src,
                  "avg_launch_ms": agg["avg_ms"], "launches": agg["launches"],
                  "algorithmic_bytes_per_launch": agg["bytes_per_launch"],
                  "frac_of_measured_copy": achieved / HBM_MEASURED_COPY}
@@ -433,7 +455,8 @@ def main():
                "config": {"workload": workload,
                           "global_batch": world * args.accum, "tokens": args.tokens, "image_res": args.res,
                           "feature_upsample_res": args.upsample_res, "micro_batch": mb,
-                          "parallelism": f"dp{world} (RCCL grad all-reduce)",
+                          "parallelism": (f"dp{world} ({'RCCL' if backend == 'nccl' else backend} all-reduce of the "
+                                          "token-embedding gradient)" if world > 1 else "dp1 (single process, no collective)"),
                           "tuned_gemms": _tuned_gemms_in_use()},
                "roofline": roof, "cpu_baseline": cpu, "kernels": extra,
                "last_loss": float(rec["loss"])}

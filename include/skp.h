@@ -74,6 +74,22 @@ int skp_capture_maps_bwd(const float* const* z_low, const int* sizes, int L, int
                          const float* dmaps, float gscale, const float* const* stats, float* const* dz_low,
                          float* workspace, void* stream);
 
+/* Backward of skp_capture_maps_fwd for a SPARSE per-image map gradient — the token-opt losses
+ * read only the selected token rows maps[b, tok] (optimize.py:403-424 sharpening / equivariance
+ * on top_embedding_indices), so image b's gradient is gsel[b, k] (R*R) at token sel_tok[b, k]
+ * (int64, −1 = unused slot; duplicates add), zero elsewhere.  Same result as
+ * skp_capture_maps_bwd on the scattered dense gradient, without forming it:
+ *   dZ = a ⊙ (g − dot) = [a_k·g_k at the K selected tokens] − dot·a,  dot = Σ_k a_k·g_k,
+ * the dense part needing one scalar per pixel.  K <= 32, N % 4 == 0, stats REQUIRED (the
+ * forward's), dz_low / z_low 16-B aligned.  workspace: skp_capture_maps_bwd_sel_workspace()
+ * floats, 16-B aligned (returns -1 on a bad shape).  R = s·{4, 8, 16} for R in {32, 64, 128}
+ * take the fast kernels; other shapes scatter into a dense gradient and run
+ * skp_capture_maps_bwd.  Deterministic (no atomics).                                   */
+long long skp_capture_maps_bwd_sel_workspace(const int* sizes, int L, int B, int H, int N, int R, int K);
+int skp_capture_maps_bwd_sel(const float* const* z_low, const int* sizes, int L, int B, int H, int N, int R,
+                             const long long* sel_tok, int K, const float* gsel, float gscale,
+                             const float* const* stats, float* const* dz_low, float* workspace, void* stream);
+
 /* ---------------------------------------------------------------- A3 aggregate
  * optimize.collect_maps (optimize.py:27-79), token-major output:
  * out[m, p] = (1/(L·BH)) Σ_l Σ_b attn_l[b, p, idx(m)], idx = indices[m] or m.

@@ -113,6 +113,31 @@ def capture_bwd(z_low, s, R, dattn):
     return dz.transpose(0, 2, 3, 1).reshape(H, S, N).astype(np.float32)
 
 
+def capture_maps_bwd_sel(z_layers, sizes, B, H, R, tok, gsel, gscale, heads=None):
+    """d z_low of every captured layer for a SPARSE per-image map gradient (the
+    skp_capture_maps_bwd_sel contract): image b's map gradient is gsel[b, k] (R*R) at token
+    tok[b, k] (-1 = unused; duplicates add), zero elsewhere — the gradient the reference's
+    losses produce, which read only maps[top_embedding_indices] (optimize.py:403-424) — scaled
+    by gscale (1/(L*H): collect_maps' mean, optimize.py:75), broadcast over the image's H heads,
+    then capture_bwd per head.  ``heads``: optional list of (b*H + h) rows to compute (the
+    full-size tests check a subset).  Returns per layer (len(rows), s*s, N)."""
+    N = z_layers[0].shape[-1]
+    rows = list(range(B * H)) if heads is None else list(heads)
+    out = []
+    dense = np.zeros((B, N, R * R), np.float32)
+    for b in range(B):
+        for k in range(tok.shape[1]):
+            if tok[b, k] >= 0:
+                dense[b, tok[b, k]] += gsel[b, k].reshape(R * R)
+    for z, s in zip(z_layers, sizes):
+        res = []
+        for bh in rows:
+            g = (dense[bh // H] * F32(gscale)).T[None]             # (1, R*R, N)
+            res.append(capture_bwd(z[bh:bh + 1], s, R, g)[0])
+        out.append(np.stack(res))
+    return out
+
+
 def heads_split(t, H):
     """(B, S, H*d) -> (B*H, S, d) — CrossAttention.reshape_heads_to_batch_dim (diffusers 0.8.0)."""
     b, s, hd = t.shape

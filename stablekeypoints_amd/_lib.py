@@ -23,6 +23,9 @@ _SIGS = {
                              ctypes.POINTER(_p), _p],
     "skp_capture_maps_bwd": [ctypes.POINTER(_p), ctypes.POINTER(_c_int), _c_int, _c_int, _c_int, _c_int, _c_int, _p,
                              _c_float, ctypes.POINTER(_p), ctypes.POINTER(_p), _p, _p],
+    "skp_capture_maps_bwd_sel": [ctypes.POINTER(_p), ctypes.POINTER(_c_int), _c_int, _c_int, _c_int, _c_int, _c_int,
+                                 _p, _c_int, _p, _c_float, ctypes.POINTER(_p), ctypes.POINTER(_p), _p, _p],
+    "skp_capture_maps_bwd_sel_workspace": [ctypes.POINTER(_c_int), _c_int, _c_int, _c_int, _c_int, _c_int, _c_int],
     "skp_aggregate": [ctypes.POINTER(_p), _c_int, _c_int, _c_int, _c_int, _p, _c_int, _p, _p],
     "skp_resize_bilinear": [_p, _c_int, _c_int, _c_int, _p, _p],
     "skp_resize_bilinear_bwd": [_p, _c_int, _c_int, _c_int, _p, _p],
@@ -64,6 +67,9 @@ _SIGS = {
 }
 
 
+_RESTYPE = {"skp_capture_maps_bwd_sel_workspace": _c_ll}
+
+
 class SkpLibraryError(RuntimeError):
     pass
 
@@ -85,7 +91,7 @@ def lib():
         for name, args in _SIGS.items():
             f = getattr(L, name)
             f.argtypes = args
-            f.restype = _c_int
+            f.restype = _RESTYPE.get(name, _c_int)
         L.skp_last_error.argtypes = []
         L.skp_last_error.restype = ctypes.c_char_p
         _lib = L

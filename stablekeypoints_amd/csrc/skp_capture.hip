@@ -1402,6 +1402,7 @@ extern "C" int skp_capture_maps_bwd(const float* const* z_low, const int* sizes,
   SKP_CHECK_ARG(B > 0 && H > 0 && N > 0 && R > 0, "non-positive shape");
   SKP_CHECK_ARG(N % 4 == 0, "N must be a multiple of 4 (use skp_capture_bwd)");
   SKP_CHECK_ARG(N <= 1024, "N > 1024 tokens is not supported");
+  SKP_CHECK_ARG(R <= 1024, "R > 1024 is not supported (capture_bwd_cols_kernel tap tables)");
   SKP_CHECK_ARG(bwd_row_lds(R, N <= 256 ? 1 : (N <= 512 ? 2 : 4)) <= 160 * 1024, "R * N too large for LDS");
   SKP_CHECK_ARG((long long)B * H <= 65535 && (long long)B * H * R < (1LL << 31), "shape too large");
   SKP_CHECK_ARG((reinterpret_cast<uintptr_t>(workspace) & 15) == 0, "workspace must be 16-B aligned");
@@ -1426,7 +1427,8 @@ extern "C" int skp_capture_maps_bwd(const float* const* z_low, const int* sizes,
   const int nq = N / 4;
   for (int l = 0; l < L; ++l) {
     const int s = sizes[l];
-    const float* stl = stats ? stats[l] : nullptr;
+    // the row kernel reads the stats as float4 pixel pairs: 16-B aligned rows need an even R
+    const float* stl = (stats && (R % 2) == 0) ? stats[l] : nullptr;
     if (nq <= 64) launch_bwd_row<1>(z_low[l], B, H, s, N, R, gT, stl, ws, st);
     else if (nq <= 128) launch_bwd_row<2>(z_low[l], B, H, s, N, R, gT, stl, ws, st);
     else launch_bwd_row<4>(z_low[l], B, H, s, N, R, gT, stl, ws, st);

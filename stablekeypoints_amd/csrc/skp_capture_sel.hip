@@ -1,0 +1,470 @@
+// Backward of the fused capture + per-image aggregate (skp_capture_maps_fwd) for a SPARSE map
+// gradient: the token-optimisation loss only reads maps[b, tok] for the few tokens the
+// selection kept (reference optimize.py:403-424: sharpening and equivariance losses on
+// top_embedding_indices), so the map gradient of image b is nonzero only in K token rows.
+//
+// Per layer l, head bh = b·H + h, output pixel p and token n, with a = softmax_n(z(p)) rebuilt
+// from the forward's per-pixel (max, 1/Σ) and g the (scaled) map gradient:
+//     dZ[p, n] = a[p, n]·(g[p, n] − dot[p]),   dot[p] = Σ_n a[p, n]·g[p, n] = Σ_k a[p, tok_k]·g_k[p]
+// which splits into
+//   - a sparse part  a[p, tok_k]·g_k[p]   (K tokens; e_k[p] below), and
+//   - a dense part  −dot[p]·a[p, n]       (every token, but with ONE scalar per pixel instead of a
+//                                           gradient row: no (B, N, R²) gradient, no transpose, no
+//                                           per-pixel 500-token reduction).
+// dz_low = bicubicᵀ(dZ) (the adjoint of the s→R upsampling, ptp_utils.py:513-529).
+//
+// Kernels (per layer):
+//   sel_gather   zsel[bh][q][k] = z_low[bh][q][tok_k]                         (the selected logits)
+//   sel_dot      per (bh, row y): a_k, e_k = a_k·g_k, dot → E[bh][k][p] = e_k, pix[bh][p] = (mb, −dot)
+//                with mb = log2(1/Σ) − max·log2e, so a = exp2(z·log2e + mb)
+//   sel_adj      per (bh, k): es[bh][k] = bicubicᵀ(E[bh][k])  (R² → s², gather form, deterministic)
+//   sel_dense    per (bh, 128-token chunk): the dense part's adjoint, plus es at the selected tokens
+// sel_dense is the hot kernel.  One workgroup = R/16 waves; wave w owns output columns
+// [16w, 16w+16) of every row and lanes own token pairs (packed f32: v_pk_fma).  With R = S·RATIO
+// (RATIO a power of two, 4..16) the bicubic taps of a wave's pixels relative to its band are the
+// same for every wave and every row group, so the horizontal taps, the pixel loop and the register
+// indices are compile-time; the tap weights (RATIO distinct sets) sit in SGPRs, and so do the
+// per-pixel (mb, d) pairs.  Registers per lane hold
+//   Zw[4][NC]  the 4 low-res z rows the current output rows interpolate (band columns),
+//   V[NC]      their vertical pass for the current row,   Hs[NC] its horizontal adjoint,
+//   acc[4][NC] the vertical adjoint of the 4 low-res rows the current rows touch.
+// A low-res row is complete when the rows' first tap moves past it: the waves' band partials are
+// merged through LDS in a fixed order (bands overlap by NC − 16/RATIO columns; virtual columns
+// and rows past the edges fold into 0 / s−1 exactly as torch's clamped taps), the sparse es is
+// added at the selected tokens, and the row leaves as coalesced 512-B token runs.
+// Every output element has one owner and a fixed summation order: deterministic, no atomics.
+#include <algorithm>
+
+#include "skp_common.h"
+
+using namespace skp;
+
+namespace {
+
+constexpr float L2E = 1.4426950408889634f;
+constexpr int SEL_MAXK = 32;
+constexpr int PW = 16;   // output pixels per wave and row
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// first bicubic tap (before clamping) of output index t relative to its ratio group:
+// floor((t + 0.5)/RATIO − 0.5) − 1, exact in integers for a power-of-two RATIO
+constexpr int floor_div(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+constexpr int lo_rel(int t, int ratio) { return floor_div(2 * t + 1 - ratio, 2 * ratio) - 1; }
+
+// ------------------------------------------------------------------------------ sel_gather
+__global__ void sel_gather_kernel(const float* __restrict__ z, int BH, int SS, int N, int H,
+                                  const long long* __restrict__ tok, int K, float* __restrict__ zsel) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long total = (long long)BH * SS * K;
+  if (e >= total) return;
+  const int k = (int)(e % K);
+  const long long bq = e / K;   // bh·SS + q
+  const int bh = (int)(bq / SS);
+  const long long t = tok[(long long)(bh / H) * K + k];
+  zsel[e] = (t >= 0 && t < N) ? z[bq * N + t] : 0.0f;
+}
+
+// ------------------------------------------------------------------------------ sel_dot
+// one block per (bh, y); threads over x.  LDS: the vertical pass Vs[S][K] of the selected logits.
+__global__ __launch_bounds__(256) void sel_dot_kernel(const float* __restrict__ zsel, int S, int R, int H, int K,
+                                                      const long long* __restrict__ tok,
+                                                      const float* __restrict__ gsel, float gscale,
+                                                      const float2* __restrict__ stats, float* __restrict__ E,
+                                                      float2* __restrict__ pix) {
+  extern __shared__ float Vs[];   // S × K
+  const int bh = blockIdx.x / R, y = blockIdx.x % R;
+  const int b = bh / H;
+  const Taps4 ty = bicubic_taps(y, S, R);
+  const float* zb = zsel + (size_t)bh * S * S * K;
+  for (int e = threadIdx.x; e < S * K; e += blockDim.x) {
+    const int j = e / K, k = e - j * K;
+    float v = ty.w[0] * zb[((size_t)ty.i[0] * S + j) * K + k];
+    v = fmaf(ty.w[1], zb[((size_t)ty.i[1] * S + j) * K + k], v);
+    v = fmaf(ty.w[2], zb[((size_t)ty.i[2] * S + j) * K + k], v);
+    v = fmaf(ty.w[3], zb[((size_t)ty.i[3] * S + j) * K + k], v);
+    Vs[e] = v;
+  }
+  __syncthreads();
+  const size_t RR = (size_t)R * R;
+  for (int x = threadIdx.x; x < R; x += blockDim.x) {
+    const Taps4 tx = bicubic_taps(x, S, R);
+    const size_t p = (size_t)y * R + x;
+    const float2 st = stats[(size_t)bh * RR + p];
+    const float mb = __builtin_amdgcn_logf(st.y) - st.x * L2E;   // v_log_f32 = log2
+    float dot = 0.0f;
+    for (int k = 0; k < K; ++k) {
+      float e = 0.0f;
+      if (tok[(size_t)b * K + k] >= 0) {
+        float z = tx.w[0] * Vs[tx.i[0] * K + k];
+        z = fmaf(tx.w[1], Vs[tx.i[1] * K + k], z);
+        z = fmaf(tx.w[2], Vs[tx.i[2] * K + k], z);
+        z = fmaf(tx.w[3], Vs[tx.i[3] * K + k], z);
+        const float a = __builtin_amdgcn_exp2f(fmaf(z, L2E, mb));
+        e = a * (gsel[((size_t)b * K + k) * RR + p] * gscale);
+      }
+      dot += e;
+      E[((size_t)bh * K + k) * RR + p] = e;
+    }
+    pix[(size_t)bh * RR + p] = make_float2(mb, -dot);
+  }
+}
+
+// ------------------------------------------------------------------------------ sel_adj
+// es[bh][k][i][j] = Σ_y Σ_x wy(y→i)·wx(x→j)·E[bh][k][y][x]: separable gather through LDS.
+__device__ __forceinline__ float adj_w(int dst, int src, int n_in, int n_out) {   // weight of dst's taps on src
+  const Taps4 t = bicubic_taps(dst, n_in, n_out);
+  float w = 0.0f;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) w += (t.i[m] == src) ? t.w[m] : 0.0f;
+  return w;
+}
+// output indices whose taps can reach low-res index j: src ∈ [j − 2, j + 2) (clamped edges included)
+__device__ __forceinline__ void adj_range(int j, int S, int R, int& lo, int& hi) {
+  const float r = (float)R / (float)S;
+  lo = max(0, (int)floorf((j - 1.5f) * r - 0.5f) - 1);
+  hi = min(R - 1, (int)ceilf((j + 2.5f) * r - 0.5f) + 1);
+  if (j == 0) lo = 0;
+  if (j == S - 1) hi = R - 1;
+}
+
+__global__ __launch_bounds__(256) void sel_adj_kernel(const float* __restrict__ E, int S, int R, int K,
+                                                      float* __restrict__ es) {
+  extern __shared__ float Hs[];   // R × S
+  const size_t bk = blockIdx.x;   // bh·K + k
+  const float* Eb = E + bk * (size_t)R * R;
+  for (int e = threadIdx.x; e < R * S; e += blockDim.x) {
+    const int y = e / S, j = e - y * S;
+    int x0, x1;
+    adj_range(j, S, R, x0, x1);
+    float acc = 0.0f;
+    for (int x = x0; x <= x1; ++x) {
+      const float w = adj_w(x, j, S, R);
+      if (w != 0.0f) acc = fmaf(w, Eb[(size_t)y * R + x], acc);
+    }
+    Hs[e] = acc;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < S * S; e += blockDim.x) {
+    const int i = e / S, j = e - i * S;
+    int y0, y1;
+    adj_range(i, S, R, y0, y1);
+    float acc = 0.0f;
+    for (int y = y0; y <= y1; ++y) {
+      const float w = adj_w(y, i, S, R);
+      if (w != 0.0f) acc = fmaf(w, Hs[y * S + j], acc);
+    }
+    es[bk * (size_t)S * S + e] = acc;
+  }
+}
+
+// ------------------------------------------------------------------------------ sel_dense
+struct SelLayers {   // up to 4 layers of the same s in one launch
+  const float* z[4];
+  const float2* pix[4];
+  const float* es[4];
+  float* dz[4];
+};
+
+template <int RATIO, int S>
+__global__ __launch_bounds__((S * RATIO / PW) * WAVE) __attribute__((amdgpu_waves_per_eu(2)))
+void sel_dense_kernel(SelLayers sl, int BH, int H, int N, int K, const long long* __restrict__ tok, int nchunk,
+                      int njobs) {
+  constexpr int R = S * RATIO;
+  constexpr int WAVES = R / PW;
+  constexpr int CS = PW / RATIO;                  // band step in low-res columns
+  constexpr int NC = lo_rel(PW - 1, RATIO) + 6;   // band columns: relative −2 … lo_rel(PW−1)+3
+  constexpr int NTH = WAVES * WAVE;
+  static_assert(R % PW == 0 && PW % RATIO == 0, "band geometry");
+  __shared__ __attribute__((aligned(16))) f2 M[WAVES][NC][WAVE];   // band partials of one low-res row
+
+  // XCD-major job order: XCD x walks a contiguous job range, so a head's 128-token chunks share
+  // one L2 (its z_low slab)
+  const int per = (njobs + 7) / 8;
+  const int job = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  if (job >= njobs) return;
+  const int chunk = job % nchunk;
+  const int bh = (job / nchunk) % BH;
+  const int l = job / (nchunk * BH);
+  const int b = bh / H;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n0 = chunk * 128 + 2 * lane;
+  const int nl = min(n0, N - 2);                   // clamped load position (N even)
+  const float* zl = sl.z[l] + (size_t)bh * S * S * N;
+  const float2* pixl = sl.pix[l] + (size_t)bh * R * R;
+  float* dzl = sl.dz[l] + (size_t)bh * S * S * N;
+  const float* esl = sl.es[l] + (size_t)bh * K * S * S;
+
+  // tap weights of the RATIO phases (identical for rows and columns): lane u < RATIO computes
+  // phase u's taps exactly as the forward did, then every lane reads them as uniform values
+  float wt[RATIO][4];
+  {
+    const Taps4 t = bicubic_taps(lane < RATIO ? lane : 0, S, R);
+#pragma unroll
+    for (int u = 0; u < RATIO; ++u)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        wt[u][m] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t.w[m]), u));
+  }
+  auto col_abs = [&](int c) { return min(max(w * CS + c - 2, 0), S - 1); };
+  auto load_row = [&](int r, f2 (&dst)[NC]) {   // z_low row r (clamped), the band's columns, this lane's pair
+    const int rr = min(max(r, 0), S - 1);
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      dst[c] = *reinterpret_cast<const f2*>(zl + ((size_t)rr * S + col_abs(c)) * N + nl);
+  };
+
+  f2 Zw[4][NC], acc[4][NC];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    load_row(k - 2, Zw[k]);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[k][c] = (f2)0.0f;
+  }
+  const f2 l2e = (f2)L2E;
+
+  auto emit = [&](int r, const f2 (&v)[NC]) {   // low-res row r complete: merge bands, add es, store
+#pragma unroll
+    for (int c = 0; c < NC; ++c) M[w][c][lane] = v[c];
+    __syncthreads();
+    for (int e = tid; e < S * WAVE; e += NTH) {
+      const int j = e >> 6, ln = e & 63;
+      f2 s = (f2)0.0f;
+      for (int w2 = 0; w2 < WAVES; ++w2) {   // contributors in a fixed order: band, then column
+        for (int c = 0; c < NC; ++c) {
+          const int a = min(max(w2 * CS + c - 2, 0), S - 1);
+          if (a == j) s += M[w2][c][ln];
+        }
+      }
+      const int n = chunk * 128 + 2 * ln;
+      if (n < N) {
+        for (int k = 0; k < K; ++k) {   // the sparse part at the selected tokens (k order)
+          const long long t = tok[(size_t)b * K + k];
+          if (t == n) s.x += esl[((size_t)k * S + r) * S + j];
+          if (t == n + 1) s.y += esl[((size_t)k * S + r) * S + j];
+        }
+        *reinterpret_cast<f2*>(dzl + ((size_t)r * S + j) * N + n) = s;
+      }
+    }
+    __syncthreads();
+  };
+
+  // phases: lo = first tap row of the output rows y = RATIO·(lo + 1) + RATIO/2 + v, v = 0..RATIO−1
+  for (int lo = -2; lo <= S - 2; ++lo) {
+#pragma unroll
+    for (int v = 0; v < RATIO; ++v) {
+      const int y = RATIO * (lo + 1) + RATIO / 2 + v;
+      if (y < 0 || y >= R) continue;   // the first and last phases have RATIO/2 rows
+      const int u = (RATIO / 2 + v) % RATIO;   // row phase (compile-time)
+      f2 V[NC], Hs[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        f2 t = Zw[0][c] * wt[u][0];
+        t = __builtin_elementwise_fma(Zw[1][c], (f2)wt[u][1], t);
+        t = __builtin_elementwise_fma(Zw[2][c], (f2)wt[u][2], t);
+        t = __builtin_elementwise_fma(Zw[3][c], (f2)wt[u][3], t);
+        V[c] = t;
+        Hs[c] = (f2)0.0f;
+      }
+      const float2* pp = pixl + (size_t)y * R + w * PW;
+#pragma unroll
+      for (int t = 0; t < PW; ++t) {
+        const int ut = t % RATIO;
+        const int c0 = lo_rel(t, RATIO) + 2;                             // band slot of the first tap
+        const float2 pd = pp[t];                                         // (mb, d), uniform
+        f2 zv = V[c0] * wt[ut][0];
+        zv = __builtin_elementwise_fma(V[c0 + 1], (f2)wt[ut][1], zv);
+        zv = __builtin_elementwise_fma(V[c0 + 2], (f2)wt[ut][2], zv);
+        zv = __builtin_elementwise_fma(V[c0 + 3], (f2)wt[ut][3], zv);
+        f2 ex = __builtin_elementwise_fma(zv, l2e, (f2)pd.x);
+        ex.x = __builtin_amdgcn_exp2f(ex.x);
+        ex.y = __builtin_amdgcn_exp2f(ex.y);
+        ex *= pd.y;
+        Hs[c0] = __builtin_elementwise_fma(ex, (f2)wt[ut][0], Hs[c0]);
+        Hs[c0 + 1] = __builtin_elementwise_fma(ex, (f2)wt[ut][1], Hs[c0 + 1]);
+        Hs[c0 + 2] = __builtin_elementwise_fma(ex, (f2)wt[ut][2], Hs[c0 + 2]);
+        Hs[c0 + 3] = __builtin_elementwise_fma(ex, (f2)wt[ut][3], Hs[c0 + 3]);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) acc[k][c] = __builtin_elementwise_fma(Hs[c], (f2)wt[u][k], acc[k][c]);
+    }
+    // virtual row lo is complete
+    if (lo < 0) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) acc[1][c] += acc[0][c];   // rows −2, −1 clamp to row 0 (next slot)
+    } else {
+      emit(lo, acc[0]);
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      acc[0][c] = acc[1][c]; acc[1][c] = acc[2][c]; acc[2][c] = acc[3][c]; acc[3][c] = (f2)0.0f;
+      Zw[0][c] = Zw[1][c]; Zw[1][c] = Zw[2][c]; Zw[2][c] = Zw[3][c];
+    }
+    if (lo + 1 <= S - 2) load_row(lo + 4, Zw[3]);   // rows lo+1 … lo+4 for the next phase
+  }
+  // the window now holds virtual rows S−1, S, S+1, S+2: all clamp to row S−1
+#pragma unroll
+  for (int c = 0; c < NC; ++c) acc[0][c] = (acc[0][c] + acc[1][c]) + (acc[2][c] + acc[3][c]);
+  emit(S - 1, acc[0]);
+}
+
+template <int RATIO, int S>
+void launch_dense(const SelLayers& sl, int nl, int BH, int H, int N, int K, const long long* tok, hipStream_t st) {
+  const int nchunk = (N + 127) / 128;
+  const int njobs = nl * BH * nchunk;
+  const int grid = 8 * ((njobs + 7) / 8);
+  hipLaunchKernelGGL((sel_dense_kernel<RATIO, S>), dim3(grid), dim3((S * RATIO / PW) * WAVE), 0, st, sl, BH, H, N, K,
+                     tok, nchunk, njobs);
+}
+
+// (R, S) pairs with a compiled sel_dense kernel
+bool dense_launch(int R, int S, const SelLayers& sl, int nl, int BH, int H, int N, int K, const long long* tok,
+                  hipStream_t st) {
+#define SKP_SEL_CASE(RR, SS)                                               \
+  if (R == RR && S == SS) {                                               \
+    launch_dense<RR / SS, SS>(sl, nl, BH, H, N, K, tok, st);               \
+    return true;                                                          \
+  }
+  SKP_SEL_CASE(128, 16)
+  SKP_SEL_CASE(128, 32)
+  SKP_SEL_CASE(128, 8)
+  SKP_SEL_CASE(64, 16)
+  SKP_SEL_CASE(64, 8)
+  SKP_SEL_CASE(64, 4)
+  SKP_SEL_CASE(32, 8)
+  SKP_SEL_CASE(32, 4)
+#undef SKP_SEL_CASE
+  return false;
+}
+
+bool dense_supported(int R, int S) {
+  const int pairs[][2] = {{128, 16}, {128, 32}, {128, 8}, {64, 16}, {64, 8}, {64, 4}, {32, 8}, {32, 4}};
+  for (auto& p : pairs)
+    if (p[0] == R && p[1] == S) return true;
+  return false;
+}
+
+// dense gradient from the sparse one (fallback): g[b][tok_k][p] = Σ_k gsel[b][k][p] (k order)
+__global__ void sel_scatter_kernel(const long long* __restrict__ tok, const float* __restrict__ gsel, int B, int K,
+                                   int N, long long RR, float* __restrict__ g) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;   // (b, p)
+  if (e >= (long long)B * RR) return;
+  const int b = (int)(e / RR);
+  const long long p = e % RR;
+  for (int k = 0; k < K; ++k) {
+    const long long t = tok[(long long)b * K + k];
+    if (t >= 0 && t < N) g[((long long)b * N + t) * RR + p] += gsel[((long long)b * K + k) * RR + p];
+  }
+}
+
+struct SelWs {   // workspace carve-up (floats)
+  size_t zsel, E, pix, es, total;
+};
+SelWs sel_ws(const int* sizes, int L, int B, int H, int R, int K) {
+  SelWs w{};
+  size_t smax2 = 1;
+  for (int l = 0; l < L; ++l) smax2 = std::max(smax2, (size_t)sizes[l] * sizes[l]);
+  const size_t BH = (size_t)B * H, RR = (size_t)R * R;
+  w.zsel = 0;
+  w.E = w.zsel + ((BH * smax2 * K + 3) & ~(size_t)3);
+  w.pix = w.E + ((BH * K * RR + 3) & ~(size_t)3);
+  w.es = w.pix + (size_t)L * BH * RR * 2;
+  w.total = w.es + (size_t)L * BH * K * smax2;
+  return w;
+}
+
+bool fast_path(const int* sizes, int L, int R, int N) {
+  if (N % 2 != 0 || N < 2) return false;
+  for (int l = 0; l < L; ++l)
+    if (!dense_supported(R, sizes[l])) return false;
+  return true;
+}
+
+}  // namespace
+
+extern "C" long long skp_capture_maps_bwd_sel_workspace(const int* sizes, int L, int B, int H, int N, int R, int K) {
+  if (!sizes || L <= 0 || L > SKP_MAX_LAYERS || B <= 0 || H <= 0 || N <= 0 || R <= 0 || K <= 0) return -1;
+  int smax = 1;
+  for (int l = 0; l < L; ++l) smax = std::max(smax, sizes[l]);
+  if (fast_path(sizes, L, R, N)) return (long long)sel_ws(sizes, L, B, H, R, K).total;
+  // fallback: the dense (B, N, R²) gradient + skp_capture_maps_bwd's workspace
+  const long long RR = (long long)R * R;
+  return (long long)B * N * RR + (long long)B * RR * N + (long long)B * H * R * smax * N + 4;
+}
+
+extern "C" int skp_capture_maps_bwd_sel(const float* const* z_low, const int* sizes, int L, int B, int H, int N, int R,
+                                        const long long* sel_tok, int K, const float* gsel, float gscale,
+                                        const float* const* stats, float* const* dz_low, float* workspace,
+                                        void* stream) {
+  SKP_CHECK_ARG(z_low && sizes && sel_tok && gsel && stats && dz_low && workspace, "null pointer");
+  SKP_CHECK_ARG(L > 0 && L <= SKP_MAX_LAYERS, "L out of range");
+  SKP_CHECK_ARG(B > 0 && H > 0 && N > 0 && R > 0, "non-positive shape");
+  SKP_CHECK_ARG(K > 0 && K <= SEL_MAXK, "K must be in [1, 32]");
+  SKP_CHECK_ARG(N % 4 == 0 && N <= 1024, "N must be a multiple of 4, at most 1024");
+  SKP_CHECK_ARG((long long)B * H <= 65535 && (long long)B * H * R * R < (1LL << 31), "shape too large");
+  SKP_CHECK_ARG((reinterpret_cast<uintptr_t>(workspace) & 15) == 0, "workspace must be 16-B aligned");
+  for (int l = 0; l < L; ++l) {
+    SKP_CHECK_ARG(z_low[l] && dz_low[l] && stats[l], "null layer pointer");
+    SKP_CHECK_ARG(sizes[l] > 0 && sizes[l] <= R, "layer size must be in [1, R]");
+    SKP_CHECK_ARG((reinterpret_cast<uintptr_t>(z_low[l]) & 15) == 0 && (reinterpret_cast<uintptr_t>(dz_low[l]) & 15) == 0,
+                  "z_low / dz_low pointers must be 16-B aligned");
+  }
+  hipStream_t st = as_stream(stream);
+  const int BH = B * H;
+  const size_t RR = (size_t)R * R;
+  if (!fast_path(sizes, L, R, N)) {
+    // no compiled kernel for this (R, s): scatter into a dense gradient, then the dense backward
+    float* g = workspace;
+    SKP_CHECK_ARG(hipMemsetAsync(g, 0, (size_t)B * N * RR * sizeof(float), st) == hipSuccess, "memset failed");
+    hipLaunchKernelGGL(sel_scatter_kernel, dim3((unsigned)(((size_t)B * RR + 255) / 256)), dim3(256), 0, st, sel_tok,
+                       gsel, B, K, N, (long long)RR, g);
+    SKP_LAUNCH_CHECK();
+    float* rest = workspace + (((size_t)B * N * RR + 3) & ~(size_t)3);
+    return skp_capture_maps_bwd(z_low, sizes, L, B, H, N, R, g, gscale, stats, dz_low, rest, stream);
+  }
+  const SelWs wsz = sel_ws(sizes, L, B, H, R, K);
+  float* zsel = workspace + wsz.zsel;
+  float* E = workspace + wsz.E;
+  float2* pix = reinterpret_cast<float2*>(workspace + wsz.pix);
+  float* es = workspace + wsz.es;
+  int smax = 1;
+  for (int l = 0; l < L; ++l) smax = std::max(smax, sizes[l]);
+  for (int l = 0; l < L; ++l) {
+    const int S = sizes[l];
+    const long long tot = (long long)BH * S * S * K;
+    hipLaunchKernelGGL(sel_gather_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, z_low[l], BH, S * S, N,
+                       H, sel_tok, K, zsel);
+    SKP_LAUNCH_CHECK();
+    hipLaunchKernelGGL(sel_dot_kernel, dim3((unsigned)(BH * R)), dim3(std::min(R, 256)), (size_t)S * K * sizeof(float),
+                       st, zsel, S, R, H, K, sel_tok, gsel, gscale, reinterpret_cast<const float2*>(stats[l]), E,
+                       pix + (size_t)l * BH * RR);
+    SKP_LAUNCH_CHECK();
+    hipLaunchKernelGGL(sel_adj_kernel, dim3((unsigned)(BH * K)), dim3(256), (size_t)R * S * sizeof(float), st, E, S, R,
+                       K, es + (size_t)l * BH * K * smax * smax);
+    SKP_LAUNCH_CHECK();
+  }
+  // the dense part: layers of equal s share a launch (up to 4 per launch)
+  bool done[SKP_MAX_LAYERS] = {};
+  for (int l = 0; l < L; ++l) {
+    if (done[l]) continue;
+    SelLayers sl{};
+    int nl = 0;
+    for (int m = l; m < L && nl < 4; ++m) {
+      if (done[m] || sizes[m] != sizes[l]) continue;
+      sl.z[nl] = z_low[m];
+      sl.pix[nl] = pix + (size_t)m * BH * RR;
+      sl.es[nl] = es + (size_t)m * BH * K * smax * smax;
+      sl.dz[nl] = dz_low[m];
+      done[m] = true;
+      ++nl;
+    }
+    if (!dense_launch(R, sizes[l], sl, nl, BH, H, N, K, sel_tok, st)) {
+      SKP_CHECK_ARG(false, "internal: no sel_dense kernel for this shape");
+    }
+    SKP_LAUNCH_CHECK();
+  }
+  return SKP_OK;
+}

@@ -304,7 +304,7 @@ class CUBParts(torch.utils.data.Dataset):
         kp[vis, :2] *= scale
         sfm_pose[0] = sfm_pose[0] * scale
         sfm_pose[1] = sfm_pose[1] * scale
-        if self.split == "train" and self.rng.rand(1) > 0.5:   # mirror (cub_parts.py:392-412)
+        if self.split == "train" and self.rng.random() > 0.5:   # mirror (cub_parts.py:392-412); one draw, as rand(1)
             img = img[:, ::-1, :].copy()
             mask = mask[:, ::-1].copy()
             new_x = img.shape[1] - kp[:, 0] - 1

@@ -28,14 +28,16 @@ class RandomAffineWithInverse:
         theta[:, :2] = theta[:, :2] * scale
         return theta.unsqueeze(0)
 
-    def draw_theta(self, batch):
-        """invertable_transform.py:40-57 (same RNG calls, same order)."""
+    def draw_theta(self, batch, generator=None):
+        """invertable_transform.py:40-57 (same RNG calls, same order); ``generator``: a
+        torch.Generator instead of the global CPU generator the reference uses."""
         thetas = []
+        g = generator
         for _ in range(batch):
-            angle = torch.rand(1).item() * (2 * self.degrees) - self.degrees
-            sf = torch.rand(1).item() * (self.scale[1] - self.scale[0]) + self.scale[0]
-            tp = (torch.rand(1).item() * (2 * self.translate[0]) - self.translate[0],
-                  torch.rand(1).item() * (2 * self.translate[1]) - self.translate[1])
+            angle = torch.rand(1, generator=g).item() * (2 * self.degrees) - self.degrees
+            sf = torch.rand(1, generator=g).item() * (self.scale[1] - self.scale[0]) + self.scale[0]
+            tp = (torch.rand(1, generator=g).item() * (2 * self.translate[0]) - self.translate[0],
+                  torch.rand(1, generator=g).item() * (2 * self.translate[1]) - self.translate[1])
             thetas.append(self.create_affine_matrix(angle, sf, tp))
         return torch.cat(thetas, dim=0)
 

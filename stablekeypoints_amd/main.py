@@ -16,7 +16,8 @@ import torch
 def build_parser():
     p = argparse.ArgumentParser(description="optimize a class embedding")
     p.add_argument("--model_type", type=str, default="runwayml/stable-diffusion-v1-5",
-                   help="local directory of diffusers-0.8.0 UNet/VAE weights; other values: seeded random SD-1.5")
+                   help="local directory of diffusers-0.8.0 UNet/VAE weights, a hub name in the local Hugging Face "
+                        "cache, or 'random' / 'random-xl' / 'tiny' for seeded random weights (anything else raises)")
     p.add_argument("--dataset_loc", type=str, default="~")
     p.add_argument("--save_folder", type=str, default="outputs")
     p.add_argument("--wandb_name", type=str, default="temp")

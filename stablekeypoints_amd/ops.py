@@ -39,6 +39,13 @@ def _c(t, dtype=F32):
     return t.contiguous() if t.dtype == dtype else t.to(dtype).contiguous()
 
 
+def _c16(t):
+    """Contiguous fp32 with a 16-B aligned base (the float4 paths of libskp require it): a view
+    at an odd storage offset is copied."""
+    t = _c(t)
+    return t if t.data_ptr() % 16 == 0 else t.clone()
+
+
 # --------------------------------------------------------------------------- Q·Kᵀ on MFMA
 def bgemm(a, b, alpha=1.0, out=None, accumulate=False):
     """out[z] = alpha · a[z] @ b[z] for 3-D fp32 tensors of any strides (skp_bgemm_f32)."""
@@ -223,23 +230,18 @@ class CaptureMaps(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, B, R, sizes, *zs):
-        zs = [_c(z) for z in zs]
+        zs = [_c16(z) for z in zs]
         BH, _, N = zs[0].shape
         H = BH // B
         L = len(zs)
         dev = zs[0].device
         RR = R * R
-        # per-pixel softmax (max, 1/Σ) of every layer, kept for the backward (8 B per pixel-head)
-        stats = [torch.empty(BH, RR, 2, device=dev, dtype=F32) for _ in range(L)]
-        out = torch.empty(B, N, R, R, device=dev, dtype=F32)
         if FUSED_MAPS:
-            zp = (ctypes.c_void_p * L)(*[z.data_ptr() for z in zs])
-            sp = (ctypes.c_int * L)(*[int(s) for s in sizes])
-            stp = (ctypes.c_void_p * L)(*[st.data_ptr() for st in stats])
-            with _timed("skp_capture_maps_fwd", capture_maps_bytes(B, H, N, R, sizes), capture_maps_flops(B, H, N, R, sizes)):
-                call("skp_capture_maps_fwd", ctypes.cast(zp, ctypes.POINTER(ctypes.c_void_p)), sp, L, B, H, N, R,
-                     ptr(out), ctypes.cast(stp, ctypes.POINTER(ctypes.c_void_p)), stream(dev))
+            out, stats = _capture_maps_run(zs, sizes, B, R)
         else:
+            # per-pixel softmax (max, 1/Σ) of every layer, kept for the backward (8 B per pixel-head)
+            stats = [torch.empty(BH, RR, 2, device=dev, dtype=F32) for _ in range(L)]
+            out = torch.empty(B, N, R, R, device=dev, dtype=F32)
             attn = [torch.empty(BH, RR, N, device=dev, dtype=F32) for _ in range(L)]
             for z, a, st, s in zip(zs, attn, stats, sizes):
                 with _timed("skp_capture_fwd", (BH * RR * N + BH * s * s * N) * 4):
@@ -259,11 +261,16 @@ class CaptureMaps(torch.autograd.Function):
     def backward(ctx, dmaps):
         saved = ctx.saved_tensors
         L = len(saved) // 2
-        zs, stats = saved[:L], saved[L:]
-        B, H, R, N, sizes = ctx.meta
+        return (None, None, None) + tuple(CaptureMaps._dense_bwd(saved[:L], saved[L:], ctx.meta, dmaps))
+
+    @staticmethod
+    def _dense_bwd(zs, stats, meta, dmaps):
+        """dz_low of every layer for a dense per-image map gradient dmaps (B, N, R, R)."""
+        B, H, R, N, sizes = meta
         dmaps = _c(dmaps)                       # (B, N, R, R)
         RR = R * R
         scale = 1.0 / float(len(zs) * H)
+        L = len(zs)
         if FUSED_MAPS and N % 4 == 0:
             dzs = [torch.empty_like(z) for z in zs]
             ws = torch.empty(B * RR * N + B * H * R * max(sizes) * N, device=dmaps.device, dtype=F32)
@@ -280,12 +287,150 @@ class CaptureMaps(torch.autograd.Function):
         else:
             dzs = [capture_bwd(z, s, R, dmaps, gscale=scale, group=H, strides=(N * RR, 1, RR), stats=st)
                    for z, s, st in zip(zs, sizes, stats)]
-        return (None, None, None) + tuple(dzs)
+        return dzs
 
 
 def capture_maps(zs, sizes, B, R):
     """Per-image (B, N, R, R) maps from captured logits (see CaptureMaps)."""
     return CaptureMaps.apply(int(B), int(R), tuple(int(s) for s in sizes), *zs)
+
+
+# A/B: 0 = the selected rows' gradient goes through the dense (B, N, R²) map gradient and
+# skp_capture_maps_bwd, as in r02
+SEL_BWD = os.environ.get("SKP_SEL_BWD", "1") != "0"
+
+
+def capture_maps_sel_bwd_bytes(B, H, N, R, sizes, K):
+    """Algorithmic HBM bytes of one skp_capture_maps_bwd_sel call (fast path), per layer: z_low read
+    and dz_low written once, the stats read once, the per-pixel (mb, d) pairs and the K selected
+    rows' e = a·g written and read once, the K gradient rows read once."""
+    RR = R * R
+    BH = B * H
+    return 4 * sum(2 * BH * s * s * N + 2 * BH * RR + 4 * BH * RR + 2 * BH * K * RR + B * K * RR for s in sizes)
+
+
+def capture_maps_sel_bwd_flops(B, H, N, R, sizes):
+    """Algorithmic fp32 VALU work of the dense part of skp_capture_maps_bwd_sel: per (image, head,
+    layer, pixel, token) 20 FLOP — rebuild a (taps 8, exp argument 2, exp 1), ×(−dot) 1, horizontal
+    adjoint 8 — and per (row, low-res column, token) 8 each for the vertical pass and the vertical
+    adjoint.  (The sparse part, K tokens per pixel, is not counted.)"""
+    return sum(B * H * N * (20 * R * R + 16 * R * s) for s in sizes)
+
+
+class CapturedMaps:
+    """The fused capture's per-image maps (B, N, R, R) — computed without an autograd graph —
+    plus what the backward needs (the logits ``zs`` with their graph, the per-pixel softmax stats).
+
+    ``maps`` feeds the selection (no gradient, as in the reference: top-k / FPS run on detached
+    maps); ``select(rows)`` gathers the selected token rows of every image as ONE differentiable
+    (M, R, R) tensor whose backward is the sparse ``skp_capture_maps_bwd_sel``: the K selected rows'
+    gradient goes straight to the kernel, and no (B, N, R²) map gradient is ever formed
+    (reference optimize.py:403-424 only differentiates maps[top_embedding_indices])."""
+
+    def __init__(self, zs, sizes, B, R):
+        self.zs = list(zs)
+        self.sizes = tuple(int(s) for s in sizes)
+        self.B, self.R = int(B), int(R)
+        with torch.no_grad():
+            self.maps, self.stats = _capture_maps_run([z.detach() for z in self.zs], self.sizes, self.B, self.R)
+        BH, _, N = self.zs[0].shape
+        self.H, self.N = BH // self.B, N
+
+    def select(self, rows):
+        """rows: per image a 1-D int64 tensor of token ids (or None) -> cat_b maps[b, rows[b]]."""
+        if len(rows) != self.B:
+            raise ValueError(f"select: {len(rows)} row lists for {self.B} images")
+        counts = [0 if r is None else int(r.numel()) for r in rows]
+        toks = [r.to(device=self.maps.device, dtype=torch.int64).reshape(-1) for r, c in zip(rows, counts) if c]
+        tok = torch.cat(toks) if toks else torch.empty(0, dtype=torch.int64, device=self.maps.device)
+        return _SelectMaps.apply(self, tok, tuple(counts), *self.zs)
+
+
+def _capture_maps_run(zs, sizes, B, R):
+    """skp_capture_maps_fwd: (maps (B, N, R, R), per-layer stats (B·H, R², 2))."""
+    zs = [_c16(z) for z in zs]
+    BH, _, N = zs[0].shape
+    H = BH // B
+    L = len(zs)
+    dev = zs[0].device
+    RR = R * R
+    stats = [torch.empty(BH, RR, 2, device=dev, dtype=F32) for _ in range(L)]
+    out = torch.empty(B, N, R, R, device=dev, dtype=F32)
+    zp = (ctypes.c_void_p * L)(*[z.data_ptr() for z in zs])
+    sp = (ctypes.c_int * L)(*[int(s) for s in sizes])
+    stp = (ctypes.c_void_p * L)(*[st.data_ptr() for st in stats])
+    with _timed("skp_capture_maps_fwd", capture_maps_bytes(B, H, N, R, sizes), capture_maps_flops(B, H, N, R, sizes)):
+        call("skp_capture_maps_fwd", ctypes.cast(zp, ctypes.POINTER(ctypes.c_void_p)), sp, L, B, H, N, R,
+             ptr(out), ctypes.cast(stp, ctypes.POINTER(ctypes.c_void_p)), stream(dev))
+    return out, stats
+
+
+def capture_maps_bwd_sel(zs, sizes, B, R, tok_table, gsel, gscale, stats):
+    """dz_low of every layer for a sparse per-image map gradient: image b's gradient is
+    gsel[b, k] (R²) at token tok_table[b, k] (−1 = unused), zero elsewhere (skp_capture_maps_bwd_sel)."""
+    zs = [_c16(z) for z in zs]
+    BH, _, N = zs[0].shape
+    H = BH // B
+    L = len(zs)
+    K = tok_table.shape[1]
+    dev = zs[0].device
+    sp = (ctypes.c_int * L)(*[int(s) for s in sizes])
+    nws = _lib.lib().skp_capture_maps_bwd_sel_workspace(sp, L, B, H, N, R, K)
+    if nws < 0:
+        raise ValueError(f"capture_maps_bwd_sel: bad shape B={B} H={H} N={N} R={R} K={K} sizes={sizes}")
+    ws = torch.empty(int(nws), device=dev, dtype=F32)
+    dzs = [torch.empty_like(z) for z in zs]
+    arr = lambda ts: ctypes.cast((ctypes.c_void_p * L)(*[t.data_ptr() for t in ts]),   # noqa: E731
+                                 ctypes.POINTER(ctypes.c_void_p))
+    tok_table = tok_table.to(device=dev, dtype=torch.int64).contiguous()
+    gsel = _c(gsel)
+    with _timed("skp_capture_maps_bwd_sel", capture_maps_sel_bwd_bytes(B, H, N, R, sizes, K),
+                capture_maps_sel_bwd_flops(B, H, N, R, sizes)):
+        call("skp_capture_maps_bwd_sel", arr(zs), sp, L, B, H, N, R, ptr(tok_table), K, ptr(gsel), float(gscale),
+             arr(stats), arr(dzs), ptr(ws), stream(dev))
+    return dzs
+
+
+class _SelectMaps(torch.autograd.Function):
+    """cat_b maps[b, rows_b] with the sparse capture backward (see CapturedMaps.select)."""
+
+    @staticmethod
+    def forward(ctx, cm, tok, counts, *zs):
+        B, N, R = cm.B, cm.N, cm.R
+        img = torch.cat([torch.full((c,), b, dtype=torch.int64, device=tok.device) for b, c in enumerate(counts) if c]) \
+            if tok.numel() else tok
+        out = cm.maps.view(B * N, R * R)[img * N + tok].view(-1, R, R)
+        ctx.cm, ctx.counts = cm, counts
+        ctx.save_for_backward(tok)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        cm, counts = ctx.cm, ctx.counts
+        (tok,) = ctx.saved_tensors
+        B, N, R, L = cm.B, cm.N, cm.R, len(cm.zs)
+        RR = R * R
+        K = max(max(counts), 1)
+        g = _c(g).view(-1, RR)
+        scale = 1.0 / float(L * cm.H)
+        if SEL_BWD and N % 4 == 0:
+            # (B, K) token table (−1 pads) and the (B, K, R²) gradient rows, in row order per image
+            tt = torch.full((B, K), -1, dtype=torch.int64, device=g.device)
+            gs = torch.zeros(B, K, RR, dtype=F32, device=g.device)
+            off = 0
+            for b, c in enumerate(counts):
+                if c:
+                    tt[b, :c] = tok[off:off + c]
+                    gs[b, :c] = g[off:off + c]
+                    off += c
+            dzs = capture_maps_bwd_sel(cm.zs, cm.sizes, B, R, tt, gs, scale, cm.stats)
+        else:
+            dense = torch.zeros(B * N, RR, dtype=F32, device=g.device)
+            img = torch.cat([torch.full((c,), b, dtype=torch.int64, device=g.device) for b, c in enumerate(counts) if c])
+            dense.index_add_(0, img * N + tok, g)
+            dzs = CaptureMaps._dense_bwd([_c(z) for z in cm.zs], cm.stats, (B, cm.H, R, N, list(cm.sizes)),
+                                         dense.view(B, N, R, R))
+        return (None, None, None) + tuple(dzs)
 
 
 class _Resize(torch.autograd.Function):

@@ -134,6 +134,7 @@ class TokenOptimizer:
             import torch.distributed as dist
             with torch.no_grad():
                 dist.broadcast(self.context, src=0)
+            self.sync_cpu_rng()
         self._prefetched = []      # FIFO of (key, thetas, latents, event) from prefetch()
         self._side = None
         self.reset_running()
@@ -168,11 +169,26 @@ class TokenOptimizer:
         ``num_gpus`` images (optimize.py:386), so its CPU generator yields, per micro-iteration,
         one theta per replica in replica order; replica r uses theta r (optimize.py:420-424).
         Every rank draws the whole sequence (k·world thetas, same CPU seed on every rank) and keeps
-        its own column, so the run is the same augmentation stream at any world size."""
+        its own column, so the run is the same augmentation stream at any world size.  The ranks'
+        CPU generators agree because ``sync_cpu_rng`` copies rank 0's into every rank when the
+        optimiser is built."""
         if self.world == 1:
             return self.transform.draw_theta(k)
         th = self.transform.draw_theta(k * self.world)
         return th.reshape(k, self.world, 2, 3)[:, self.rank].contiguous()
+
+    def sync_cpu_rng(self):
+        """Give every rank rank 0's CPU generator state (world > 1).  The reference is one process
+        with one CPU generator, which draws every replica's warp (optimize.py:386); here each rank
+        draws the whole replica-ordered sequence and keeps its column (``draw_thetas``), which is
+        the reference's stream only if the ranks' generators agree — whatever seeds the caller
+        gave each rank."""
+        import torch.distributed as dist
+        state = torch.get_rng_state()
+        if dist.get_backend() == "nccl":
+            state = state.to(self.context.device)
+        dist.broadcast(state, src=0)
+        torch.set_rng_state(state.cpu())
 
     def _take_prefetched(self, images):
         key = tuple(id(t) for t in images)
@@ -228,16 +244,26 @@ class TokenOptimizer:
             batch = torch.cat(list(images))
             transformed = self.transform(batch, theta=self.draw_thetas(k))   # k thetas, image order
             inputs = torch.cat([batch, transformed])
-        maps = ptp_utils.run_and_find_attn_per_image(
-            self.ldm, inputs, self.context, noise_level=self.kw["noise_level"],
-            device=self.device, layers=self.kw["layers"], controllers=self.controllers, stacked=True)[0]
+        sparse = ops.SEL_BWD
+        got = ptp_utils.run_and_find_attn_per_image(
+            self.ldm, inputs, self.context, noise_level=self.kw["noise_level"], device=self.device,
+            layers=self.kw["layers"], controllers=self.controllers, stacked=True, captured=sparse)[0]
+        maps = got.maps if sparse else got        # (2k, N, R, R); the selection needs no gradient
         th_inv = self.transform.theta_inverse().to(self.device)   # all k warps, one upload
         sel = [self._select(maps[i], maps[k + i]) for i in range(k)]
-        # one gather of every image's selected rows (its backward is one scatter into the
-        # (2k, N, R, R) map gradient instead of 2k full-size zero-fills and adds)
-        img = torch.cat([torch.full_like(idx, i) for i, idx in enumerate(sel)])
-        tok = torch.cat(sel)
-        A, At = maps[img, tok], maps[img + k, tok]
+        if sparse:
+            # every image's selected rows in ONE gather whose backward is the sparse capture backward
+            # (skp_capture_maps_bwd_sel): the rows' gradient goes straight to the kernel, no
+            # (2k, N, R, R) map gradient is formed
+            rows = got.select(sel + sel)
+            n = rows.shape[0] // 2
+            A, At = rows[:n], rows[n:]
+        else:
+            # one gather of every image's selected rows (its backward is one scatter into the
+            # (2k, N, R, R) map gradient instead of 2k full-size zero-fills and adds)
+            img = torch.cat([torch.full_like(idx, i) for i, idx in enumerate(sel)])
+            tok = torch.cat(sel)
+            A, At = maps[img, tok], maps[img + k, tok]
         total, off = 0.0, 0
         for i, idx in enumerate(sel):
             n = idx.numel()

@@ -4,10 +4,11 @@
 ``(ldm, controllers, num_gpus)`` (``optimize_token.py:24-79``), MI355X-style:
 - no ``nn.DataParallel``: one process per GPU; ``controllers`` holds the single
   ``AttentionStore`` of this process's device and ``num_gpus`` is the world size;
-- no network: ``type`` names a local directory of diffusers-0.8.0 UNet/VAE
-  weights (``unet.safetensors``/``vae.safetensors``/``.pt``); any other value
-  (e.g. the reference's hub name) builds the SD-1.5 architecture with seeded
-  random weights, which is what the benchmarks use.
+- no network.  ``type`` is resolved by ``resolve_model``: a local weight directory, a hub
+  name already present in the local Hugging Face cache, or an explicit random-init name
+  (``"random"``, ``"random-xl"``, ``"tiny"``, ``"tiny-xl"``).  Anything else raises
+  ``ModelNotAvailableError``: the reference's default names never silently become random
+  weights.
 """
 import os
 
@@ -15,6 +16,19 @@ import torch
 
 from . import ops, ptp_utils
 from .sd import build_sd15, build_sdxl
+
+# explicit random-init model names -> (SDXL?, tiny config?)
+RANDOM_MODELS = {"random": (False, False), "random-xl": (True, False), "tiny": (False, True),
+                 "tiny-xl": (True, True)}
+
+
+# Hugging Face cache to resolve hub names in (None: huggingface_hub's default, HF_HUB_CACHE / HF_HOME)
+HF_CACHE_DIR = None
+
+
+class ModelNotAvailableError(FileNotFoundError):
+    """``load_ldm`` was given a model it cannot load offline (not a local directory, not in the
+    local Hugging Face cache, not an explicit random-init name)."""
 
 
 def _world():
@@ -24,30 +38,105 @@ def _world():
     return 1
 
 
+def _hub_snapshot(name):
+    """The local snapshot directory of hub repo ``name`` if the Hugging Face cache holds it
+    (``local_files_only``: never touches the network), else None."""
+    if "/" not in name or name.count("/") != 1:
+        return None
+    try:
+        from huggingface_hub import snapshot_download
+    except ImportError:
+        return None
+    try:
+        return snapshot_download(name, local_files_only=True, cache_dir=HF_CACHE_DIR)
+    except Exception:   # LocalEntryNotFoundError, a malformed id, a broken cache: not available
+        return None
+
+
+# diffusers config.json keys that map one-to-one onto this package's SD-1.5 constructors
+_UNET_KEYS = ("in_channels", "out_channels", "block_out_channels", "cross_attention_dim", "attention_head_dim",
+              "norm_num_groups")
+_VAE_KEYS = ("block_out_channels", "latent_channels", "norm_num_groups")
+
+
+def _snapshot_model(path, xl):
+    """(path, is_sdxl, architecture config) of a weight directory.  A diffusers pipeline layout
+    carries ``unet/config.json`` and ``vae/config.json``: the UNet's cross-attention width decides
+    SDXL (2048) vs the SD-1.x family, whose block widths, head count, groups and channels are
+    taken from the files (SDXL keeps the base-1.0 architecture of ``sd.SDXL_CONFIG``)."""
+    import json
+    cfgs = {}
+    for part in ("unet", "vae"):
+        p = os.path.join(path, part, "config.json")
+        if os.path.exists(p):
+            with open(p) as f:
+                cfgs[part] = json.load(f)
+    if "unet" in cfgs:
+        xl = cfgs["unet"].get("cross_attention_dim") == 2048
+    if xl or not cfgs:
+        return path, xl, None
+    arch = {}
+    for part, keys in (("unet", _UNET_KEYS), ("vae", _VAE_KEYS)):
+        if part in cfgs:
+            arch[part] = {k: (tuple(v) if isinstance(v, list) else v) for k, v in cfgs[part].items() if k in keys}
+    return path, xl, arch
+
+
+def resolve_model(type):
+    """(weights directory or None, is_sdxl, architecture config or None) for ``load_ldm``'s ``type``.
+
+    - a local directory: its weights (``unet.safetensors`` / ``.pt`` / ``.bin`` or the diffusers
+      pipeline layout ``unet/diffusion_pytorch_model.*``; see ``sd.build_sd15``);
+    - a hub name (``"runwayml/stable-diffusion-v1-5"``): its snapshot in the local Hugging Face
+      cache, if present;
+    - ``"random"`` / ``"random-xl"``: SD-1.5 / SDXL with seeded random weights (benchmarks);
+      ``"tiny"`` / ``"tiny-xl"``: the toy-width models of the tests;
+    - otherwise ``ModelNotAvailableError``.
+    SDXL is chosen by a name containing "xl" (``stabilityai/stable-diffusion-xl-base-1.0``).
+    """
+    if not isinstance(type, (str, os.PathLike)):
+        raise TypeError(f"load_ldm: model type must be a string or path, got {type!r}")
+    type = os.fspath(type)
+    if type in RANDOM_MODELS:
+        xl, tiny = RANDOM_MODELS[type]
+        cfg = None
+        if tiny:
+            from .sd import TINY_CONFIG, TINY_SDXL_CONFIG
+            cfg = TINY_SDXL_CONFIG if xl else TINY_CONFIG
+        return None, xl, cfg
+    xl = "xl" in os.path.basename(type.rstrip("/")).lower()
+    path = os.path.expanduser(type)
+    snap = path if os.path.isdir(path) else _hub_snapshot(type)
+    if snap is not None:
+        return _snapshot_model(snap, xl)
+    raise ModelNotAvailableError(
+        f"load_ldm: cannot load model {type!r}: it is not a local directory and not in the local Hugging Face "
+        "cache, and this build never downloads. Pass a directory of diffusers-0.8.0 UNet/VAE weights, or "
+        "type='random' (SD-1.5) / 'random-xl' (SDXL) for seeded random weights.")
+
+
 def load_ldm(device, type="CompVis/stable-diffusion-v1-4", feature_upsample_res=256, seed=0, config=None,
              early_exit=True):
     """optimize_token.py:24-79.
 
-    ``early_exit`` lets the patched attention stop the UNet forward after the 4th
+    ``type``: see ``resolve_model`` (raises ``ModelNotAvailableError`` for a model it cannot load;
+    the reference would download it).  ``config`` overrides the architecture of a random-init
+    model (tests).  ``early_exit`` lets the patched attention stop the UNet forward after the 4th
     capture (the reference discards that output; DESIGN.md §UNet early exit).
     """
-    weights = type if (isinstance(type, str) and os.path.isdir(type)) else None
-    xl = isinstance(type, str) and ("xl" in type.lower())   # SDXL (SURVEY §8 A16, config 5)
-    if type == "tiny" and config is None:   # toy-width SD-1.5 (tests, CLI smoke runs)
-        from .sd import TINY_CONFIG
-        config = TINY_CONFIG
-    if type == "tiny-xl" and config is None:
-        from .sd import TINY_SDXL_CONFIG
-        config = TINY_SDXL_CONFIG
-    if weights is None and str(device) != "cpu":
-        pass  # hub names cannot be fetched offline: random-init SD-1.5 (seeded) instead
-    ldm = (build_sdxl if xl else build_sd15)(seed=seed, device=device, weights=weights, config=config)
+    weights, xl, cfg = resolve_model(type)
+    if config is not None:
+        if weights is not None:
+            raise ValueError("load_ldm: `config` only applies to random-init models, not to loaded weights")
+        cfg = config
+    ldm = (build_sdxl if xl else build_sd15)(seed=seed, device=device, weights=weights, config=cfg)
+    ldm.model_type = type
     dev = torch.device(device)
-    if dev.type == "cuda":
-        from .tuning import use_tuned_gemms
-        use_tuned_gemms()   # measured hipBLASLt / rocBLAS choices for the UNet/VAE GEMM shapes
     if dev.type == "cuda" and dev.index is None:
         dev = torch.device("cuda", torch.cuda.current_device())
+    if dev.type == "cuda":
+        from .tuning import use_tuned_gemms
+        use_tuned_gemms(dev)   # measured hipBLASLt / rocBLAS choices for the UNet/VAE GEMM shapes
     controllers = {dev: ptp_utils.AttentionStore(early_exit=early_exit)}
     ptp_utils.register_attention_control(ldm.unet, controllers[dev], feature_upsample_res=feature_upsample_res)
 

@@ -103,11 +103,15 @@ class LogitStore(AttentionStore):
         self.heads = dict.get("heads", getattr(self, "heads", 8))
         return dict
 
-    def maps_per_image(self, B, R, layers=(0, 1, 2, 3)):
+    def maps_per_image(self, B, R, layers=(0, 1, 2, 3), captured=False):
+        """(B, N, R, R) maps (CaptureMaps, dense backward), or with ``captured`` an
+        ``ops.CapturedMaps`` whose ``select`` gathers rows with the sparse backward."""
         zs = [z for li, z in enumerate(self.step_store["attn"]) if li in layers]
         ss = [sz for li, sz in enumerate(self.step_store["size"]) if li in layers]
         if not zs:
             raise RuntimeError("LogitStore: no captured layers (is the hook registered?)")
+        if captured:
+            return ops.CapturedMaps(zs, ss, B, R)
         return ops.capture_maps(zs, ss, B, R)
 
 
@@ -255,7 +259,7 @@ def run_and_find_attn(ldm, image, context, noise_level=-1, device="cuda",
 
 
 def run_and_find_attn_per_image(ldm, images, context, noise_level=-1, device="cuda", layers=(0, 1, 2, 3),
-                                upsample_res=-1, indices=None, controllers=None, stacked=False):
+                                upsample_res=-1, indices=None, controllers=None, stacked=False, captured=False):
     """Batched capture: ONE VAE + UNet pass over B images, maps aggregated PER IMAGE.
 
     Equivalent to B calls of ``run_and_find_attn`` with one image each (every UNet/VAE op is
@@ -272,6 +276,10 @@ def run_and_find_attn_per_image(ldm, images, context, noise_level=-1, device="cu
     for key in controllers:
         ctl = controllers[key]
         if getattr(ctl, "stores_logits", False):
+            if captured:
+                out.append(ctl.maps_per_image(B, ldm.feature_upsample_res, layers, captured=True))
+                ctl.reset()
+                continue
             maps = ctl.maps_per_image(B, ldm.feature_upsample_res, layers)
             if stacked and indices is None and upsample_res in (-1, maps.shape[-1]):
                 out.append(maps)

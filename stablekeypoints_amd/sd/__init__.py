@@ -42,7 +42,8 @@ def build_sd15(seed=0, device="cpu", weights=None, config=None, unet_cls=None):
     """Random-init SD-1.5 parts (seeded), or load a local diffusers-0.8.0 state dict.
 
     ``weights`` may be a directory holding ``unet.safetensors``/``vae.safetensors`` or
-    ``.pt`` files (loaded with ``weights_only=True``).  ``config`` shrinks the
+    ``.pt`` files (loaded with ``weights_only=True``), or a diffusers pipeline directory
+    (``unet/diffusion_pytorch_model.safetensors`` …); missing files raise.  ``config`` shrinks the
     architecture (``TINY_CONFIG`` keeps SD-1.5's block structure at toy widths for
     golden vectors and CPU tests).
     """
@@ -56,18 +57,21 @@ def build_sd15(seed=0, device="cpu", weights=None, config=None, unet_cls=None):
         vae = AutoencoderKL(**cfg.get("vae", {}))
     if weights:
         for name, mod in (("unet", unet), ("vae", vae)):
-            for ext in (".safetensors", ".pt", ".bin"):
-                p = os.path.join(weights, name + ext)
-                if os.path.exists(p):
-                    if ext == ".safetensors":
-                        from safetensors.torch import load_file
-                        sd = load_file(p)
-                    else:
-                        sd = torch.load(p, map_location="cpu", weights_only=True)
-                    if name == "vae":
-                        sd = {k: v for k, v in sd.items() if k.startswith(("encoder.", "quant_conv."))}
-                    mod.load_state_dict(sd, strict=True)
-                    break
+            cands = [os.path.join(weights, name + ext) for ext in (".safetensors", ".pt", ".bin")]
+            # the diffusers pipeline layout (a Hugging Face snapshot): <name>/diffusion_pytorch_model.*
+            cands += [os.path.join(weights, name, "diffusion_pytorch_model" + ext) for ext in (".safetensors", ".bin")]
+            found = [p for p in cands if os.path.exists(p)]
+            if not found:
+                raise FileNotFoundError(f"no {name} weights in {weights} (looked for {', '.join(cands)})")
+            p = found[0]
+            if p.endswith(".safetensors"):
+                from safetensors.torch import load_file
+                sd = load_file(p)
+            else:
+                sd = torch.load(p, map_location="cpu", weights_only=True)
+            if name == "vae":
+                sd = {k: v for k, v in sd.items() if k.startswith(("encoder.", "quant_conv."))}
+            mod.load_state_dict(sd, strict=True)
     sched = DDIMScheduler(beta_start=0.00085, beta_end=0.012, beta_schedule="scaled_linear",
                           clip_sample=False, set_alpha_to_one=False)
     sched.set_timesteps(50)

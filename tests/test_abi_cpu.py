@@ -75,3 +75,31 @@ def test_vae_downsample_edge_pad_equals_f_pad():
     ref = m.conv(F.pad(x, (0, 1, 0, 1)))
     ref.sum().backward()
     assert torch.equal(y, ref) and torch.equal(g, x.grad)
+
+
+def test_sparse_capture_backward_workspace_and_arguments():
+    """skp_capture_maps_bwd_sel: the workspace query sizes both paths and refuses bad shapes;
+    the entry point rejects bad arguments before any launch (no GPU needed)."""
+    from stablekeypoints_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libskp.so not built")
+    L = _lib.lib()
+    sizes = (ctypes.c_int * 4)(16, 16, 16, 32)
+    fast = L.skp_capture_maps_bwd_sel_workspace(sizes, 4, 8, 8, 500, 128, 10)
+    # zsel + E (one layer) + pix (all layers) + es (all layers), floats
+    BH, RR = 64, 128 * 128
+    assert fast >= BH * 32 * 32 * 10 + BH * 10 * RR + 4 * BH * RR * 2 + 4 * BH * 10 * 32 * 32
+    odd = (ctypes.c_int * 2)(5, 3)
+    slow = L.skp_capture_maps_bwd_sel_workspace(odd, 2, 2, 3, 36, 40, 4)   # no compiled kernel: dense fallback
+    assert slow >= 2 * 36 * 40 * 40 * 2
+    assert L.skp_capture_maps_bwd_sel_workspace(sizes, 0, 8, 8, 500, 128, 10) == -1
+    assert L.skp_capture_maps_bwd_sel_workspace(sizes, 4, 8, 8, 500, 128, 0) == -1
+    p = ctypes.c_void_p(256)
+    arr = (ctypes.c_void_p * 4)(256, 256, 256, 256)
+    parr = ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p))
+    rc = L.skp_capture_maps_bwd_sel(parr, sizes, 4, 8, 8, 500, 128, p, 33, p, 1.0, parr, parr, p, None)
+    assert rc == -1 and b"K must be" in L.skp_last_error()
+    rc = L.skp_capture_maps_bwd_sel(parr, sizes, 4, 8, 8, 502, 128, p, 10, p, 1.0, parr, parr, p, None)
+    assert rc == -1 and b"multiple of 4" in L.skp_last_error()
+    rc = L.skp_capture_maps_bwd_sel(parr, sizes, 4, 8, 8, 500, 128, p, 10, p, 1.0, None, parr, p, None)
+    assert rc == -1 and b"null" in L.skp_last_error()

@@ -1,0 +1,140 @@
+"""Sparse capture backward skp_capture_maps_bwd_sel vs the oracle's dense
+backward of the scattered gradient (oracle.capture_maps_bwd_sel: optimize.py:403-424 losses on the
+selected rows → collect_maps' mean, optimize.py:27-79 → softmax + bicubic adjoint,
+ptp_utils.py:513-536).  Tolerance: relative 1e-4 of the gradient's max (north_star: 1e-4 fp32)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+import recipes
+from oracle import skp_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def T(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def N(t):
+    return t.detach().cpu().numpy()
+
+
+def _fwd(zs, sizes, B, H, R):
+    from stablekeypoints_amd import ops
+    maps, stats = ops._capture_maps_run(zs, sizes, B, R)
+    torch.cuda.synchronize()
+    return maps, stats
+
+
+def _sel_abi(zs, sizes, B, H, R, tok, gsel, gscale, stats, ws_fill=float("nan")):
+    from stablekeypoints_amd._lib import call, lib, ptr, stream
+    L = len(zs)
+    Nn = zs[0].shape[-1]
+    K = tok.shape[1]
+    sp = (ctypes.c_int * L)(*sizes)
+    nws = lib().skp_capture_maps_bwd_sel_workspace(sp, L, B, H, Nn, R, K)
+    assert nws > 0
+    ws = torch.full((nws,), ws_fill, device=DEV)
+    dzs = [torch.full_like(z, float("nan")) for z in zs]
+    arr = lambda ts: ctypes.cast((ctypes.c_void_p * L)(*[t.data_ptr() for t in ts]), ctypes.POINTER(ctypes.c_void_p))
+    call("skp_capture_maps_bwd_sel", arr(zs), sp, L, B, H, Nn, R, ptr(tok), K, ptr(gsel), float(gscale), arr(stats),
+         arr(dzs), ptr(ws), stream(DEV))
+    torch.cuda.synchronize()
+    return dzs
+
+
+def _case(seed, B, H, sizes, R, Nn, K, dup=False, ragged=False):
+    rng = np.random.default_rng(seed)
+    zs = [recipes.random_logits(seed + 3 * i, (B * H, s * s, Nn), scale=2.0) for i, s in enumerate(sizes)]
+    tok = np.stack([rng.choice(Nn, size=K, replace=False) for _ in range(B)]).astype(np.int64)
+    if dup:
+        tok[:, -1] = tok[:, 0]                  # a repeated token: its two gradient rows add
+    if ragged:
+        tok[0, K // 2:] = -1                    # fewer rows for image 0 (FPS ran out of candidates)
+        if B > 1:
+            tok[-1, :] = -1                     # an image with no selected row
+    gsel = rng.standard_normal((B, K, R, R)).astype(np.float32)
+    gsel[tok < 0] = 0.0
+    return zs, tok, gsel
+
+
+@pytest.mark.parametrize("B,H,sizes,R,Nn,K,dup,ragged", [
+    (2, 8, (8, 8, 8, 16), 64, 40, 6, False, False),       # fast path, R = 8·s and 4·s
+    (2, 4, (4, 8), 32, 64, 5, True, False),               # fast path at R = 32, a duplicated token
+    (3, 2, (16, 32), 128, 36, 4, False, True),            # fast path at the bench's R, ragged rows
+    (1, 2, (8,), 128, 132, 3, False, False),              # R = 16·s, N past one 128-token chunk
+    (2, 3, (5, 3), 40, 36, 4, True, True),                # no compiled kernel: dense fallback
+    (1, 2, (16,), 32, 20, 2, False, False),               # R = 2·s: dense fallback
+])
+def test_capture_maps_bwd_sel_vs_oracle(B, H, sizes, R, Nn, K, dup, ragged):
+    zs, tok, gsel = _case(500 + Nn + R, B, H, sizes, R, Nn, K, dup, ragged)
+    zt = [T(z) for z in zs]
+    _, stats = _fwd(zt, list(sizes), B, H, R)
+    L = len(sizes)
+    gscale = 1.0 / (L * H)
+    dzs = _sel_abi(zt, list(sizes), B, H, R, T(tok), T(gsel), gscale, stats)
+    ref = O.capture_maps_bwd_sel(zs, sizes, B, H, R, tok, gsel, gscale)
+    for i in range(L):
+        got = N(dzs[i])
+        assert np.isfinite(got).all()
+        err = np.abs(got - ref[i]).max() / max(1e-6, np.abs(ref[i]).max())
+        assert err < 1e-4, (i, err)
+
+
+def test_capture_maps_bwd_sel_full_size_vs_oracle_and_dense_kernel():
+    """Bench shape (B = 8 images × 8 heads, s = 16, 16, 16, 32, R = 128, N = 500, K = 10 selected
+    rows per image): the sparse backward vs (a) the oracle's dense backward of the scattered
+    gradient for the heads of images 0 and 7, (b) the dense skp_capture_maps_bwd on the whole
+    scattered gradient; and bitwise deterministic across two runs."""
+    from stablekeypoints_amd import ops
+    B, H, R, Nn, K, sizes = 8, 8, 128, 500, 10, (16, 16, 16, 32)
+    g = torch.Generator().manual_seed(21)
+    zs = [(torch.randn(B * H, s * s, Nn, generator=g) * 3).to(DEV) for s in sizes]
+    tok = torch.stack([torch.randperm(Nn, generator=g)[:K] for _ in range(B)]).to(DEV)
+    gsel = torch.randn(B, K, R, R, generator=g).to(DEV)
+    _, stats = _fwd(zs, list(sizes), B, H, R)
+    gscale = 1.0 / 32
+    d1 = _sel_abi(zs, list(sizes), B, H, R, tok, gsel, gscale, stats)
+    d2 = _sel_abi(zs, list(sizes), B, H, R, tok, gsel, gscale, stats, ws_fill=0.0)
+    dense = torch.zeros(B, Nn, R * R, device=DEV)
+    for b in range(B):
+        dense[b].index_add_(0, tok[b], gsel[b].reshape(K, R * R))
+    ref_k = ops.CaptureMaps._dense_bwd(zs, stats, (B, H, R, Nn, list(sizes)), dense.view(B, Nn, R, R))
+    heads = list(range(H)) + list(range(7 * H, 8 * H))
+    ref_o = O.capture_maps_bwd_sel([N(z) for z in zs], sizes, B, H, R, N(tok), N(gsel), gscale, heads=heads)
+    for i, s in enumerate(sizes):
+        assert torch.equal(d1[i], d2[i]), f"layer {i}: not deterministic"
+        scale = ref_k[i].abs().max().item()
+        ek = (d1[i] - ref_k[i]).abs().max().item() / scale
+        eo = np.abs(N(d1[i][heads]) - ref_o[i]).max() / np.abs(ref_o[i]).max()
+        print(f"\ns={s}: sel vs dense kernel rel-max {ek:.2e}, vs oracle (16 heads) {eo:.2e}")
+        assert ek < 2e-5 and eo < 1e-4, (i, ek, eo)
+
+
+def test_select_autograd_equals_dense_gather():
+    """CapturedMaps.select (the token-opt path: one differentiable gather of every image's selected
+    rows, sparse backward) gives the same dz_low as indexing CaptureMaps' output (dense backward)."""
+    from stablekeypoints_amd import ops
+    B, H, R, Nn, sizes = 4, 8, 64, 60, (8, 8, 8, 16)
+    zs = [recipes.random_logits(700 + i, (B * H, s * s, Nn), scale=2.0) for i, s in enumerate(sizes)]
+    rows = [torch.tensor(r, device=DEV) for r in ([3, 7, 11], [0, 59], [5, 5, 9, 1], [])]
+    w = torch.from_numpy(recipes.random_logits(71, (9, R, R))).to(DEV)
+    za = [T(z).requires_grad_(True) for z in zs]
+    cm = ops.CapturedMaps(za, sizes, B, R)
+    out = cm.select(rows)
+    (out * w).sum().backward()
+    zb = [T(z).requires_grad_(True) for z in zs]
+    maps = ops.capture_maps(zb, sizes, B, R)
+    assert torch.equal(maps.detach(), cm.maps)
+    img = torch.tensor([0, 0, 0, 1, 1, 2, 2, 2, 2], device=DEV)
+    tk = torch.cat([r for r in rows if r.numel()])
+    ref = maps[img, tk]
+    assert torch.equal(ref.detach(), out.detach())
+    (ref * w).sum().backward()
+    for a, b in zip(za, zb):
+        err = (a.grad - b.grad).abs().max().item() / b.grad.abs().max().item()
+        assert err < 2e-5, err
