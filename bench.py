@@ -246,6 +246,114 @@ def _tuned_gemms_in_use():
     return bool(_state["loaded"])
 
 
+# ------------------------------------------------------------------------------ eval-stage benches
+FIND_INDICES_T4_ITS = 1.34   # find_best_indices, N=100, upsample 256, 1 image per it, Colab T4
+
+
+def stage_main(args, ldm, controllers, context, dev, world, rank, backend):
+    """--stage find_indices / tta: the no-grad evaluation stages on the fused capture.
+
+    find_indices (keypoint_regressor.find_best_indices, reference keypoint_regressor.py:16-121 with
+    main.py:248-267's arguments: upsample_res 256, gaussian top-k 25, σ 2, FPS 10, layers 0-3): one
+    step = ``--stage-images`` images per rank, captured in ONE batched VAE/UNet pass, then per image
+    top-k + FPS; it/s = images/s (the reference's tqdm "it" is one image at num_gpus = 1).
+    tta (keypoint_regressor.precompute_all_keypoints, reference :124-224 with main.py:302-320's
+    arguments: 10 augmentations, upscale 512, argmax): one step = ``--stage-images`` images per
+    rank, each image's 10 warped copies in one batched pass (with N ranks, each runs 10 // N of every
+    image's augmentations, as the reference's replicas do); it/s = images/s.
+    Every rank draws the same loader order (one CPU seed) and takes replica ``rank`` of each group,
+    as in the reference's DataParallel replicas; value = images of all ranks ÷ max-over-ranks time."""
+    from stablekeypoints_amd import keypoint_regressor as kr, ops
+    from stablekeypoints_amd.datasets import SyntheticDataset
+    n = args.stage_images
+    timer = KernelTimer(["skp_capture_maps_fwd", "skp_aggregate", "skp_capture_fwd"])
+    ops.set_kernel_timer(timer)
+    if args.stage == "find_indices":
+        data = SyntheticDataset(n=n * world, size=args.res, seed=7)
+
+        def step():
+            return kr.find_best_indices(ldm, context, num_steps=n * world, device=dev, upsample_res=256,
+                                        layers=(0, 1, 2, 3), top_k=10, furthest_point_num_samples=25,
+                                        controllers=controllers, num_gpus=world, top_k_strategy="gaussian",
+                                        sigma=2.0, dataset=data, capture_batch=n)
+    else:
+        data = SyntheticDataset(n=n, size=args.res, seed=7)
+        top = torch.arange(10)
+
+        def step():
+            return kr.precompute_all_keypoints(ldm, context, top, device=dev, layers=(0, 1, 2, 3),
+                                               augmentation_iterations=10, controllers=controllers,
+                                               num_gpus=world, dataset=data, upscale_size=512)
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+    torch.manual_seed(1234)   # same CPU stream on every rank: loader order and thetas agree
+    for _ in range(args.warmup):
+        out = step()
+    barrier()
+    torch.cuda.synchronize()
+    timer.enabled = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    timer.enabled = False
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    # find_indices shards the images over the ranks (weak); tta splits each image's augmentations
+    # over the ranks (the reference's augmentation_iterations // num_gpus per replica: strong)
+    images = (world * n if args.stage == "find_indices" else n) * args.steps
+    value = images / elapsed
+    roof = None
+    fw = timer.summary("skp_capture_maps_fwd")
+    if fw:
+        t = fw["avg_ms"] * 1e-3
+        flops = fw["flop_per_launch"]
+        roof = {"kernel": "skp_capture_maps_fwd", "bound": "valu", "achieved": flops / t / 1e12,
+                "peak": VALU_F32_PEAK / 1e12, "unit": "TFLOP/s", "frac": flops / t / VALU_F32_PEAK, "traffic": None,
+                "avg_launch_ms": fw["avg_ms"], "launches": fw["launches"],
+                "timing_source": "HIP events around every launch in the timed region (bench.py KernelTimer)",
+                "algorithmic_flop_per_launch": flops, "algorithmic_bytes_per_launch": fw["bytes_per_launch"],
+                "hbm_achieved_GBps": fw["bytes_per_launch"] / t / 1e9,
+                "flop_model": "15 FLOP per (image, head, layer, pixel, token) + 8 per (row, low-res column, token); "
+                              "ops.capture_maps_flops"}
+    if rank == 0:
+        if args.stage == "find_indices":
+            metric = f"it/s (find_best_indices, {args.res}², N={args.tokens} tokens, 1 image per it)"
+            workload = (f"keypoint_regressor.find_best_indices: SD-1.5 fp32, {args.res}², N={args.tokens}, "
+                        f"feature_upsample_res={args.upsample_res}, upsample_res 256, gaussian top-25 (σ 2) -> FPS 10, "
+                        f"{n} images per rank per batched capture pass")
+            vs = value / FIND_INDICES_T4_ITS if args.tokens == 100 and args.res == 512 else None
+        else:
+            metric = f"it/s (precompute_all_keypoints, {args.res}², 10 augmentations, 1 image per it)"
+            workload = (f"keypoint_regressor.precompute_all_keypoints: SD-1.5 fp32, {args.res}², N={args.tokens}, "
+                        f"feature_upsample_res={args.upsample_res}, 10 tokens, 10 augmentations per image in one "
+                        "batched capture pass, upscale 512, argmax")
+            vs = None
+        line = {"metric": metric, "value": value, "unit": "it/s", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+                "scaling": "weak" if args.stage == "find_indices" else "strong", "vs_baseline": vs,
+                "vs_baseline_source": ("BASELINE.md: 1.34 it/s, Colab T4, StableKeypoints.ipynb:2724" if vs else None),
+                "dtype": "f32", "data": f"synthetic (seeded torch.rand {args.res}² images, random-init SD15)",
+                "config": {"workload": workload, "stage": args.stage, "images_per_step": images // args.steps,
+                           "tokens": args.tokens, "image_res": args.res,
+                           "parallelism": (f"dp{world} (replicas; {'RCCL' if backend == 'nccl' else backend} "
+                                           "all_gather / all-reduce at the end)" if world > 1 else "dp1"),
+                           "tuned_gemms": _tuned_gemms_in_use()},
+                "roofline": roof, "cpu_baseline": None}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -270,6 +378,12 @@ def main():
                          "steady state: every timed step runs one UNet pass and one VAE pass, the warm-up's "
                          "prefetch is balanced by the last timed step's")
     ap.add_argument("--gc-freeze", type=int, default=1, help="gc.freeze() after the model is built (host overhead)")
+    ap.add_argument("--stage", default="token_opt", choices=["token_opt", "find_indices", "tta"],
+                    help="token_opt = the headline token-optimisation step; find_indices = "
+                         "keypoint_regressor.find_best_indices (no-grad capture at upsample 256, gaussian top-25 -> "
+                         "FPS 10), one step = --stage-images images per rank in one batched pass; tta = "
+                         "precompute_all_keypoints (10 augmentations at 512, argmax), one step = --stage-images images")
+    ap.add_argument("--stage-images", type=int, default=8, help="images per rank per step of a --stage bench")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
                     help="JSON with PMC-derived HBM bytes per launch of the roofline kernel")
     args = ap.parse_args()
@@ -314,6 +428,8 @@ def main():
         gc.freeze()   # the model's ~10^5 long-lived objects leave the cyclic collector's scans
     torch.manual_seed(0)
     context = torch.randn(1, args.tokens, ldm.unet.cross_attention_dim).to(dev)
+    if args.stage != "token_opt":
+        return stage_main(args, ldm, controllers, context.detach(), dev, world, rank, backend)
     torch.manual_seed(1234 + rank)
     opt = TokenOptimizer(ldm, controllers, context, accum=args.accum, device=dev)
     data = SyntheticDataset(n=16, size=args.res, seed=rank)

@@ -40,7 +40,8 @@ def run_image_with_context_augmented(ldm, image, context, indices, device="cuda"
                                      from_where=("down_cross", "mid_cross", "up_cross"), layers=(0, 1, 2, 3, 4, 5),
                                      augmentation_iterations=20, noise_level=-1, augment_degrees=30,
                                      augment_scale=(0.9, 1.1), augment_translate=(0.1, 0.1), visualize=False,
-                                     controllers=None, num_gpus=1, save_folder="outputs", upscale_size=512):
+                                     controllers=None, num_gpus=1, save_folder="outputs", upscale_size=512,
+                                     augmentation_batch=None):
     """eval.py:197-355 (hot part 221-266, 327-330): TTA-averaged maps of the chosen tokens.
 
     ``image`` is (3, H, W) in [0, 1] (torch or numpy HWC).  Each of the
@@ -49,10 +50,20 @@ def run_image_with_context_augmented(ldm, image, context, indices, device="cuda"
     copy is captured (``indices`` gathered, bilinear to ``upscale_size``: collect_maps), then its
     map and a ones map are inverse-warped and summed.  Returns Σmaps / Σones with NaN → 0.
 
+    ``augmentation_batch`` (extra; None = all of this rank's iterations): how many iterations'
+    warped copies go through ONE batched VAE/UNet capture pass.  Every copy is captured on its
+    own (per-image maps, ``run_and_find_attn_per_image``), the thetas are drawn iteration by
+    iteration exactly as the reference draws them, and the copies' contributions are summed in
+    iteration order, so this is the reference's loop up to fp32 summation order and the GPU
+    noise draw (one ``randn_like`` per batch instead of per copy; the reference's CUDA noise is
+    not reproducible on another device anyway).  At batch 1 a 64² latent UNet pass cannot fill
+    256 CUs; 10 copies in one pass do.
+
     Replicas: with torch.distributed initialised and ``num_gpus`` equal to the world size,
     rank r runs replica r of every iteration and the two (n, S, S) sums are all-reduced (SUM)
     once at the end; every rank must hold the same CPU RNG state (same seed) so that all draw
-    the same thetas.  In one process, the ``num_gpus`` copies run as one batched capture.
+    the same thetas.  In one process, the ``num_gpus`` copies of an iteration are captured in
+    the same batched pass.
     """
     if visualize:
         raise NotImplementedError("visualisation is outside the hot path")
@@ -68,10 +79,16 @@ def run_image_with_context_augmented(ldm, image, context, indices, device="cuda"
     num_samples = torch.zeros(n, upscale_size, upscale_size, device=device)
     sum_samples = torch.zeros(n, upscale_size, upscale_size, device=device)
     T = RandomAffineWithInverse(degrees=augment_degrees, scale=augment_scale, translate=augment_translate)
-    for _ in range(augmentation_iterations // num_gpus):
-        theta = T.draw_theta(num_gpus)                        # every rank draws all replicas' thetas
-        mine = slice(rank, rank + 1) if world > 1 else slice(0, num_gpus)
-        aug = T(img[None].expand(theta[mine].shape[0], -1, -1, -1), theta=theta[mine])
+    iters = augmentation_iterations // num_gpus
+    chunk = iters if augmentation_batch is None else max(1, int(augmentation_batch))
+    done = 0
+    while done < iters:
+        c = min(chunk, iters - done)
+        # every rank draws all replicas' thetas, iteration by iteration (eval.py:238-242)
+        theta = torch.cat([T.draw_theta(num_gpus) for _ in range(c)])
+        if world > 1:
+            theta = theta.reshape(c, num_gpus, 2, 3)[:, rank]
+        aug = T(img[None].expand(theta.shape[0], -1, -1, -1), theta=theta)
         if aug.shape[0] == 1:
             maps = torch.stack(ptp_utils.run_and_find_attn(
                 ldm, aug, context, layers=layers, noise_level=noise_level, from_where=from_where,
@@ -80,9 +97,10 @@ def run_image_with_context_augmented(ldm, image, context, indices, device="cuda"
             per = ptp_utils.run_and_find_attn_per_image(ldm, aug, context, noise_level=noise_level, device=device,
                                                         layers=layers, upsample_res=upscale_size, indices=indices,
                                                         controllers=controllers)
-            maps = torch.stack([m for ctl_maps in per for m in ctl_maps])
+            maps = torch.stack([per[k][b] for b in range(aug.shape[0]) for k in range(len(per))])
         num_samples += T.inverse(torch.ones_like(maps)).sum(dim=0)
         sum_samples += T.inverse(maps).sum(dim=0)
+        done += c
     if world > 1:
         import torch.distributed as dist
         dist.all_reduce(num_samples)

@@ -41,8 +41,15 @@ def find_best_indices(ldm, context, num_steps=100, device="cuda", noise_level=-1
                       layers=(0, 1, 2, 3, 4, 5), from_where=("down_cross", "mid_cross", "up_cross"), num_tokens=1000,
                       top_k=30, dataset_loc="~", dataset_name="celeba_aligned", min_dist=0.05,
                       furthest_point_num_samples=50, controllers=None, num_gpus=1, top_k_strategy="entropy", sigma=3,
-                      validation=False, num_subjects=1, dataset=None):
-    """keypoint_regressor.py:16-121.  ``dataset`` (extra) overrides the dataset_name lookup."""
+                      validation=False, num_subjects=1, dataset=None, capture_batch=8):
+    """keypoint_regressor.py:16-121.  ``dataset`` (extra) overrides the dataset_name lookup.
+
+    ``capture_batch`` (extra): how many of this rank's images go through ONE batched VAE/UNet
+    capture pass (``run_and_find_attn_per_image``: maps per image, exactly what one
+    ``run_and_find_attn`` per image gives, up to the GPU noise draw — one ``randn_like`` per
+    batch).  The images are taken from the loader in the reference's order and their
+    candidates / FPS picks appended in that order, so the ranking is the reference's.  1 = the
+    reference's one pass per image."""
     from .optimize import _world
     if top_k_strategy not in ("entropy", "gaussian", "consistent"):
         raise NotImplementedError(top_k_strategy)
@@ -54,14 +61,24 @@ def find_best_indices(ldm, context, num_steps=100, device="cuda", noise_level=-1
     loader = _loader(dataset, num_gpus)
     state = {"loader": loader, "it": iter(loader)}
     indices_list = []
-    for _ in range(num_steps // num_gpus):
-        images = _next(state)["img"]
-        mine = images[rank:rank + 1] if world > 1 else images
-        for image in mine:   # one replica = one image (the reference's per-device maps)
-            attention_maps = ptp_utils.run_and_find_attn(ldm, image[None].to(device), context, layers=layers,
-                                                         noise_level=noise_level, from_where=from_where,
-                                                         upsample_res=upsample_res, controllers=controllers,
-                                                         device=device)
+    steps = num_steps // num_gpus
+    chunk = max(1, int(capture_batch))
+    done = 0
+    while done < steps:
+        c = min(chunk, steps - done)
+        groups = [_next(state)["img"] for _ in range(c)]
+        # one replica = one image (the reference's per-device maps)
+        mine = torch.cat([g[rank:rank + 1] if world > 1 else g for g in groups]).to(device)
+        if mine.shape[0] == 1:
+            per_image = [ptp_utils.run_and_find_attn(ldm, mine, context, layers=layers, noise_level=noise_level,
+                                                     from_where=from_where, upsample_res=upsample_res,
+                                                     controllers=controllers, device=device)]
+        else:
+            per = ptp_utils.run_and_find_attn_per_image(ldm, mine, context, noise_level=noise_level, device=device,
+                                                        layers=layers, upsample_res=upsample_res,
+                                                        controllers=controllers)
+            per_image = [[per[k][b] for k in range(len(per))] for b in range(mine.shape[0])]
+        for attention_maps in per_image:
             for attention_map in attention_maps:
                 if top_k_strategy == "entropy":
                     cand = ptp_utils.entropy_sort(attention_map, furthest_point_num_samples)
@@ -71,6 +88,7 @@ def find_best_indices(ldm, context, num_steps=100, device="cuda", noise_level=-1
                 else:
                     cand = torch.arange(furthest_point_num_samples, device=attention_map.device)
                 indices_list.append(ptp_utils.furthest_point_sampling(attention_map, top_k, cand).cpu())
+        done += c
     indices_list = torch.cat(indices_list)
     if world > 1:
         import torch.distributed as dist

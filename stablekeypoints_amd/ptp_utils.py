@@ -14,6 +14,8 @@ softmax·V path, and hands them to ``skp_capture_fwd`` for the R×R capture:
 an HBM-bound upsample/softmax kernel.
 """
 import abc
+import contextlib
+import os
 
 import numpy as np
 import torch
@@ -62,9 +64,16 @@ class AttentionStore(AttentionControl):
     attention raises ``CaptureComplete`` once the 4th map is stored, so the UNet
     forward stops there; the reference discards that forward's output anyway
     (``ptp_utils.py:246-252``) and nothing later feeds the loss.
+
+    ``stores_logits`` (class default False): when set, the hook hands the store each captured
+    layer's low-resolution logits (B·H, s², N) with their grid side instead of the (B·H, R², N)
+    attention; ``maps_per_image`` then builds maps with the fused capture.  ``LogitStore`` sets
+    it for good; ``logit_capture`` sets it on an ``AttentionStore`` for one capture pass whose
+    maps the caller collects at once (``run_and_find_attn``).
     """
 
     max_captures = 4
+    stores_logits = False
 
     @staticmethod
     def get_empty_store():
@@ -72,6 +81,9 @@ class AttentionStore(AttentionControl):
 
     def forward(self, dict, is_cross: bool, place_in_unet: str):
         self.step_store["attn"].append(dict["attn"])
+        if "size" in dict:
+            self.step_store.setdefault("size", []).append(dict["size"])
+            self.heads = dict.get("heads", getattr(self, "heads", 8))
         return dict
 
     def reset(self):
@@ -82,6 +94,20 @@ class AttentionStore(AttentionControl):
         super().__init__()
         self.step_store = self.get_empty_store()
         self.early_exit = early_exit
+
+    def maps_per_image(self, B, R, layers=(0, 1, 2, 3), captured=False):
+        """(B, N, R, R) maps of the stored logits (CaptureMaps, dense backward), or with
+        ``captured`` an ``ops.CapturedMaps`` whose ``select`` gathers rows with the sparse
+        backward.  Needs a store that holds logits (``stores_logits``)."""
+        zs = [z for li, z in enumerate(self.step_store["attn"]) if li in layers]
+        ss = [sz for li, sz in enumerate(self.step_store.get("size", [])) if li in layers]
+        if not zs:
+            raise RuntimeError("maps_per_image: no captured layers (is the hook registered?)")
+        if len(ss) != len(zs):
+            raise RuntimeError("maps_per_image: the store holds attention, not logits (stores_logits unset)")
+        if captured:
+            return ops.CapturedMaps(zs, ss, B, R)
+        return ops.capture_maps(zs, ss, B, R)
 
 
 class LogitStore(AttentionStore):
@@ -97,22 +123,36 @@ class LogitStore(AttentionStore):
     def get_empty_store():
         return {"attn": [], "size": []}
 
-    def forward(self, dict, is_cross: bool, place_in_unet: str):
-        self.step_store["attn"].append(dict["attn"])
-        self.step_store["size"].append(dict["size"])
-        self.heads = dict.get("heads", getattr(self, "heads", 8))
-        return dict
 
-    def maps_per_image(self, B, R, layers=(0, 1, 2, 3), captured=False):
-        """(B, N, R, R) maps (CaptureMaps, dense backward), or with ``captured`` an
-        ``ops.CapturedMaps`` whose ``select`` gathers rows with the sparse backward."""
-        zs = [z for li, z in enumerate(self.step_store["attn"]) if li in layers]
-        ss = [sz for li, sz in enumerate(self.step_store["size"]) if li in layers]
-        if not zs:
-            raise RuntimeError("LogitStore: no captured layers (is the hook registered?)")
-        if captured:
-            return ops.CapturedMaps(zs, ss, B, R)
-        return ops.capture_maps(zs, ss, B, R)
+# A/B: 0 = run_and_find_attn fills an AttentionStore with the materialised (B·H, R², N)
+# attention of every captured layer, as in r02
+EVAL_LOGITS = os.environ.get("SKP_EVAL_LOGITS", "1") != "0"
+
+
+@contextlib.contextmanager
+def logit_capture(controllers):
+    """Capture LOGITS into the given ``AttentionStore``s for one pass whose maps the caller
+    collects before the block ends (``run_and_find_attn`` / ``run_and_find_attn_per_image``).
+
+    The reference stores the (B·H, R², N) attention of every captured layer (1.05 GB per
+    layer at N=500, R=128, B·H=8; ptp_utils.py:508-538) and ``collect_maps`` immediately
+    reduces it to the (N', R', R') map (optimize.py:27-79); here the same maps come from the
+    fused ``skp_capture_maps_fwd`` over the stored (B·H, s², N) logits, and nothing of size
+    (B·H, R², N) is written.  Stores that already hold logits, stores of another class and
+    non-store controllers are left alone.  On exit every switched store is reset (the
+    reference's callers reset after collecting) and switched back."""
+    switched = []
+    if EVAL_LOGITS:
+        for ctl in controllers.values():
+            if type(ctl) is AttentionStore and not ctl.stores_logits and not ctl.step_store["attn"]:
+                ctl.stores_logits = True
+                switched.append(ctl)
+    try:
+        yield
+    finally:
+        for ctl in switched:
+            del ctl.stores_logits
+            ctl.reset()
 
 
 # --------------------------------------------------------------------------- A1 capture hook
@@ -181,6 +221,8 @@ def register_attention_control(model, controller, feature_upsample_res=256):
                 count = register_recr(net__, count, place_in_unet)
         return count
 
+    if not isinstance(controller, DummyController):
+        controller.feature_upsample_res = feature_upsample_res   # R of the logit-store maps
     cross_att_count = 0
     for name, net in model.named_children():
         if "up" in name:
@@ -249,12 +291,13 @@ def run_and_find_attn(ldm, image, context, noise_level=-1, device="cuda",
                       upsample_res=32, indices=None, controllers=None):
     """ptp_utils.py:234-272: one UNet pass, then collect_maps + reset per controller."""
     from .optimize import collect_maps
-    find_pred_noise(ldm, image, context, noise_level=noise_level, device=device)
     attention_maps = []
-    for controller in controllers:
-        attention_maps.append(collect_maps(controllers[controller], from_where=from_where,
-                                           upsample_res=upsample_res, layers=layers, indices=indices))
-        controllers[controller].reset()
+    with logit_capture(controllers):   # same maps, no (B·H, R², N) attention written
+        find_pred_noise(ldm, image, context, noise_level=noise_level, device=device)
+        for controller in controllers:
+            attention_maps.append(collect_maps(controllers[controller], from_where=from_where,
+                                               upsample_res=upsample_res, layers=layers, indices=indices))
+            controllers[controller].reset()
     return attention_maps
 
 
@@ -270,6 +313,13 @@ def run_and_find_attn_per_image(ldm, images, context, noise_level=-1, device="cu
     with ``stacked`` (logit store, no ``indices``/``upsample_res``) one (B, N, R, R) tensor per
     controller instead, so callers can gather rows of several images in one autograd op.
     """
+    with logit_capture(controllers):   # same maps, no (B·H, R², N) attention written
+        return _collect_per_image(ldm, images, context, noise_level, device, layers, upsample_res, indices,
+                                  controllers, stacked, captured)
+
+
+def _collect_per_image(ldm, images, context, noise_level, device, layers, upsample_res, indices, controllers,
+                       stacked, captured):
     find_pred_noise(ldm, images, context, noise_level=noise_level, device=device)
     B = images.shape[0]
     out = []

@@ -56,7 +56,9 @@ def _replay_inputs(monkeypatch, ldm, latents, noises, check_vae=True):
     real = ptp_utils.image2latent
 
     def replay(model, image, device):
-        ref = lat.pop(0)
+        # a batched capture pass (TTA augmentation_batch, find_best_indices capture_batch) encodes
+        # several recorded captures at once
+        ref = torch.cat([lat.pop(0) for _ in range(image.shape[0])])
         if check_vae:
             mine = real(model, image, device)
             assert torch.allclose(mine, ref, atol=1e-4), float((mine - ref).abs().max())
@@ -68,7 +70,7 @@ def _replay_inputs(monkeypatch, ldm, latents, noises, check_vae=True):
         timesteps = inner.timesteps
 
         def add_noise(self, x, noise, t):
-            return inner.add_noise(x, nz.pop(0), t)
+            return inner.add_noise(x, torch.cat([nz.pop(0) for _ in range(x.shape[0])]), t)
     ldm.scheduler = Sched()
     return lat, nz
 

@@ -1,0 +1,60 @@
+"""CPU checks of the store-side logic of the capture drivers (no kernels run).
+
+``ptp_utils.logit_capture`` switches a plain ``AttentionStore`` to logit capture for one
+``run_and_find_attn`` pass and restores it (reference ptp_utils.py:63-83: the store's contents
+are collected and reset by the same call, ptp_utils.py:234-272)."""
+import torch
+
+from stablekeypoints_amd import ptp_utils
+
+
+def test_logit_capture_switches_plain_store_and_restores():
+    st = ptp_utils.AttentionStore(early_exit=True)
+    assert st.stores_logits is False and st.step_store == {"attn": []}
+    with ptp_utils.logit_capture({"cuda:0": st}):
+        assert st.stores_logits is True
+        st({"attn": torch.zeros(2, 4, 3), "size": 2, "heads": 2}, True, "up")
+        assert st.step_store["size"] == [2] and st.heads == 2
+    assert st.stores_logits is False and "stores_logits" not in vars(st)
+    assert st.step_store == {"attn": []}, "the switched store is reset on exit"
+
+
+def test_logit_capture_restores_on_error():
+    st = ptp_utils.AttentionStore()
+    try:
+        with ptp_utils.logit_capture({0: st}):
+            st({"attn": torch.zeros(1), "size": 1, "heads": 1}, True, "up")
+            raise RuntimeError("boom")
+    except RuntimeError:
+        pass
+    assert st.stores_logits is False and st.step_store == {"attn": []}
+
+
+def test_logit_capture_leaves_other_controllers_alone():
+    class MyStore(ptp_utils.AttentionStore):   # a user subclass may read the attention itself
+        pass
+    logits = ptp_utils.LogitStore()
+    mine = MyStore()
+    busy = ptp_utils.AttentionStore()
+    busy({"attn": torch.ones(1)}, True, "up")   # holds attention already: not switched
+    with ptp_utils.logit_capture({0: logits, 1: mine, 2: busy}):
+        assert logits.stores_logits and not mine.stores_logits and not busy.stores_logits
+    assert logits.stores_logits and len(busy.step_store["attn"]) == 1
+
+
+def test_logit_capture_ab_switch(monkeypatch):
+    monkeypatch.setattr(ptp_utils, "EVAL_LOGITS", False)
+    st = ptp_utils.AttentionStore()
+    with ptp_utils.logit_capture({0: st}):
+        assert not st.stores_logits
+
+
+def test_attention_store_maps_need_logits():
+    st = ptp_utils.AttentionStore()
+    st({"attn": torch.zeros(8, 16, 4)}, True, "up")
+    try:
+        st.maps_per_image(1, 16)
+    except RuntimeError as e:
+        assert "logits" in str(e)
+    else:
+        raise AssertionError("maps_per_image on stored attention must raise")

@@ -85,6 +85,17 @@ def main():
             res[name] = timed(lambda: torch.autograd.grad(maps, z8, gm, retain_graph=True), args.iters)
             ops.FUSED_MAPS = True
             del z8, maps, gm
+        elif name in ("mapssel8", "mapssel8_dense"):   # sparse backward of 10 selected rows per image, bench shape
+            sizes = (16, 16, 16, 32)
+            z8 = [(torch.randn(8 * H, s * s, N, device=dev, generator=g) * 2).requires_grad_(True) for s in sizes]
+            ops.SEL_BWD = name == "mapssel8"
+            cm = ops.CapturedMaps(z8, sizes, 8, R)
+            rows = [torch.randperm(N, device=dev, generator=g)[:10] for _ in range(8)]
+            out = cm.select(rows)
+            gsel = torch.randn_like(out)
+            res[name] = timed(lambda: torch.autograd.grad(out, z8, gsel, retain_graph=True), args.iters)
+            ops.SEL_BWD = True
+            del z8, cm, out, gsel
         elif name == "sum1g":   # read-bandwidth reference: torch reduction over a fresh 1 GiB tensor
             big = torch.empty(256 * 1024 * 1024, device=dev).normal_()
             res[name] = timed(lambda: big.sum(), args.iters)
