@@ -17,7 +17,8 @@
 //   sel_gather   zsel[bh][q][k] = z_low[bh][q][tok_k]                         (the selected logits)
 //   sel_dot      per (bh, row y): a_k, e_k = a_k·g_k, dot → E[bh][k][p] = e_k, pix[bh][p] = (mb, −dot)
 //                with mb = log2(1/Σ) − max·log2e, so a = exp2(z·log2e + mb)
-//   sel_adj      per (bh, k): es[bh][k] = bicubicᵀ(E[bh][k])  (R² → s², gather form, deterministic)
+//   sel_adj      per (bh, k): es[bh][k] = bicubicᵀ(E[bh][k])  (R² → s², separable through an LDS table
+//                of the adjoint weights, deterministic)
 //   sel_dense    per (bh, 128-token chunk): the dense part's adjoint, plus es at the selected tokens
 // sel_dense is the hot kernel.  One workgroup = R/16 waves; wave w owns output columns
 // [16w, 16w+16) of every row and lanes own token pairs (packed f32: v_pk_fma).  With R = S·RATIO
@@ -43,7 +44,6 @@ namespace {
 
 constexpr float L2E = 1.4426950408889634f;
 constexpr int SEL_MAXK = 32;
-constexpr int PW = 16;   // output pixels per wave and row
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 
@@ -65,8 +65,33 @@ __global__ void sel_gather_kernel(const float* __restrict__ z, int BH, int SS, i
   zsel[e] = (t >= 0 && t < N) ? z[bq * N + t] : 0.0f;
 }
 
+// ------------------------------------------------------------------------------ bicubic adjoint matrix
+// A[j][x] = Σ_m [taps(x).i[m] == j]·taps(x).w[m] (m ascending): the weight output index x puts on
+// low-res index j (clamped edge taps add), the same for rows and columns.  Built in LDS, one
+// column per thread.
+__device__ __forceinline__ void build_adj(float* A, int S, int R) {
+  for (int e = threadIdx.x; e < S * R; e += blockDim.x) A[e] = 0.0f;
+  __syncthreads();
+  for (int x = threadIdx.x; x < R; x += blockDim.x) {
+    const Taps4 t = bicubic_taps(x, S, R);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) A[t.i[m] * R + x] += t.w[m];
+  }
+  __syncthreads();
+}
+// output indices whose taps can reach low-res index j: src ∈ [j − 2, j + 2) (clamped edges included)
+__device__ __forceinline__ void adj_range(int j, int S, int R, int& lo, int& hi) {
+  const float r = (float)R / (float)S;
+  lo = max(0, (int)floorf((j - 1.5f) * r - 0.5f) - 1);
+  hi = min(R - 1, (int)ceilf((j + 2.5f) * r - 0.5f) + 1);
+  if (j == 0) lo = 0;
+  if (j == S - 1) hi = R - 1;
+}
+
 // ------------------------------------------------------------------------------ sel_dot
-// one block per (bh, y); threads over x.  LDS: the vertical pass Vs[S][K] of the selected logits.
+// one block per (bh, y); threads over x.  Per pixel: a_k, e_k = a_k·g_k (E[bh][k][p]) and dot →
+// pix[bh][p] = (mb, −dot) with mb = log2(1/Σ) − max·log2e, so a = exp2(z·log2e + mb).
+// LDS: the vertical pass Vs[S][K] of the selected logits.
 __global__ __launch_bounds__(256) void sel_dot_kernel(const float* __restrict__ zsel, int S, int R, int H, int K,
                                                       const long long* __restrict__ tok,
                                                       const float* __restrict__ gsel, float gscale,
@@ -111,72 +136,81 @@ __global__ __launch_bounds__(256) void sel_dot_kernel(const float* __restrict__ 
 }
 
 // ------------------------------------------------------------------------------ sel_adj
-// es[bh][k][i][j] = Σ_y Σ_x wy(y→i)·wx(x→j)·E[bh][k][y][x]: separable gather through LDS.
-__device__ __forceinline__ float adj_w(int dst, int src, int n_in, int n_out) {   // weight of dst's taps on src
-  const Taps4 t = bicubic_taps(dst, n_in, n_out);
-  float w = 0.0f;
-#pragma unroll
-  for (int m = 0; m < 4; ++m) w += (t.i[m] == src) ? t.w[m] : 0.0f;
-  return w;
-}
-// output indices whose taps can reach low-res index j: src ∈ [j − 2, j + 2) (clamped edges included)
-__device__ __forceinline__ void adj_range(int j, int S, int R, int& lo, int& hi) {
-  const float r = (float)R / (float)S;
-  lo = max(0, (int)floorf((j - 1.5f) * r - 0.5f) - 1);
-  hi = min(R - 1, (int)ceilf((j + 2.5f) * r - 0.5f) + 1);
-  if (j == 0) lo = 0;
-  if (j == S - 1) hi = R - 1;
-}
-
-__global__ __launch_bounds__(256) void sel_adj_kernel(const float* __restrict__ E, int S, int R, int K,
+// es[bh][k] = bicubicᵀ(E[bh][k]) (R² → s²), separable, through LDS: A[S][R] (the adjoint matrix,
+// built once), the horizontal pass Hs[y][j] = Σ_x A[j][x]·E[y][x] over 32-row tiles of E staged in
+// LDS, then es[i][j] = Σ_y A[i][y]·Hs[y][j].  Fixed summation order (x, then y ascending).
+constexpr int SEL_ADJ_TILE = 32;
+__global__ __launch_bounds__(256) void sel_adj_kernel(const float* __restrict__ E, int S, int R,
                                                       float* __restrict__ es) {
-  extern __shared__ float Hs[];   // R × S
-  const size_t bk = blockIdx.x;   // bh·K + k
+  extern __shared__ float sh[];
+  float* A = sh;                 // S × R
+  float* Hs = A + S * R;         // R × S
+  float* Et = Hs + R * S;        // SEL_ADJ_TILE × R
+  const size_t bk = blockIdx.x;  // bh·K + k
   const float* Eb = E + bk * (size_t)R * R;
-  for (int e = threadIdx.x; e < R * S; e += blockDim.x) {
-    const int y = e / S, j = e - y * S;
-    int x0, x1;
-    adj_range(j, S, R, x0, x1);
-    float acc = 0.0f;
-    for (int x = x0; x <= x1; ++x) {
-      const float w = adj_w(x, j, S, R);
-      if (w != 0.0f) acc = fmaf(w, Eb[(size_t)y * R + x], acc);
+  build_adj(A, S, R);
+  for (int y0 = 0; y0 < R; y0 += SEL_ADJ_TILE) {
+    const int ny = min(SEL_ADJ_TILE, R - y0);
+    const float4* src = reinterpret_cast<const float4*>(Eb + (size_t)y0 * R);
+    for (int e = threadIdx.x; e < ny * R / 4; e += blockDim.x) reinterpret_cast<float4*>(Et)[e] = src[e];
+    __syncthreads();
+    for (int e = threadIdx.x; e < ny * S; e += blockDim.x) {
+      const int yy = e / S, j = e - yy * S;
+      int x0, x1;
+      adj_range(j, S, R, x0, x1);
+      const float* Aj = A + j * R;
+      const float* Ey = Et + yy * R;
+      float acc = 0.0f;
+      for (int x = x0; x <= x1; ++x) acc = fmaf(Aj[x], Ey[x], acc);
+      Hs[(y0 + yy) * S + j] = acc;
     }
-    Hs[e] = acc;
+    __syncthreads();
   }
-  __syncthreads();
   for (int e = threadIdx.x; e < S * S; e += blockDim.x) {
     const int i = e / S, j = e - i * S;
     int y0, y1;
     adj_range(i, S, R, y0, y1);
+    const float* Ai = A + i * R;
     float acc = 0.0f;
-    for (int y = y0; y <= y1; ++y) {
-      const float w = adj_w(y, i, S, R);
-      if (w != 0.0f) acc = fmaf(w, Hs[y * S + j], acc);
-    }
+    for (int y = y0; y <= y1; ++y) acc = fmaf(Ai[y], Hs[y * S + j], acc);
     es[bk * (size_t)S * S + e] = acc;
   }
 }
 
 // ------------------------------------------------------------------------------ sel_dense
-struct SelLayers {   // up to 4 layers of the same s in one launch
+struct SelLayers {   // up to 4 layers of the same s per launch
   const float* z[4];
   const float2* pix[4];
   const float* es[4];
   float* dz[4];
 };
 
+// output columns per wave and row: 16 where R/s ≥ 8; 8 at R/s = 4 (the s = 32 layers), which keeps
+// the band at 6 low-res columns and the registers under 128 (4 waves per SIMD, 16-wave blocks)
+template <int RATIO>
+constexpr int sel_pw() { return RATIO >= 8 ? 16 : 8; }
+template <int RATIO>
+constexpr int sel_nc() { return lo_rel(sel_pw<RATIO>() - 1, RATIO) + 6; }   // band columns: relative −2 … lo_rel(PW−1)+3
+
+// One block = (layer l, head bh, 128-token chunk); R/PW waves, wave w owns output columns
+// [PW·w, PW·w + PW) of every row, lanes own token pairs.  The 4 low-res z rows the current output
+// rows interpolate sit in an LDS ring Z[slot][column][lane] shared by all waves (bands overlap, so
+// each column is loaded once per block); the next row is fetched into registers at the start of a
+// phase and stored into the retired slot behind the emit's first barrier.  acc (the vertical adjoint
+// of the 4 rows) and the per-row V / Hs stay in registers.
 template <int RATIO, int S>
-__global__ __launch_bounds__((S * RATIO / PW) * WAVE) __attribute__((amdgpu_waves_per_eu(2)))
+__global__ __launch_bounds__((S * RATIO / sel_pw<RATIO>()) * WAVE)
 void sel_dense_kernel(SelLayers sl, int BH, int H, int N, int K, const long long* __restrict__ tok, int nchunk,
                       int njobs) {
+  constexpr int PW = sel_pw<RATIO>();
   constexpr int R = S * RATIO;
   constexpr int WAVES = R / PW;
   constexpr int CS = PW / RATIO;                  // band step in low-res columns
-  constexpr int NC = lo_rel(PW - 1, RATIO) + 6;   // band columns: relative −2 … lo_rel(PW−1)+3
-  constexpr int NTH = WAVES * WAVE;
+  constexpr int NC = sel_nc<RATIO>();
+  constexpr int CPT = (S + WAVES - 1) / WAVES;    // ring columns each thread fetches per row
   static_assert(R % PW == 0 && PW % RATIO == 0, "band geometry");
-  __shared__ __attribute__((aligned(16))) f2 M[WAVES][NC][WAVE];   // band partials of one low-res row
+  __shared__ __attribute__((aligned(16))) f2 M[WAVES * NC * WAVE];   // band partials of one low-res row
+  __shared__ __attribute__((aligned(16))) f2 Z[4 * S * WAVE];        // ring of 4 low-res z rows
 
   // XCD-major job order: XCD x walks a contiguous job range, so a head's 128-token chunks share
   // one L2 (its z_low slab)
@@ -195,6 +229,13 @@ void sel_dense_kernel(SelLayers sl, int BH, int H, int N, int K, const long long
   const float2* pixl = sl.pix[l] + (size_t)bh * R * R;
   float* dzl = sl.dz[l] + (size_t)bh * S * S * N;
   const float* esl = sl.es[l] + (size_t)bh * K * S * S;
+  // the selected rows this lane's token pair (n0, n0 + 1) carries (bit k: tok_k; duplicates add)
+  unsigned mx = 0u, my = 0u;
+  for (int k = 0; k < K; ++k) {
+    const long long t = tok[(size_t)b * K + k];
+    if (t == n0) mx |= 1u << k;
+    if (t == n0 + 1) my |= 1u << k;
+  }
 
   // tap weights of the RATIO phases (identical for rows and columns): lane u < RATIO computes
   // phase u's taps exactly as the forward did, then every lane reads them as uniform values
@@ -208,50 +249,74 @@ void sel_dense_kernel(SelLayers sl, int BH, int H, int N, int K, const long long
         wt[u][m] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t.w[m]), u));
   }
   auto col_abs = [&](int c) { return min(max(w * CS + c - 2, 0), S - 1); };
-  auto load_row = [&](int r, f2 (&dst)[NC]) {   // z_low row r (clamped), the band's columns, this lane's pair
+  auto slot = [](int r) { return (r + 4) & 3; };   // virtual rows ≥ −2
+  f2 pre[CPT];
+  auto fetch = [&](int r) {   // z_low row r (clamped): this thread's ring columns, its lane's token pair
     const int rr = min(max(r, 0), S - 1);
 #pragma unroll
-    for (int c = 0; c < NC; ++c)
-      dst[c] = *reinterpret_cast<const f2*>(zl + ((size_t)rr * S + col_abs(c)) * N + nl);
+    for (int k = 0; k < CPT; ++k) {
+      const int col = w + k * WAVES;
+      if (col < S) pre[k] = *reinterpret_cast<const f2*>(zl + ((size_t)rr * S + col) * N + nl);
+    }
   };
-
-  f2 Zw[4][NC], acc[4][NC];
+  auto stash = [&](int r) {
+    f2* zs = Z + slot(r) * S * WAVE;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    load_row(k - 2, Zw[k]);
+    for (int k = 0; k < CPT; ++k) {
+      const int col = w + k * WAVES;
+      if (col < S) zs[col * WAVE + lane] = pre[k];
+    }
+  };
+#pragma unroll 1
+  for (int r = -2; r <= 1; ++r) {
+    fetch(r);
+    stash(r);
+  }
+  __syncthreads();
+
+  f2 acc[4][NC];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
 #pragma unroll
     for (int c = 0; c < NC; ++c) acc[k][c] = (f2)0.0f;
-  }
   const f2 l2e = (f2)L2E;
 
-  auto emit = [&](int r, const f2 (&v)[NC]) {   // low-res row r complete: merge bands, add es, store
+  // low-res row r complete: merge the bands, add es at the selected tokens, store; then the
+  // fetched row `next` goes into the retired slot (every wave is past its reads of it)
+  auto emit = [&](int r, const f2 (&v)[NC], int next) {
 #pragma unroll
-    for (int c = 0; c < NC; ++c) M[w][c][lane] = v[c];
+    for (int c = 0; c < NC; ++c) M[(w * NC + c) * WAVE + lane] = v[c];
     __syncthreads();
-    for (int e = tid; e < S * WAVE; e += NTH) {
-      const int j = e >> 6, ln = e & 63;
+    const int n = chunk * 128 + 2 * lane;
+    for (int j = w; j < S; j += WAVES) {   // a wave per low-res column (uniform j)
       f2 s = (f2)0.0f;
-      for (int w2 = 0; w2 < WAVES; ++w2) {   // contributors in a fixed order: band, then column
-        for (int c = 0; c < NC; ++c) {
-          const int a = min(max(w2 * CS + c - 2, 0), S - 1);
-          if (a == j) s += M[w2][c][ln];
-        }
+      if (j == 0 || j == S - 1) {   // clamped edge columns: every (band, column) folding into j, band order
+        for (int w2 = 0; w2 < WAVES; ++w2)
+          for (int c = 0; c < NC; ++c)
+            if (min(max(w2 * CS + c - 2, 0), S - 1) == j) s += M[(w2 * NC + c) * WAVE + lane];
+      } else {                      // interior: one column per band, c = j + 2 − w2·CS (band order)
+        const int wlo = max(0, (j + 2 - NC + CS) / CS), whi = min(WAVES - 1, (j + 2) / CS);
+        for (int w2 = wlo; w2 <= whi; ++w2) s += M[(w2 * NC + j + 2 - w2 * CS) * WAVE + lane];
       }
-      const int n = chunk * 128 + 2 * ln;
       if (n < N) {
-        for (int k = 0; k < K; ++k) {   // the sparse part at the selected tokens (k order)
-          const long long t = tok[(size_t)b * K + k];
-          if (t == n) s.x += esl[((size_t)k * S + r) * S + j];
-          if (t == n + 1) s.y += esl[((size_t)k * S + r) * S + j];
-        }
+        for (unsigned m = mx; m; m &= m - 1) s.x += esl[((size_t)__builtin_ctz(m) * S + r) * S + j];   // k order
+        for (unsigned m = my; m; m &= m - 1) s.y += esl[((size_t)__builtin_ctz(m) * S + r) * S + j];
         *reinterpret_cast<f2*>(dzl + ((size_t)r * S + j) * N + n) = s;
       }
     }
+    if (next <= S + 1) stash(next);
     __syncthreads();
   };
 
   // phases: lo = first tap row of the output rows y = RATIO·(lo + 1) + RATIO/2 + v, v = 0..RATIO−1
+#pragma unroll 1
   for (int lo = -2; lo <= S - 2; ++lo) {
+    const bool more = lo + 1 <= S - 2;             // the next phase needs row lo + 4
+    if (more) fetch(lo + 4);
+    const f2* z0 = Z + slot(lo) * S * WAVE + lane;
+    const f2* z1 = Z + slot(lo + 1) * S * WAVE + lane;
+    const f2* z2 = Z + slot(lo + 2) * S * WAVE + lane;
+    const f2* z3 = Z + slot(lo + 3) * S * WAVE + lane;
 #pragma unroll
     for (int v = 0; v < RATIO; ++v) {
       const int y = RATIO * (lo + 1) + RATIO / 2 + v;
@@ -260,10 +325,11 @@ void sel_dense_kernel(SelLayers sl, int BH, int H, int N, int K, const long long
       f2 V[NC], Hs[NC];
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
-        f2 t = Zw[0][c] * wt[u][0];
-        t = __builtin_elementwise_fma(Zw[1][c], (f2)wt[u][1], t);
-        t = __builtin_elementwise_fma(Zw[2][c], (f2)wt[u][2], t);
-        t = __builtin_elementwise_fma(Zw[3][c], (f2)wt[u][3], t);
+        const int o = col_abs(c) * WAVE;
+        f2 t = z0[o] * wt[u][0];
+        t = __builtin_elementwise_fma(z1[o], (f2)wt[u][1], t);
+        t = __builtin_elementwise_fma(z2[o], (f2)wt[u][2], t);
+        t = __builtin_elementwise_fma(z3[o], (f2)wt[u][3], t);
         V[c] = t;
         Hs[c] = (f2)0.0f;
       }
@@ -295,20 +361,21 @@ void sel_dense_kernel(SelLayers sl, int BH, int H, int N, int K, const long long
     if (lo < 0) {
 #pragma unroll
       for (int c = 0; c < NC; ++c) acc[1][c] += acc[0][c];   // rows −2, −1 clamp to row 0 (next slot)
+      __syncthreads();                                        // every wave past its reads of slot(lo)
+      if (more) stash(lo + 4);
+      __syncthreads();
     } else {
-      emit(lo, acc[0]);
+      emit(lo, acc[0], more ? lo + 4 : S + 2);
     }
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       acc[0][c] = acc[1][c]; acc[1][c] = acc[2][c]; acc[2][c] = acc[3][c]; acc[3][c] = (f2)0.0f;
-      Zw[0][c] = Zw[1][c]; Zw[1][c] = Zw[2][c]; Zw[2][c] = Zw[3][c];
     }
-    if (lo + 1 <= S - 2) load_row(lo + 4, Zw[3]);   // rows lo+1 … lo+4 for the next phase
   }
   // the window now holds virtual rows S−1, S, S+1, S+2: all clamp to row S−1
 #pragma unroll
   for (int c = 0; c < NC; ++c) acc[0][c] = (acc[0][c] + acc[1][c]) + (acc[2][c] + acc[3][c]);
-  emit(S - 1, acc[0]);
+  emit(S - 1, acc[0], S + 2);
 }
 
 template <int RATIO, int S>
@@ -316,8 +383,8 @@ void launch_dense(const SelLayers& sl, int nl, int BH, int H, int N, int K, cons
   const int nchunk = (N + 127) / 128;
   const int njobs = nl * BH * nchunk;
   const int grid = 8 * ((njobs + 7) / 8);
-  hipLaunchKernelGGL((sel_dense_kernel<RATIO, S>), dim3(grid), dim3((S * RATIO / PW) * WAVE), 0, st, sl, BH, H, N, K,
-                     tok, nchunk, njobs);
+  hipLaunchKernelGGL((sel_dense_kernel<RATIO, S>), dim3(grid), dim3((S * RATIO / sel_pw<RATIO>()) * WAVE), 0, st, sl,
+                     BH, H, N, K, tok, nchunk, njobs);
 }
 
 // (R, S) pairs with a compiled sel_dense kernel
@@ -365,8 +432,9 @@ struct SelWs {   // workspace carve-up (floats)
 };
 SelWs sel_ws(const int* sizes, int L, int B, int H, int R, int K) {
   SelWs w{};
-  size_t smax2 = 1;
-  for (int l = 0; l < L; ++l) smax2 = std::max(smax2, (size_t)sizes[l] * sizes[l]);
+  size_t smax = 1;
+  for (int l = 0; l < L; ++l) smax = std::max(smax, (size_t)sizes[l]);
+  const size_t smax2 = smax * smax;
   const size_t BH = (size_t)B * H, RR = (size_t)R * R;
   w.zsel = 0;
   w.E = w.zsel + ((BH * smax2 * K + 3) & ~(size_t)3);
@@ -442,8 +510,9 @@ extern "C" int skp_capture_maps_bwd_sel(const float* const* z_low, const int* si
                        st, zsel, S, R, H, K, sel_tok, gsel, gscale, reinterpret_cast<const float2*>(stats[l]), E,
                        pix + (size_t)l * BH * RR);
     SKP_LAUNCH_CHECK();
-    hipLaunchKernelGGL(sel_adj_kernel, dim3((unsigned)(BH * K)), dim3(256), (size_t)R * S * sizeof(float), st, E, S, R,
-                       K, es + (size_t)l * BH * K * smax * smax);
+    hipLaunchKernelGGL(sel_adj_kernel, dim3((unsigned)(BH * K)), dim3(256),
+                       (size_t)(2 * S * R + SEL_ADJ_TILE * R) * sizeof(float), st, E, S, R,
+                       es + (size_t)l * BH * K * smax * smax);
     SKP_LAUNCH_CHECK();
   }
   // the dense part: layers of equal s share a launch (up to 4 per launch)
