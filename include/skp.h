@@ -234,6 +234,21 @@ int skp_attn_fwd(const float* Q, const float* K, const float* V, float* O, float
 int skp_attn_bwd_flash(const float* Q, const float* K, const float* V, const float* dO, const float* stats,
                        const float* D, float* dS, float* dV, float* dK, int BH, int S, int L, int d, float scale,
                        void* stream);
+/* skp_attn_fwd / skp_attn_bwd_flash on the projections' own layout, without the head permutes of
+ * diffusers' reshape_heads_to_batch_dim / reshape_batch_dim_to_heads (CrossAttention.forward,
+ * reference ptp_utils.py:481-506 for the layers the capture does not patch): element (b, h, s, j)
+ * of Q / K / V / O / dO / dV / dK sits at base + b·sb + s·rs + h·d + j (a (B, S, H·d) tensor:
+ * sb = S·H·d, rs = H·d; a context shared by the batch: sb = 0 — then dK / dV still get their own
+ * per-image rows and the caller sums them).  stats (B·H, S, 2), D (B·H, S), dS (B·H, S, L)
+ * contiguous, as in the (B·H, S, d) entries; strides multiples of 4, 16-byte aligned.         */
+int skp_attn_fwd_bshd(const float* Q, long long q_sb, int q_rs, const float* K, long long k_sb, int k_rs,
+                      const float* V, long long v_sb, int v_rs, float* O, long long o_sb, int o_rs, float* stats, int B,
+                      int H, int S, int L, int d, float scale, void* stream);
+int skp_attn_bwd_flash_bshd(const float* Q, long long q_sb, int q_rs, const float* K, long long k_sb, int k_rs,
+                            const float* V, long long v_sb, int v_rs, const float* dO, long long o_sb, int o_rs,
+                            const float* stats, const float* D, float* dS, float* dV, long long dv_sb, int dv_rs,
+                            float* dK, long long dk_sb, int dk_rs, int B, int H, int S, int L, int d, float scale,
+                            void* stream);
 /* LayerNorm over the last dimension (the UNet transformer blocks' norm1/2/3; frozen γ, β):
  * x, y (rows, C), C a multiple of 4 ≤ 2048; stats (rows, 2) = (mean, 1/sqrt(var + eps)) for the
  * backward, which gives dx = rstd·(dy·γ − mean(dy·γ) − x̂·mean(dy·γ·x̂)).  Replaces

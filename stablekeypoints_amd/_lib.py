@@ -55,6 +55,11 @@ _SIGS = {
     "skp_attn_bwd_kv": [_p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _p],
     "skp_attn_fwd": [_p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _p],
     "skp_attn_bwd_flash": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _p],
+    "skp_attn_fwd_bshd": [_p, _c_ll, _c_int, _p, _c_ll, _c_int, _p, _c_ll, _c_int, _p, _c_ll, _c_int, _p, _c_int, _c_int,
+                          _c_int, _c_int, _c_int, _c_float, _p],
+    "skp_attn_bwd_flash_bshd": [_p, _c_ll, _c_int, _p, _c_ll, _c_int, _p, _c_ll, _c_int, _p, _c_ll, _c_int, _p, _p, _p,
+                                _p, _c_ll, _c_int, _p, _c_ll, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_float,
+                                _p],
     "skp_layernorm_fwd": [_p, _p, _p, _c_ll, _c_int, _c_float, _p, _p, _p],
     "skp_layernorm_bwd": [_p, _p, _p, _p, _c_ll, _c_int, _p, _p],
     "skp_geglu_fwd": [_p, _c_ll, _c_int, _p, _p],

@@ -268,6 +268,22 @@ extern "C" int skp_attn_dscore(const float* P, const float* dO, const float* V, 
 }
 
 // ------------------------------------------------------------------------------------------------
+// Head layouts of the attention operands.  Row s of head b·H + h starts at base + b·sb + h·d + s·rs:
+//   (B·H, S, d) contiguous:               H = 1, sb = S·d, rs = d;
+//   (B, S, H·d), the projections' own layout (diffusers' to_q / to_k / to_v output and to_out
+//   input, no head permute):             sb = S·H·d, rs = H·d;
+//   a context shared by the batch (the token embedding expanded over B): sb = 0.
+struct AttnLay {
+  long long sb;
+  int rs;
+  template <typename T>
+  __device__ __forceinline__ T* at(T* base, int bh, int H, int d) const {
+    const int b = bh / H;
+    return base + (size_t)b * sb + (size_t)(bh - b * H) * d;
+  }
+};
+
+// ------------------------------------------------------------------------------------------------
 // Forward-only fused attention O = softmax(scale·Q Kᵀ) V for the UNet's self-attention layers
 // that need no backward (the first 64²-token layer: its input does not depend on the token
 // embedding), so no (B·H, S, L) score or probability tensor is written or read.
@@ -281,17 +297,21 @@ namespace {
 template <int KS, int DB>   // head dim / 4, 16-wide head-dim blocks (d ≤ 16·DB)
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__ Q, const float* __restrict__ K,
                                                        const float* __restrict__ V, float* __restrict__ O,
-                                                       float2* __restrict__ ST, int S, int L, float scale) {
+                                                       float2* __restrict__ ST, int S, int L, float scale, int H,
+                                                       AttnLay lq, AttnLay lk, AttnLay lv, AttnLay lo) {
   constexpr int d = 4 * KS, dp = d + 1;
   __shared__ float sK[64 * dp], sV[64 * 16 * DB];   // sV rows padded to 16·DB with zeros
-  const int b = blockIdx.y;
+  const int b = blockIdx.y;                         // b·H + h
   const int r0 = blockIdx.x * 64;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int row = r0 + 16 * w + (lane & 15);        // this lane's query row
+  const float* Qb = lq.at(Q, b, H, d);
+  const float* Kb = lk.at(K, b, H, d);
+  const float* Vb = lv.at(V, b, H, d);
   // B operand of Sᵀ = K·Qᵀ: Qᵀ[k = 4ks + (lane>>4)][j = row] (pre-scaled)
   float qv[KS];
   {
-    const float* q = Q + ((size_t)b * S + row) * d + (lane >> 4);
+    const float* q = Qb + (size_t)row * lq.rs + (lane >> 4);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) qv[ks] = q[4 * ks] * scale;
   }
@@ -302,12 +322,13 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
   for (int k0 = 0; k0 < L; k0 += 64) {
     __syncthreads();   // previous block's tiles consumed
     {
-      const float4* gK = reinterpret_cast<const float4*>(K + ((size_t)b * L + k0) * d);
-      const float4* gV = reinterpret_cast<const float4*>(V + ((size_t)b * L + k0) * d);
       for (int e = t; e < 64 * KS; e += 256) {
         const int key = e / KS, c = 4 * (e - key * KS);
         float4 kk = make_float4(0.f, 0.f, 0.f, 0.f), vv = kk;   // keys past L (ragged last block): zero
-        if (k0 + key < L) { kk = gK[e]; vv = gV[e]; }
+        if (k0 + key < L) {
+          kk = *reinterpret_cast<const float4*>(Kb + (size_t)(k0 + key) * lk.rs + c);
+          vv = *reinterpret_cast<const float4*>(Vb + (size_t)(k0 + key) * lv.rs + c);
+        }
         float* pk = sK + key * dp + c;
         pk[0] = kk.x; pk[1] = kk.y; pk[2] = kk.z; pk[3] = kk.w;
         *reinterpret_cast<float4*>(sV + key * 16 * DB + c) = vv;
@@ -369,7 +390,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
   }
   // lane: Oᵀ[d = 16db + 4(lane>>4) + r][row (lane & 15)] → O[row][d..d+3]
   const float inv = 1.0f / l;
-  float* orow = O + ((size_t)b * S + row) * d;
+  float* orow = lo.at(O, b, H, d) + (size_t)row * lo.rs;
 #pragma unroll
   for (int db = 0; db < DB; ++db) {
     const int dd = 16 * db + 4 * (lane >> 4);
@@ -381,27 +402,49 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
 
 }  // namespace
 
-extern "C" int skp_attn_fwd(const float* Q, const float* K, const float* V, float* O, float* stats, int BH, int S,
-                            int L, int d, float scale, void* stream) {
+namespace {
+int attn_fwd_launch(const float* Q, AttnLay lq, const float* K, AttnLay lk, const float* V, AttnLay lv, float* O,
+                    AttnLay lo, float* stats, int BH, int H, int S, int L, int d, float scale, void* stream) {
   SKP_CHECK_ARG(Q && K && V && O, "null pointer");
-  SKP_CHECK_ARG(BH > 0 && S > 0 && L > 0, "non-positive shape");
+  SKP_CHECK_ARG(BH > 0 && H > 0 && BH % H == 0 && S > 0 && L > 0, "non-positive shape");
   SKP_CHECK_ARG(S % 64 == 0, "S must be a multiple of 64");
   SKP_CHECK_ARG(BH <= 65535, "grid too large");
   SKP_CHECK_ARG(((reinterpret_cast<uintptr_t>(K) | reinterpret_cast<uintptr_t>(V) | reinterpret_cast<uintptr_t>(O)) &
                  15) == 0,
                 "tensors must be 16-byte aligned");
+  SKP_CHECK_ARG(((lk.rs | lv.rs | lo.rs | lk.sb | lv.sb | lo.sb) & 3) == 0, "K, V, O strides must be multiples of 4");
   SKP_CHECK_ARG((reinterpret_cast<uintptr_t>(stats) & 7) == 0, "stats must be 8-byte aligned");
   const dim3 grid((unsigned)(S / 64), (unsigned)BH);
   hipStream_t st = as_stream(stream);
   float2* ST = reinterpret_cast<float2*>(stats);
+#define SKP_AF(KS_, DB_)                                                                                        \
+  hipLaunchKernelGGL((attn_fwd_kernel<KS_, DB_>), grid, dim3(256), 0, st, Q, K, V, O, ST, S, L, scale, H, lq, lk, lv, \
+                     lo)
   switch (d) {
-    case 40: hipLaunchKernelGGL((attn_fwd_kernel<10, 3>), grid, dim3(256), 0, st, Q, K, V, O, ST, S, L, scale); break;
-    case 64: hipLaunchKernelGGL((attn_fwd_kernel<16, 4>), grid, dim3(256), 0, st, Q, K, V, O, ST, S, L, scale); break;
-    case 80: hipLaunchKernelGGL((attn_fwd_kernel<20, 5>), grid, dim3(256), 0, st, Q, K, V, O, ST, S, L, scale); break;
+    case 40: SKP_AF(10, 3); break;
+    case 64: SKP_AF(16, 4); break;
+    case 80: SKP_AF(20, 5); break;
     default: SKP_CHECK_ARG(false, "head dim must be 40, 64 or 80");
   }
+#undef SKP_AF
   SKP_LAUNCH_CHECK();
   return SKP_OK;
+}
+AttnLay contig(int rows, int d) { return AttnLay{(long long)rows * d, d}; }
+}  // namespace
+
+extern "C" int skp_attn_fwd(const float* Q, const float* K, const float* V, float* O, float* stats, int BH, int S,
+                            int L, int d, float scale, void* stream) {
+  return attn_fwd_launch(Q, contig(S, d), K, contig(L, d), V, contig(L, d), O, contig(S, d), stats, BH, 1, S, L, d,
+                         scale, stream);
+}
+
+extern "C" int skp_attn_fwd_bshd(const float* Q, long long q_sb, int q_rs, const float* K, long long k_sb, int k_rs,
+                                 const float* V, long long v_sb, int v_rs, float* O, long long o_sb, int o_rs,
+                                 float* stats, int B, int H, int S, int L, int d, float scale, void* stream) {
+  SKP_CHECK_ARG(B > 0 && H > 0 && (long long)B * H <= 65535, "bad B, H");
+  return attn_fwd_launch(Q, AttnLay{q_sb, q_rs}, K, AttnLay{k_sb, k_rs}, V, AttnLay{v_sb, v_rs}, O, AttnLay{o_sb, o_rs},
+                         stats, B * H, H, S, L, d, scale, stream);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -421,25 +464,30 @@ template <int KS, int DB, int WPE, bool RC>   // head dim / 4, 16-wide head-dim 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void attn_bwd_kv_kernel(
     const float* __restrict__ P, const float* __restrict__ dO, const float* __restrict__ Q, const float* __restrict__ V,
     const float* __restrict__ D, float* __restrict__ dS, float* __restrict__ dV, float* __restrict__ dK, int S, int L,
-    float alpha, const float* __restrict__ Kt, const float2* __restrict__ ST, float scale) {
+    float alpha, const float* __restrict__ Kt, const float2* __restrict__ ST, float scale, int H, AttnLay lo, AttnLay lq,
+    AttnLay lk, AttnLay lv, AttnLay ldv, AttnLay ldk) {
   constexpr int d = 4 * KS, dp = d + 1, dq = 16 * DB + 1;
   __shared__ float sV[64 * dp];     // this block's keys
   __shared__ float sK[RC ? 64 * dp : 1];
   __shared__ float2 sST[2][RC ? 64 : 1];
   __shared__ float sO[2][64 * dq], sQ[2][64 * dq];   // row blocks of dO and Q, double-buffered (zero-padded to 16·DB)
   __shared__ float sD[2][64];
-  const int b = blockIdx.y, k0 = blockIdx.x * 64;
+  const int b = blockIdx.y, k0 = blockIdx.x * 64;   // b = head b·H + h
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const float* Vb = lv.at(V, b, H, d);
+  const float* dOb = lo.at(dO, b, H, d);
+  const float* Qb = lq.at(Q, b, H, d);
   {
-    const float4* gV = reinterpret_cast<const float4*>(V + ((size_t)b * L + k0) * d);
     for (int e = t; e < 64 * KS; e += 256) {
       const int key = e / KS, c = 4 * (e - key * KS);
       const bool in = k0 + key < L;   // ragged last block (RC only): keys past L are zero
-      const float4 v = in ? gV[e] : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 v = in ? *reinterpret_cast<const float4*>(Vb + (size_t)(k0 + key) * lv.rs + c)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
       float* p = sV + key * dp + c;
       p[0] = v.x; p[1] = v.y; p[2] = v.z; p[3] = v.w;
       if constexpr (RC) {
-        const float4 kk = in ? reinterpret_cast<const float4*>(Kt + ((size_t)b * L + k0) * d)[e] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 kk = in ? *reinterpret_cast<const float4*>(lk.at(Kt, b, H, d) + (size_t)(k0 + key) * lk.rs + c)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
         float* pk = sK + key * dp + c;
         pk[0] = kk.x; pk[1] = kk.y; pk[2] = kk.z; pk[3] = kk.w;
       }
@@ -458,12 +506,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
   float2 fst = make_float2(0.0f, 0.0f);
   const int rl = 16 * w + 4 * (lane >> 4);
   auto fetch = [&](int r0) {
-    const float4* gO = reinterpret_cast<const float4*>(dO + ((size_t)b * S + r0) * d);
-    const float4* gQ = reinterpret_cast<const float4*>(Q + ((size_t)b * S + r0) * d);
 #pragma unroll
     for (int j = 0; j < NPF; ++j) {
       const int e = t + 256 * j;
-      if (e < 64 * KS) { fo[j] = gO[e]; fq[j] = gQ[e]; }
+      if (e < 64 * KS) {
+        const int row = e / KS, c = 4 * (e - row * KS);
+        fo[j] = *reinterpret_cast<const float4*>(dOb + (size_t)(r0 + row) * lo.rs + c);
+        fq[j] = *reinterpret_cast<const float4*>(Qb + (size_t)(r0 + row) * lq.rs + c);
+      }
     }
     if (t < 64) {
       fd = D[(size_t)b * S + r0 + t];
@@ -616,7 +666,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
           }
           const int dd = 16 * db + 4 * (lane >> 4);
           const int key = k0 + 16 * bj + (lane & 15);
-          if (dd < d && key < L) *reinterpret_cast<float4*>((m == 0 ? dV : dK) + ((size_t)b * L + key) * d + dd) = acc;
+          if (dd < d && key < L) {
+            float* dst = m == 0 ? ldv.at(dV, b, H, d) + (size_t)key * ldv.rs : ldk.at(dK, b, H, d) + (size_t)key * ldk.rs;
+            *reinterpret_cast<float4*>(dst + dd) = acc;
+          }
         }
         __syncthreads();
       }
@@ -637,10 +690,11 @@ extern "C" int skp_attn_bwd_kv(const float* P, const float* dO, const float* Q, 
                 "tensors must be 16-byte aligned");
   const dim3 grid((unsigned)(L / 64), (unsigned)BH);
   hipStream_t st = as_stream(stream);
+  const AttnLay ls = contig(S, d), ll = contig(L, d);
   switch (d) {
 #define SKP_BKV(KS_, DB_, W_) \
   hipLaunchKernelGGL((attn_bwd_kv_kernel<KS_, DB_, W_, false>), grid, dim3(256), 0, st, P, dO, Q, V, D, dS, dV, dK, S, L, \
-                     alpha, nullptr, nullptr, 0.0f)
+                     alpha, nullptr, nullptr, 0.0f, 1, ls, ls, ll, ll, ll, ll)
     case 40: SKP_BKV(10, 3, 2); break;
     case 64: SKP_BKV(16, 4, 1); break;
     case 80: SKP_BKV(20, 5, 1); break;
@@ -651,24 +705,28 @@ extern "C" int skp_attn_bwd_kv(const float* P, const float* dO, const float* Q, 
   return SKP_OK;
 }
 
-extern "C" int skp_attn_bwd_flash(const float* Q, const float* K, const float* V, const float* dO, const float* stats,
-                                  const float* D, float* dS, float* dV, float* dK, int BH, int S, int L, int d, float scale,
-                                  void* stream) {
+namespace {
+int attn_bwd_flash_launch(const float* Q, AttnLay lq, const float* K, AttnLay lk, const float* V, AttnLay lv,
+                          const float* dO, AttnLay lo, const float* stats, const float* D, float* dS, float* dV,
+                          AttnLay ldv, float* dK, AttnLay ldk, int BH, int H, int S, int L, int d, float scale,
+                          void* stream) {
   SKP_CHECK_ARG(Q && K && V && dO && stats && D && dS && dV && dK, "null pointer");
-  SKP_CHECK_ARG(BH > 0 && S > 0 && L > 0, "non-positive shape");
+  SKP_CHECK_ARG(BH > 0 && H > 0 && BH % H == 0 && S > 0 && L > 0, "non-positive shape");
   SKP_CHECK_ARG(S % 64 == 0, "S must be a multiple of 64");
   SKP_CHECK_ARG(BH <= 65535, "grid too large");
   SKP_CHECK_ARG(((reinterpret_cast<uintptr_t>(dO) | reinterpret_cast<uintptr_t>(Q) | reinterpret_cast<uintptr_t>(K) |
                   reinterpret_cast<uintptr_t>(V) | reinterpret_cast<uintptr_t>(dV) | reinterpret_cast<uintptr_t>(dK)) &
                  15) == 0 && (reinterpret_cast<uintptr_t>(stats) & 7) == 0,
                 "tensors must be 16-byte aligned (stats 8-byte)");
+  SKP_CHECK_ARG(((lq.rs | lk.rs | lv.rs | lo.rs | ldv.rs | ldk.rs | lq.sb | lk.sb | lv.sb | lo.sb | ldv.sb | ldk.sb) & 3) == 0,
+                "strides must be multiples of 4");
   const dim3 grid((unsigned)((L + 63) / 64), (unsigned)BH);
   hipStream_t st = as_stream(stream);
   const float2* ST = reinterpret_cast<const float2*>(stats);
   switch (d) {
 #define SKP_BFL(KS_, DB_, W_) \
   hipLaunchKernelGGL((attn_bwd_kv_kernel<KS_, DB_, W_, true>), grid, dim3(256), 0, st, nullptr, dO, Q, V, D, dS, dV, dK, \
-                     S, L, scale, K, ST, scale)
+                     S, L, scale, K, ST, scale, H, lo, lq, lk, lv, ldv, ldk)
     case 40: SKP_BFL(10, 3, 2); break;
     case 64: SKP_BFL(16, 4, 1); break;
     case 80: SKP_BFL(20, 5, 1); break;
@@ -677,4 +735,23 @@ extern "C" int skp_attn_bwd_flash(const float* Q, const float* K, const float* V
   }
   SKP_LAUNCH_CHECK();
   return SKP_OK;
+}
+}  // namespace
+
+extern "C" int skp_attn_bwd_flash(const float* Q, const float* K, const float* V, const float* dO, const float* stats,
+                                  const float* D, float* dS, float* dV, float* dK, int BH, int S, int L, int d, float scale,
+                                  void* stream) {
+  const AttnLay ls = contig(S, d), ll = contig(L, d);
+  return attn_bwd_flash_launch(Q, ls, K, ll, V, ll, dO, ls, stats, D, dS, dV, ll, dK, ll, BH, 1, S, L, d, scale, stream);
+}
+
+extern "C" int skp_attn_bwd_flash_bshd(const float* Q, long long q_sb, int q_rs, const float* K, long long k_sb,
+                                       int k_rs, const float* V, long long v_sb, int v_rs, const float* dO,
+                                       long long o_sb, int o_rs, const float* stats, const float* D, float* dS,
+                                       float* dV, long long dv_sb, int dv_rs, float* dK, long long dk_sb, int dk_rs,
+                                       int B, int H, int S, int L, int d, float scale, void* stream) {
+  SKP_CHECK_ARG(B > 0 && H > 0 && (long long)B * H <= 65535, "bad B, H");
+  return attn_bwd_flash_launch(Q, AttnLay{q_sb, q_rs}, K, AttnLay{k_sb, k_rs}, V, AttnLay{v_sb, v_rs}, dO,
+                               AttnLay{o_sb, o_rs}, stats, D, dS, dV, AttnLay{dv_sb, dv_rs}, dK, AttnLay{dk_sb, dk_rs},
+                               B * H, H, S, L, d, scale, stream);
 }

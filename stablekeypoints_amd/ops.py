@@ -934,6 +934,89 @@ def math_attention(q, k, v, scale):
     return MathAttention.apply(q, k, v, float(scale))
 
 
+# --------------------------------------------------------------------------- attention on (B, S, H·d) projections
+# A/B: 0 = permute q / k / v / out between (B, S, H·d) and (B·H, S, d) around the attention kernels (r02)
+ATTN_BSHD = os.environ.get("SKP_ATTN_BSHD", "1") != "0"
+
+
+def _lay(t):
+    """(batch stride, row stride) of a (B, S, H·d) operand whose last dimension is unit-stride."""
+    return int(t.stride(0)), int(t.stride(1))
+
+
+def _bshd_ok(q, k, v, H):
+    B, S, C = q.shape
+    if not ATTN_BSHD or C % H or S % 64 or k.shape[-1] != C or v.shape[-1] != C:
+        return False
+    return all(t.is_cuda and t.dtype == F32 and t.dim() == 3 and t.stride(2) == 1 and t.stride(1) % 4 == 0
+               and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0 for t in (q, k, v))
+
+
+class FlashAttentionBSHD(torch.autograd.Function):
+    """FlashAttention on the projections' own (B, S, H·d) layout: skp_attn_fwd_bshd reads q / k / v
+    and writes the output with head strides (no reshape_heads_to_batch_dim / _to_heads copies, a
+    batch-shared k / v read through a zero batch stride), skp_attn_bwd_flash_bshd reads dO, q, k, v
+    the same way and writes dV, dK per image in (B, L, H·d) (summed over a shared batch by the
+    expand's backward).  dQ = dS·K is one torch.matmul per head (its operands are the only permutes
+    left)."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, H, scale):
+        B, S, C = q.shape
+        L = k.shape[1]
+        d = C // H
+        out = torch.empty(B, S, C, device=q.device, dtype=F32)
+        stats = torch.empty(B * H, S, 2, device=q.device, dtype=F32)
+        call("skp_attn_fwd_bshd", ptr(q), *_lay(q), ptr(k), *_lay(k), ptr(v), *_lay(v), ptr(out), S * C, C, ptr(stats),
+             B, H, S, L, d, float(scale), stream(q.device))
+        ctx.save_for_backward(q, k, v, out, stats)
+        ctx.H, ctx.scale = H, scale
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, k, v, out, stats = ctx.saved_tensors
+        H, scale = ctx.H, ctx.scale
+        dout = _c16(dout)
+        B, S, C = q.shape
+        L = k.shape[1]
+        d = C // H
+        D = (dout.view(B, S, H, d) * out.view(B, S, H, d)).sum(-1).transpose(1, 2).contiguous()   # (B, H, S)
+        ds = torch.empty(B * H, S, L, device=q.device, dtype=F32)
+        dv = torch.empty(B, L, C, device=q.device, dtype=F32)
+        dk = torch.empty(B, L, C, device=q.device, dtype=F32)
+        call("skp_attn_bwd_flash_bshd", ptr(q), *_lay(q), ptr(k), *_lay(k), ptr(v), *_lay(v), ptr(dout), S * C, C,
+             ptr(stats), ptr(D), ptr(ds), ptr(dv), L * C, C, ptr(dk), L * C, C, B, H, S, L, d, float(scale),
+             stream(q.device))
+        dq = None
+        if ctx.needs_input_grad[0]:
+            k4 = k.view(k.shape[0], L, H, d).transpose(1, 2).expand(B, H, L, d)
+            dq = torch.matmul(ds.view(B, H, S, L), k4).transpose(1, 2).reshape(B, S, C)
+        return (dq, dk if ctx.needs_input_grad[1] else None, dv if ctx.needs_input_grad[2] else None, None, None)
+
+
+def attention_heads(q, k, v, H, scale):
+    """softmax(q kᵀ·scale) v per head for (B, S, H·d) q and (B or stride-0 B, L, H·d) k, v, output
+    (B, S, H·d) — diffusers' CrossAttention between to_q/to_k/to_v and to_out without the head
+    permutes.  None when the shape is not covered (the caller keeps the permuting path): the
+    gradient-needing form for head dims in ATTN_FLASH, the no-grad online-softmax form for d ∈
+    {40, 64, 80}, S a multiple of 64."""
+    if not _bshd_ok(q, k, v, H):
+        return None
+    B, S, C = q.shape
+    d = C // H
+    if torch.is_grad_enabled() and (q.requires_grad or k.requires_grad or v.requires_grad):
+        if d not in ATTN_FLASH:
+            return None
+        return FlashAttentionBSHD.apply(q, k, v, int(H), float(scale))
+    if d not in (40, 64, 80):
+        return None
+    out = torch.empty(B, S, C, device=q.device, dtype=F32)
+    call("skp_attn_fwd_bshd", ptr(q), *_lay(q), ptr(k), *_lay(k), ptr(v), *_lay(v), ptr(out), S * C, C, None,
+         B, H, S, k.shape[1], d, float(scale), stream(q.device))
+    return out
+
+
 # --------------------------------------------------------------------------- UNet-side: token projections
 class TokensProjIn(torch.autograd.Function):
     """Transformer2DModel.proj_in (1×1 conv) + NCHW→(B, HW, C') as ONE strided batched GEMM:

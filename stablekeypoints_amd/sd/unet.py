@@ -108,8 +108,18 @@ class CrossAttention(nn.Module):
 
     def forward(self, x, context=None, mask=None):
         context = x if context is None else context
-        q = self.reshape_heads_to_batch_dim(self.to_q(x))
-        k, v = kv_projection(self, context)
+        if mask is None and USE_FUSED_GROUPNORM and x.is_cuda and CrossAttention.backend == "math":
+            from .. import ops   # attention straight on the (B, S, H·d) projections: no head permutes
+            qf = self.to_q(x)
+            kf, vf = kv_projection(self, context)
+            out = ops.attention_heads(qf, kf, vf, self.heads, self.scale)
+            if out is not None:
+                return self.to_out[1](self.to_out[0](out))
+            q = self.reshape_heads_to_batch_dim(qf)
+            k, v = kf, vf
+        else:
+            q = self.reshape_heads_to_batch_dim(self.to_q(x))
+            k, v = kv_projection(self, context)
         k = self.reshape_heads_to_batch_dim(k)
         v = self.reshape_heads_to_batch_dim(v)
         out = attention_core(q, k, v, self.scale, mask, self.heads)
