@@ -65,20 +65,6 @@ __global__ void sel_gather_kernel(const float* __restrict__ z, int BH, int SS, i
   zsel[e] = (t >= 0 && t < N) ? z[bq * N + t] : 0.0f;
 }
 
-// ------------------------------------------------------------------------------ bicubic adjoint matrix
-// A[j][x] = Σ_m [taps(x).i[m] == j]·taps(x).w[m] (m ascending): the weight output index x puts on
-// low-res index j (clamped edge taps add), the same for rows and columns.  Built in LDS, one
-// column per thread.
-__device__ __forceinline__ void build_adj(float* A, int S, int R) {
-  for (int e = threadIdx.x; e < S * R; e += blockDim.x) A[e] = 0.0f;
-  __syncthreads();
-  for (int x = threadIdx.x; x < R; x += blockDim.x) {
-    const Taps4 t = bicubic_taps(x, S, R);
-#pragma unroll
-    for (int m = 0; m < 4; ++m) A[t.i[m] * R + x] += t.w[m];
-  }
-  __syncthreads();
-}
 // output indices whose taps can reach low-res index j: src ∈ [j − 2, j + 2) (clamped edges included)
 __device__ __forceinline__ void adj_range(int j, int S, int R, int& lo, int& hi) {
   const float r = (float)R / (float)S;
@@ -136,30 +122,44 @@ __global__ __launch_bounds__(256) void sel_dot_kernel(const float* __restrict__ 
 }
 
 // ------------------------------------------------------------------------------ sel_adj
-// es[bh][k] = bicubicᵀ(E[bh][k]) (R² → s²), separable, through LDS: A[S][R] (the adjoint matrix,
-// built once), the horizontal pass Hs[y][j] = Σ_x A[j][x]·E[y][x] over 32-row tiles of E staged in
-// LDS, then es[i][j] = Σ_y A[i][y]·Hs[y][j].  Fixed summation order (x, then y ascending).
+// es[bh][k] = bicubicᵀ(E[bh][k]) (R² → s²), separable, through LDS: A[S][R + 1] (the adjoint matrix,
+// built once; rows padded so the lanes' different j hit different banks), the horizontal pass
+// Hs[y][j] = Σ_x A[j][x]·E[y][x] over 32-row tiles of E staged in LDS (rows padded to R + 1; lanes
+// take consecutive rows of the tile, so one wave reads 32 different banks), then
+// es[i][j] = Σ_y A[i][y]·Hs[y][j].  Fixed summation order (x, then y ascending).
 constexpr int SEL_ADJ_TILE = 32;
 __global__ __launch_bounds__(256) void sel_adj_kernel(const float* __restrict__ E, int S, int R,
                                                       float* __restrict__ es) {
   extern __shared__ float sh[];
-  float* A = sh;                 // S × R
-  float* Hs = A + S * R;         // R × S
-  float* Et = Hs + R * S;        // SEL_ADJ_TILE × R
+  const int RP = R + 1;
+  float* A = sh;                 // S × (R + 1)
+  float* Hs = A + S * RP;        // R × S
+  float* Et = Hs + R * S;        // SEL_ADJ_TILE × (R + 1)
   const size_t bk = blockIdx.x;  // bh·K + k
   const float* Eb = E + bk * (size_t)R * R;
-  build_adj(A, S, R);
+  for (int e = threadIdx.x; e < S * RP; e += blockDim.x) A[e] = 0.0f;
+  __syncthreads();
+  for (int x = threadIdx.x; x < R; x += blockDim.x) {
+    const Taps4 t = bicubic_taps(x, S, R);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) A[t.i[m] * RP + x] += t.w[m];
+  }
   for (int y0 = 0; y0 < R; y0 += SEL_ADJ_TILE) {
     const int ny = min(SEL_ADJ_TILE, R - y0);
     const float4* src = reinterpret_cast<const float4*>(Eb + (size_t)y0 * R);
-    for (int e = threadIdx.x; e < ny * R / 4; e += blockDim.x) reinterpret_cast<float4*>(Et)[e] = src[e];
-    __syncthreads();
+    for (int e = threadIdx.x; e < ny * R / 4; e += blockDim.x) {
+      const float4 v = src[e];
+      const int yy = (4 * e) / R, x = 4 * e - yy * R;
+      float* d = Et + yy * RP + x;
+      d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    }
+    __syncthreads();   // (the first pass also publishes A)
     for (int e = threadIdx.x; e < ny * S; e += blockDim.x) {
-      const int yy = e / S, j = e - yy * S;
+      const int yy = e % ny, j = e / ny;   // lanes over rows: distinct banks
       int x0, x1;
       adj_range(j, S, R, x0, x1);
-      const float* Aj = A + j * R;
-      const float* Ey = Et + yy * R;
+      const float* Aj = A + j * RP;
+      const float* Ey = Et + yy * RP;
       float acc = 0.0f;
       for (int x = x0; x <= x1; ++x) acc = fmaf(Aj[x], Ey[x], acc);
       Hs[(y0 + yy) * S + j] = acc;
@@ -170,7 +170,7 @@ __global__ __launch_bounds__(256) void sel_adj_kernel(const float* __restrict__ 
     const int i = e / S, j = e - i * S;
     int y0, y1;
     adj_range(i, S, R, y0, y1);
-    const float* Ai = A + i * R;
+    const float* Ai = A + i * RP;
     float acc = 0.0f;
     for (int y = y0; y <= y1; ++y) acc = fmaf(Ai[y], Hs[y * S + j], acc);
     es[bk * (size_t)S * S + e] = acc;
@@ -511,7 +511,7 @@ extern "C" int skp_capture_maps_bwd_sel(const float* const* z_low, const int* si
                        pix + (size_t)l * BH * RR);
     SKP_LAUNCH_CHECK();
     hipLaunchKernelGGL(sel_adj_kernel, dim3((unsigned)(BH * K)), dim3(256),
-                       (size_t)(2 * S * R + SEL_ADJ_TILE * R) * sizeof(float), st, E, S, R,
+                       (size_t)(S * (R + 1) + R * S + SEL_ADJ_TILE * (R + 1)) * sizeof(float), st, E, S, R,
                        es + (size_t)l * BH * K * smax * smax);
     SKP_LAUNCH_CHECK();
   }

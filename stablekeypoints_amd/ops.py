@@ -999,14 +999,19 @@ def attention_heads(q, k, v, H, scale):
     """softmax(q kᵀ·scale) v per head for (B, S, H·d) q and (B or stride-0 B, L, H·d) k, v, output
     (B, S, H·d) — diffusers' CrossAttention between to_q/to_k/to_v and to_out without the head
     permutes.  None when the shape is not covered (the caller keeps the permuting path): the
-    gradient-needing form for head dims in ATTN_FLASH, the no-grad online-softmax form for d ∈
-    {40, 64, 80}, S a multiple of 64."""
+    gradient-needing form for a batch-shared context and head dims in ATTN_FLASH, the no-grad
+    online-softmax form for d ∈ {40, 64, 80}, S a multiple of 64."""
     if not _bshd_ok(q, k, v, H):
         return None
     B, S, C = q.shape
     d = C // H
     if torch.is_grad_enabled() and (q.requires_grad or k.requires_grad or v.requires_grad):
-        if d not in ATTN_FLASH:
+        # gradient-needing self-attention keeps the head-major copies: both kernels re-read K / V once
+        # per 64-row block, and a head's 160-B rows strided by H·d touch 1.6× the cache lines; at the
+        # 64² shape that costs more than the permutes (measured: 2.05 + 3.85 ms vs 1.85 + 3.38 ms for
+        # the kernels, tools/attn_bshd_time.py); a batch-shared context (cross-attention) is small and
+        # takes this path (0.95 vs 1.00 ms per call)
+        if d not in ATTN_FLASH or k.stride(0) != 0:
             return None
         return FlashAttentionBSHD.apply(q, k, v, int(H), float(scale))
     if d not in (40, 64, 80):

@@ -40,12 +40,14 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("B,H,S,L,d,shared", [
-    (2, 8, 256, 256, 40, False),     # self-attention, the UNet's 64² head dim
+    (2, 8, 256, 256, 40, False),     # self-attention, the UNet's 64² head dim (kernels called directly)
     (2, 8, 192, 77, 40, True),       # cross-attention, batch-shared context, ragged keys
     (3, 4, 128, 128, 64, False),     # SDXL's head dim
     (2, 5, 64, 500, 64, True),       # 500 tokens (the bench's N), shared
 ])
 def test_attention_heads_fwd_bwd_vs_torch(B, H, S, L, d, shared):
+    """The BSHD kernels (FlashAttentionBSHD) for shared and per-image k / v; attention_heads routes
+    only the shared case with gradients through them (see ops.attention_heads)."""
     from stablekeypoints_amd import ops
     g = torch.Generator(device=DEV).manual_seed(S + L + d)
     C = H * d
@@ -67,7 +69,7 @@ def test_attention_heads_fwd_bwd_vs_torch(B, H, S, L, d, shared):
         (out * go).sum().backward()
         return out.detach(), qq.grad, kk.grad, vv.grad
 
-    got = run(lambda a, b, c: ops.attention_heads(a, b, c, H, scale))
+    got = run(lambda a, b, c: ops.FlashAttentionBSHD.apply(a, b, c, H, scale))
     ref = run(lambda a, b, c: _ref(a, b, c, H, scale))
     for name, x, y in zip(("out", "dq", "dk", "dv"), got, ref):
         assert _rel(x, y) < 2e-5, (name, _rel(x, y))
@@ -84,6 +86,9 @@ def test_attention_heads_nograd_and_fallbacks():
         assert ops.attention_heads(q[:, :100], k, v, H, 0.1) is None              # S not a multiple of 64
     qg = q.clone().requires_grad_(True)
     assert ops.attention_heads(qg, k, v, H, 0.1) is None        # d = 80 with grad: the caller's path
+    q40, k40 = (torch.randn(B, S, 320, device=DEV, generator=g) for _ in range(2))
+    assert ops.attention_heads(q40.requires_grad_(True), k40, k40, 8, 0.1) is None   # self-attention with grad
+    assert ops.attention_heads(q40, k40[:1].expand(B, -1, -1), k40[:1].expand(B, -1, -1), 8, 0.1) is not None
 
 
 def test_unet_cross_attention_module_uses_bshd_and_matches_permuting_path(monkeypatch):

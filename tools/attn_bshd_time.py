@@ -43,8 +43,11 @@ def main():
     dev = "cuda:0"
     g = torch.Generator(device=dev).manual_seed(0)
     B, H = 8, 8
+    ap_only = os.environ.get("ATTN_ONLY", "")
     for name, S, L, C, shared in (("64x64 self", 4096, 4096, 320, False), ("64x64 cross", 4096, 500, 320, True),
                                   ("32x32 self", 1024, 1024, 640, False)):
+        if ap_only and ap_only not in name:
+            continue
         d = C // H
         q = torch.randn(B, S, C, device=dev, generator=g).requires_grad_(True)
         k1 = torch.randn(1 if shared else B, L, C, device=dev, generator=g).requires_grad_(True)
@@ -74,8 +77,9 @@ def main():
                 k, v = kv()
                 merge(ops.attention_nograd(heads(q, H), heads(k, H), heads(v, H), scale), H)
             t_ng = (timed(bshd_ng, args.iters), timed(perm_ng, args.iters))
-        res = [timed(bshd, args.iters) if ops.attention_heads(q.detach(), *[t.detach() for t in kv()], H, scale)
-               is not None else float("nan"), timed(perm, args.iters)]
+        k, v = kv()
+        res = [timed(bshd, args.iters) if ops.attention_heads(q, k, v, H, scale) is not None else float("nan"),
+               timed(perm, args.iters)]
         print(f"{name:12s} d={d:3d}  fwd+bwd: bshd {res[0]:8.1f} us  permute {res[1]:8.1f} us   "
               f"no-grad fwd: bshd {t_ng[0]:8.1f} us  permute {t_ng[1]:8.1f} us", flush=True)
 
