@@ -289,6 +289,14 @@ int skp_conv3x3_wino(const float* x, const float* U, const float* bias, const fl
 int skp_wino2_weights(const float* w, int K, int C, int flip, float* U, void* stream);
 int skp_conv3x3_wino2(const float* x, const float* U, const float* bias, const float* residual, float* y, int B,
                       int C, int K, int H, int W, int nsplit, float* ws, void* stream);
+/* diffusers' Downsample2D(padding=0) of the VAE encoder (F.pad(x, (0, 1, 0, 1)) then a 3×3 stride-2
+ * convolution; the encoder behind ptp_utils.image2latent, reference ptp_utils.py:289-304):
+ * y (B, K, H/2, W/2) = the stride-1 pad-1 convolution of x sampled at (2oy + 1, 2ox + 1), + bias,
+ * computed by the skp_conv3x3_wino2 kernel (U from skp_wino2_weights) with a stride-2 epilogue.
+ * H, W multiples of 32; C % 4 == 0, K % 32 == 0; nsplit as skp_conv3x3_wino2 (workspace
+ * nsplit·B·K·(H/2)·(W/2) floats).                                                              */
+int skp_conv3x3s2_wino2(const float* x, const float* U, const float* bias, float* y, int B, int C, int K, int H,
+                        int W, int nsplit, float* ws, void* stream);
 
 #ifdef __cplusplus
 }

@@ -191,7 +191,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
     kb = L - tb * nkb;
   }
   const int c0 = sp * csplit;
-  y += (size_t)sp * nimg * K * H * W;
+  y += (size_t)sp * nimg * K * ((EPI & 4) ? (H / 2) * (W / 2) : H * W);   // EPI bit 2: stride-2 output
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -913,6 +913,26 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
       }
     }
     __syncthreads();
+    if constexpr ((EPI & 4) != 0) {
+      // stride-2 output (EPI bit 2, TXB 8): the block's odd rows / columns, a 16×16 block of the
+      // (H/2, W/2) output per channel = 16 channels × 64 float4, two per thread
+      static_assert(TXB == 8 && (EPI & 2) == 0, "stride-2 output: 32×32 blocks, no residual");
+      const int Ho = H / 2, Wo = W / 2;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int idx = i * w2::kThreads + tid;
+        const int c = idx >> 6, q = idx & 63;
+        const int row = q >> 2, c4 = q & 3;
+        const float* pp = plane_of(c) + (2 * row + 1) * 32 + 8 * c4 + 1;
+        const int k = kb * w2::kNC + 16 * blk + c;
+        const float bv = (EPI & 1) ? bias[k] : 0.0f;
+        const size_t o = (((size_t)img * K + k) * Ho + y0 / 2 + row) * Wo + x0 / 2 + 4 * c4;
+        const float4 v = make_float4(pp[0] + bv, pp[2] + bv, pp[4] + bv, pp[6] + bv);
+        if (!(dbg & 64)) *reinterpret_cast<float4*>(y + o) = v;
+      }
+      if (blk == 0) __syncthreads();
+      continue;
+    }
     // 16 channels × 1024 floats in 16-B chunks; a wave instruction = 1 KB of one channel:
     // TXB 8: 8 whole rows of the 32×32 block; TXB 4: one whole 16×16 image plane
 #pragma unroll
@@ -960,7 +980,7 @@ __global__ __launch_bounds__(w2::kThreads) __attribute__((amdgpu_waves_per_eu(2,
   const int Lg = (G % 8 == 0) ? (g % 8) * (G / 8) + g / 8 : g;
   const int sp = Lg / (nblk * nkb);
   const int L = Lg - sp * (nblk * nkb);
-  y += (size_t)sp * nimg * K * H * W;
+  y += (size_t)sp * nimg * K * ((EPI & 4) ? (H / 2) * (W / 2) : H * W);   // EPI bit 2: stride-2 output
   int tb, kb;
   if (kb_major) {
     kb = L / nblk;
@@ -1025,6 +1045,41 @@ extern "C" int skp_wino2_weights(const float* w, int K, int C, int flip, float* 
   hipLaunchKernelGGL(wino2_weights_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), w, K, C,
                      flip, U);
   SKP_LAUNCH_CHECK();
+  return SKP_OK;
+}
+
+// The VAE's Downsample2D (diffusers: F.pad(x, (0, 1, 0, 1)) then a 3×3 stride-2 convolution; reference
+// ptp_utils.py:289-304 encodes through it): y[oy, ox] taps rows 2oy..2oy+2 and columns 2ox..2ox+2 with a
+// zero row / column past the bottom-right edge, which is exactly the stride-1, pad-1 convolution sampled at
+// the odd positions (2oy + 1, 2ox + 1).  The Winograd kernel computes the 32×32 blocks and its epilogue
+// stores only the odd rows / columns (+ bias): no padded copy, no NCHW↔NHWC transposes, no bias pass.
+extern "C" int skp_conv3x3s2_wino2(const float* x, const float* U, const float* bias, float* y, int B, int C, int K,
+                                   int H, int W, int nsplit, float* ws, void* stream) {
+  SKP_CHECK_ARG(x && U && y, "null pointer");
+  SKP_CHECK_ARG(B > 0 && C > 0 && K > 0 && H > 0 && W > 0, "non-positive shape");
+  SKP_CHECK_ARG(C % w2::kCK == 0, "input channels must be a multiple of 4");
+  SKP_CHECK_ARG(K % w2::kNC == 0, "output channels must be a multiple of 32");
+  SKP_CHECK_ARG(H % 32 == 0 && W % 32 == 0, "H and W must be multiples of 32");
+  SKP_CHECK_ARG(nsplit >= 1 && C % (w2::kCK * nsplit) == 0, "nsplit must divide C into multiples of 4");
+  SKP_CHECK_ARG(nsplit == 1 || ws, "split-K needs a workspace of nsplit·B·K·(H/2)·(W/2) floats");
+  SKP_CHECK_ARG(aligned16(x) && aligned16(U) && aligned16(y) && (!ws || aligned16(ws)), "tensors must be 16-byte aligned");
+  SKP_CHECK_ARG((long long)B * C * H * W * 4 < 0x7fffffffLL, "input larger than 2 GiB (32-bit buffer offsets)");
+  const int bw = W / 32, bpi = (H / 32) * bw;
+  const long long nblk = (long long)B * bpi;
+  const int nkb = K / w2::kNC;
+  SKP_CHECK_ARG(nblk * nkb * nsplit <= 0x7fffffffLL, "grid too large");
+  static const int dbg = getenv("SKP_WINO2_DEBUG") ? atoi(getenv("SKP_WINO2_DEBUG")) : 0;
+  float* out = nsplit > 1 ? ws : y;
+  hipStream_t st = as_stream(stream);
+  const dim3 grid((unsigned)(nblk * nkb * nsplit));
+  if (nsplit == 1 && bias)
+    hipLaunchKernelGGL((wino2_kernel<5, 8>), grid, dim3(w2::kThreads), 0, st, x, U, bias, nullptr, out, B, C, K, H, W,
+                       bw, bpi, (int)nblk, nkb, 0, C / nsplit, dbg);
+  else
+    hipLaunchKernelGGL((wino2_kernel<4, 8>), grid, dim3(w2::kThreads), 0, st, x, U, nullptr, nullptr, out, B, C, K, H,
+                       W, bw, bpi, (int)nblk, nkb, 0, C / nsplit, dbg);
+  SKP_LAUNCH_CHECK();
+  if (nsplit > 1) return splitk_reduce(ws, nsplit, B, K, (H / 2) * (W / 2), bias, nullptr, y, st);
   return SKP_OK;
 }
 

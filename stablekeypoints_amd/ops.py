@@ -1212,6 +1212,82 @@ class Conv3x3(torch.autograd.Function):
         return dx, None, None, (dy if ctx.has_res else None)
 
 
+class Conv1x1(torch.autograd.Function):
+    """y[b] = W x[b] for a frozen 1×1 convolution (K, C) on NCHW x viewed as (B, C, H·W): ONE strided
+    batched GEMM with the weight broadcast over the batch (zero batch stride), straight between NCHW
+    tensors — no NCHW↔NHWC transposes around a MIOpen 1×1 kernel; dx[b] = Wᵀ dy[b] the same way."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        B, C, H, W = x.shape
+        K = w.shape[0]
+        y = torch.bmm(w.expand(B, K, C), x.reshape(B, C, H * W))
+        ctx.save_for_backward(w)
+        ctx.shape = (B, C, H, W)
+        return y.view(B, K, H, W)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (w,) = ctx.saved_tensors
+        B, C, H, W = ctx.shape
+        K = w.shape[0]
+        dx = torch.bmm(w.t().expand(B, C, K), dy.reshape(B, K, H * W)) if ctx.needs_input_grad[0] else None
+        return (None if dx is None else dx.view(B, C, H, W)), None
+
+
+# A/B: 0 = the resnets' 1×1 shortcut convolutions run on MIOpen (r02)
+CONV1X1_GEMM = os.environ.get("SKP_CONV1X1_GEMM", "1") != "0"
+
+
+def conv1x1(x, weight):
+    """Bias-free 1×1 convolution of NCHW fp32 x with a frozen weight (K, C, 1, 1) (the caller folds
+    the bias into the next epilogue): Conv1x1's batched GEMM, or F.conv2d with CONV1X1_GEMM off."""
+    _lib.require_device(x)
+    if weight.requires_grad:
+        raise ValueError("conv1x1: the weight must be frozen (requires_grad=False)")
+    if not CONV1X1_GEMM or x.dtype != F32:
+        return torch.nn.functional.conv2d(x, weight)
+    return Conv1x1.apply(_c(x), weight.detach().reshape(weight.shape[0], weight.shape[1]))
+
+
+# A/B: 0 = the VAE's stride-2 downsampling convolutions run as F.pad + MIOpen (r02)
+WINO_S2 = os.environ.get("SKP_WINO_S2", "1") != "0"
+
+
+def conv3x3_s2_eligible(x, weight):
+    B, C, H, W = x.shape
+    K = weight.shape[0]
+    return (WINO_S2 and x.is_cuda and x.dtype == F32 and tuple(weight.shape[1:]) == (C, 3, 3) and C % 4 == 0
+            and K % 32 == 0 and H % 32 == 0 and W % 32 == 0 and not weight.requires_grad
+            and not (torch.is_grad_enabled() and x.requires_grad))
+
+
+def conv3x3_s2(x, weight, bias=None):
+    """diffusers' Downsample2D(padding=0) — F.pad(x, (0, 1, 0, 1)) then a 3×3 / stride-2 conv2d —
+    forward only (the frozen VAE encoder runs without gradient): skp_conv3x3s2_wino2, the stride-1
+    pad-1 Winograd convolution sampled at the odd rows / columns (the same taps, the same zero
+    row / column past the bottom-right edge) with the bias in its epilogue.  (B, C, H, W) →
+    (B, K, H/2, W/2)."""
+    _lib.require_device(x)
+    if not conv3x3_s2_eligible(x, weight):
+        raise ValueError(f"conv3x3_s2: unsupported x {tuple(x.shape)} / weight {tuple(weight.shape)}")
+    x = _c16(x)
+    B, C, H, W = x.shape
+    K = weight.shape[0]
+    y = torch.empty(B, K, H // 2, W // 2, device=x.device, dtype=F32)
+    U = _wino_u(weight, False, True)
+    b = None if bias is None else _c(bias.detach())
+    bmax = max(1, (2 ** 31 - 1) // (C * H * W * 4))   # 32-bit buffer offsets into x
+    for b0 in range(0, B, bmax):
+        b1 = min(B, b0 + bmax)
+        _, nsplit, _ = _wino_plan(b1 - b0, C, K, H, W)
+        ws = torch.empty(nsplit, b1 - b0, K, H // 2, W // 2, device=x.device, dtype=F32) if nsplit > 1 else None
+        with _timed("skp_conv3x3s2_wino2", 0):
+            call("skp_conv3x3s2_wino2", ptr(x[b0:b1]), ptr(U), ptr(b), ptr(y[b0:b1]), b1 - b0, C, K, H, W, nsplit,
+                 ptr(ws), stream(x.device))
+    return y
+
+
 def conv3x3(x, weight, bias=None, residual=None):
     """3×3 / stride 1 / pad 1 convolution (+ bias, + residual) of NCHW fp32 ``x`` with a frozen
     ``weight`` (K, C, 3, 3): the Winograd F(4×4, 3×3) kernel when the shape is eligible, else

@@ -269,9 +269,15 @@ class ResnetBlock2D(nn.Module):
             shift = self.conv1.bias[None]
             if temb is not None and self.time_emb_proj is not None:
                 shift = shift + self.time_emb_proj(F.silu(temb))
+            bias = self.conv2.bias
             if self.conv_shortcut is not None:
-                x = self.conv_shortcut(x)
-            return ops.conv3x3(self.dropout(gn_act(self.norm2, h, True, shift)), self.conv2.weight, self.conv2.bias, x)
+                if _fused(x, self.conv_shortcut):
+                    # the shortcut as one batched GEMM on NCHW; its bias joins conv2's in the epilogue
+                    x = ops.conv1x1(x, self.conv_shortcut.weight)
+                    bias = bias + self.conv_shortcut.bias
+                else:
+                    x = self.conv_shortcut(x)
+            return ops.conv3x3(self.dropout(gn_act(self.norm2, h, True, shift)), self.conv2.weight, bias, x)
         h = self.conv1(gn_act(self.norm1, x, True))
         if temb is not None and self.time_emb_proj is not None:
             h = h + self.time_emb_proj(F.silu(temb))[:, :, None, None]
@@ -288,6 +294,10 @@ class Downsample2D(nn.Module):
         self.conv = nn.Conv2d(channels, channels, 3, stride=2, padding=padding)
 
     def forward(self, x):
+        if self.padding == 0 and _fused(x, self.conv):
+            from .. import ops
+            if ops.conv3x3_s2_eligible(x, self.conv.weight):   # no padded copy, no MIOpen glue
+                return ops.conv3x3_s2(x, self.conv.weight, self.conv.bias)
         if self.padding == 0:
             # F.pad(x, (0, 1, 0, 1)) without F.pad's zero fill of the whole output (the VAE's
             # 512² / 256² levels: a 1 GB fill per step): copy x, zero only the new row and column

@@ -238,3 +238,87 @@ def test_sd_models_winograd_vs_miopen(monkeypatch):
         outs.append((z, out.detach(), ctx.grad.detach()))
     for a, b in zip(outs[0], outs[1]):
         assert _rel(b, a.double()) < 1e-4
+
+
+@pytest.mark.parametrize("B,C,K,H,W,bias,nsplit", [(2, 64, 64, 64, 64, True, 0), (1, 32, 96, 32, 96, True, 0),
+                                                   (3, 8, 32, 32, 32, False, 0), (2, 128, 64, 64, 32, True, 4),
+                                                   (1, 256, 32, 32, 32, True, 8)])
+def test_conv3x3_stride2_downsample_vs_fp64(all_shapes, monkeypatch, B, C, K, H, W, bias, nsplit):
+    """ops.conv3x3_s2 (skp_conv3x3s2_wino2: the Winograd kernel with the stride-2 epilogue) vs the
+    reference's Downsample2D(padding=0) in fp64: F.pad(x, (0, 1, 0, 1)) then conv2d(stride=2);
+    with and without bias, unsplit and split-K (the sums reduced by splitk_reduce)."""
+    ops = all_shapes
+    if nsplit:
+        monkeypatch.setenv("SKP_WINO_NSPLIT", str(nsplit))
+    g = torch.Generator().manual_seed(B * 1000 + C + K + H)
+    x = torch.randn(B, C, H, W, generator=g)
+    w = torch.randn(K, C, 3, 3, generator=g) / (3 * C ** 0.5)
+    b = torch.randn(K, generator=g) if bias else None
+    ref = F.conv2d(F.pad(x.double(), (0, 1, 0, 1)), w.double(), None if b is None else b.double(), stride=2)
+    with torch.no_grad():
+        y = ops.conv3x3_s2(x.to(DEV), w.to(DEV), None if b is None else b.to(DEV))
+    assert y.shape == ref.shape
+    assert _rel(y.cpu(), ref) < 3e-5
+
+
+def test_vae_downsample_uses_stride2_winograd_and_matches_miopen(monkeypatch):
+    """The VAE's Downsample2D takes the stride-2 Winograd path under no_grad and equals the
+    F.pad + MIOpen path (the SKP_WINO_S2=0 form) at 128 channels, batch 2."""
+    from stablekeypoints_amd import ops
+    from stablekeypoints_amd.sd.unet import Downsample2D
+    torch.manual_seed(0)
+    m = Downsample2D(128, padding=0).to(DEV)
+    for p in m.parameters():
+        p.requires_grad_(False)
+    x = torch.randn(2, 128, 128, 96, device=DEV)
+    calls = []
+    real = ops.conv3x3_s2
+    monkeypatch.setattr(ops, "conv3x3_s2", lambda *a: calls.append(1) or real(*a))
+    with torch.no_grad():
+        y = m(x)
+        assert calls, "Downsample2D did not take the stride-2 Winograd path"
+        monkeypatch.setattr(ops, "WINO_S2", False)
+        y2 = m(x)
+    assert y.shape == (2, 128, 64, 48)
+    assert ((y - y2).abs().max() / y2.abs().max()).item() < 3e-5
+
+
+@pytest.mark.parametrize("B,C,K,H,W", [(2, 320, 640, 16, 16), (3, 96, 32, 8, 12), (1, 2560, 1280, 8, 8)])
+def test_conv1x1_gemm_vs_fp64(B, C, K, H, W):
+    """ops.conv1x1 (one batched GEMM on NCHW, the resnets' shortcut) vs conv2d in fp64: output and
+    input gradient."""
+    from stablekeypoints_amd import ops
+    g = torch.Generator().manual_seed(C + K + H)
+    x = torch.randn(B, C, H, W, generator=g)
+    w = torch.randn(K, C, 1, 1, generator=g) / C ** 0.5
+    dy = torch.randn(B, K, H, W, generator=g)
+    x64 = x.double().requires_grad_(True)
+    ref = F.conv2d(x64, w.double())
+    ref.backward(dy.double())
+    xd = x.to(DEV).requires_grad_(True)
+    y = ops.conv1x1(xd, w.to(DEV))
+    y.backward(dy.to(DEV))
+    assert _rel(y.detach().cpu(), ref.detach()) < 1e-5
+    assert _rel(xd.grad.cpu(), x64.grad) < 1e-5
+
+
+def test_resnet_block_shortcut_gemm_matches_miopen_form(monkeypatch):
+    """ResnetBlock2D with a 1×1 shortcut: the fused form (shortcut GEMM, its bias folded into conv2's
+    epilogue) equals the MIOpen shortcut form (SKP_CONV1X1_GEMM=0), forward and input gradient."""
+    from stablekeypoints_amd import ops
+    from stablekeypoints_amd.sd.unet import ResnetBlock2D
+    torch.manual_seed(1)
+    m = ResnetBlock2D(64, 128, temb_channels=256).to(DEV)
+    for p in m.parameters():
+        p.requires_grad_(False)
+    x = torch.randn(4, 64, 32, 32, device=DEV, requires_grad=True)
+    temb = torch.randn(4, 256, device=DEV)
+    y = m(x, temb)
+    y.square().sum().backward()
+    gx = x.grad.clone()
+    x.grad = None
+    monkeypatch.setattr(ops, "CONV1X1_GEMM", False)
+    y2 = m(x, temb)
+    y2.square().sum().backward()
+    assert ((y - y2).abs().max() / y2.abs().max()).item() < 3e-5
+    assert ((gx - x.grad).abs().max() / x.grad.abs().max()).item() < 3e-5

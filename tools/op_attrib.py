@@ -55,6 +55,17 @@ def caller(e):
     return "?"
 
 
+# stack-grouped table of the copy-like ops (the Python call sites of every strided copy / memcpy)
+ka = prof.key_averages(group_by_stack_n=6)
+rows_s = [k for k in ka if any(n in k.key for n in ("copy_", "clone", "contiguous", "cat", "_to_copy", "fill_", "add"))]
+rows_s.sort(key=lambda k: -(getattr(k, "self_device_time_total", 0) or 0))
+print("--- copy-like ops by Python stack (self device time)")
+for k in rows_s[:40]:
+    t = getattr(k, "self_device_time_total", 0) or 0
+    if t <= 0:
+        continue
+    st = [f for f in (k.stack or []) if "torch/" not in f][:4]
+    print(f"{t / 1e3:8.3f} ms {k.count:4d} {k.key:24s} {str(k.input_shapes)[:70]:70s} | " + " <- ".join(st))
 match = [m for m in args.match.split(",") if m]
 rows = {}
 total = 0.0
