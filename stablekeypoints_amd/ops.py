@@ -1235,8 +1235,11 @@ class Conv1x1(torch.autograd.Function):
         return (None if dx is None else dx.view(B, C, H, W)), None
 
 
-# A/B: 0 = the resnets' 1×1 shortcut convolutions run on MIOpen (r02)
-CONV1X1_GEMM = os.environ.get("SKP_CONV1X1_GEMM", "1") != "0"
+# A/B (default off): 1 = the resnets' 1×1 shortcuts as Conv1x1's batched GEMM.  Measured at the
+# bench's shortcut shapes (tools/conv1x1_time.py, batch 8, fwd + input grad): within ±3% of MIOpen's
+# 1×1 kernels at 8², 16² and 32² (2560→1280 @16²: 274 vs 272 us; 960→640 @32²: 186 vs 201 us;
+# 1280→640 @32²: 290 vs 249 us), the VAE's 128→256 @256² 318 vs 343 us — no net gain, so MIOpen stays
+CONV1X1_GEMM = os.environ.get("SKP_CONV1X1_GEMM", "0") == "1"
 
 
 def conv1x1(x, weight):
@@ -1252,14 +1255,18 @@ def conv1x1(x, weight):
 
 # A/B: 0 = the VAE's stride-2 downsampling convolutions run as F.pad + MIOpen (r02)
 WINO_S2 = os.environ.get("SKP_WINO_S2", "1") != "0"
+WINO_S2_MIN_PIXELS = 384 * 384
 
 
 def conv3x3_s2_eligible(x, weight):
     B, C, H, W = x.shape
     K = weight.shape[0]
+    # measured at batch 8 (tools/conv_s2_time.py): 512² × 128 ch 2.21 vs 2.75 ms for pad + MIOpen; at
+    # 256² × 256 (1.89 vs 1.85) and 128² × 512 (1.81 vs 1.53) MIOpen's implicit GEMM is as fast or
+    # faster than the 4×-redundant Winograd blocks, so only the large-image levels take this path
     return (WINO_S2 and x.is_cuda and x.dtype == F32 and tuple(weight.shape[1:]) == (C, 3, 3) and C % 4 == 0
-            and K % 32 == 0 and H % 32 == 0 and W % 32 == 0 and not weight.requires_grad
-            and not (torch.is_grad_enabled() and x.requires_grad))
+            and K % 32 == 0 and H % 32 == 0 and W % 32 == 0 and H * W >= WINO_S2_MIN_PIXELS
+            and not weight.requires_grad and not (torch.is_grad_enabled() and x.requires_grad))
 
 
 def conv3x3_s2(x, weight, bias=None):
