@@ -13,6 +13,14 @@ import torch
 from . import ops
 
 
+def _upload(t, device):
+    """Host θ to the device without blocking the host (pinned staging, async copy); a pageable
+    copy waits for everything queued on the stream."""
+    if t.device.type != "cpu" or torch.device(device).type == "cpu":
+        return t.to(device)
+    return t.pin_memory().to(device, non_blocking=True)
+
+
 class RandomAffineWithInverse:
     def __init__(self, degrees=0, scale=(1.0, 1.0), translate=(0.0, 0.0)):
         self.degrees = degrees
@@ -45,7 +53,7 @@ class RandomAffineWithInverse:
         if theta is None:
             theta = self.draw_theta(img_tensor.shape[0])
         self.last_params = {"theta": theta.detach().cpu().float()}
-        return ops.affine_warp(img_tensor, theta.to(img_tensor.device, torch.float32))
+        return ops.affine_warp(img_tensor, _upload(theta.float(), img_tensor.device))
 
     def theta_inverse(self):
         """2×3 part of the 3×3 inverse of each stored theta (invertable_transform.py:77-84)."""
@@ -59,4 +67,4 @@ class RandomAffineWithInverse:
         th = self.theta_inverse()
         if th.shape[0] != img_tensor.shape[0]:
             raise ValueError(f"inverse: {img_tensor.shape[0]} images but {th.shape[0]} stored thetas")
-        return ops.affine_warp(img_tensor, th.to(img_tensor.device))
+        return ops.affine_warp(img_tensor, _upload(th, img_tensor.device))

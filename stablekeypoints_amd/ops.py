@@ -1118,7 +1118,7 @@ def _wino_u(weight, flip, v2=False):
     return U
 
 
-def _wino_plan(B, C, K, H, W):
+def _wino_plan_uncached(B, C, K, H, W, force):
     """(v2, nsplit, workgroups) for a (B, C, H, W) → (B, K, H, W) convolution.
 
     One workgroup per CU (their LDS), so a grid runs in ceil(workgroups / 256) rounds of
@@ -1143,10 +1143,23 @@ def _wino_plan(B, C, K, H, W):
     if WINO_SPLIT:
         cands = [s for s in range(1, 33) if C % (4 * s) == 0 and (s == 1 or C // s >= 32)]
         nsplit = min(cands, key=cost)
-        force = int(os.environ.get("SKP_WINO_NSPLIT", "0"))   # dev: measure a given split
-        if force and C % (4 * force) == 0:
+        if force and C % (4 * force) == 0:   # dev: SKP_WINO_NSPLIT measures a given split
             nsplit = force
     return v2, nsplit, wgs * nsplit
+
+
+_WINO_PLANS = {}
+
+
+def _wino_plan(B, C, K, H, W):
+    """_wino_plan_uncached, memoised per shape (and the module switches it reads): the planner's
+    32-candidate cost loop ran in Python on every convolution call, ~1500 launches per step."""
+    force = int(os.environ.get("SKP_WINO_NSPLIT", "0"))
+    key = (B, C, K, H, W, force, WINO_KERNEL, WINO_SPLIT, WINO_WIDE)
+    plan = _WINO_PLANS.get(key)
+    if plan is None:
+        plan = _WINO_PLANS[key] = _wino_plan_uncached(B, C, K, H, W, force)
+    return plan
 
 
 def wino_eligible(B, C, K, H, W, min_workgroups=None):

@@ -18,6 +18,14 @@ from . import eval as skp_eval
 from .invertable_transform import RandomAffineWithInverse
 
 
+def _upload(t, device):
+    """A small host tensor to the device without blocking the host: pinned staging + an async copy
+    (a pageable copy is hipMemcpyWithStream, which waits for everything queued on the stream)."""
+    if t.device.type != "cpu" or torch.device(device).type == "cpu":
+        return t.to(device)
+    return t.pin_memory().to(device, non_blocking=True)
+
+
 def collect_maps(controller, from_where=("up_cross",), upsample_res=512, layers=(0, 1, 2, 3), indices=None):
     """optimize.py:27-79: mean over the selected stored layers and B·heads -> (N', R', R').
 
@@ -156,7 +164,7 @@ class TokenOptimizer:
         self._side.wait_stream(main)
         with torch.cuda.stream(self._side), torch.no_grad():
             batch.record_stream(self._side)
-            transformed = ops.affine_warp(batch, thetas.to(self.device, torch.float32))
+            transformed = ops.affine_warp(batch, _upload(thetas.float(), self.device))
             lat = ptp_utils.image2latent(self.ldm, torch.cat([batch, transformed]), self.device)
             ev = torch.cuda.Event()
             ev.record(self._side)
@@ -249,7 +257,7 @@ class TokenOptimizer:
             self.ldm, inputs, self.context, noise_level=self.kw["noise_level"], device=self.device,
             layers=self.kw["layers"], controllers=self.controllers, stacked=True, captured=sparse)[0]
         maps = got.maps if sparse else got        # (2k, N, R, R); the selection needs no gradient
-        th_inv = self.transform.theta_inverse().to(self.device)   # all k warps, one upload
+        th_inv = _upload(self.transform.theta_inverse(), self.device)   # all k warps, one upload
         sel = [self._select(maps[i], maps[k + i]) for i in range(k)]
         if sparse:
             # every image's selected rows in ONE gather whose backward is the sparse capture backward

@@ -274,6 +274,10 @@ def find_pred_noise(ldm, image, context, noise_level=-1, device="cuda"):
         latent = image2latent(ldm, image, device)
     noise = torch.randn_like(latent)
     t = ldm.scheduler.timesteps[noise_level]
+    if t.device != latent.device:
+        # the timestep made on the device (a fill), not uploaded: a pageable host-to-device copy
+        # waits for the whole queued stream and stalls the host at every capture
+        t = torch.full((), int(t), dtype=t.dtype, device=latent.device)
     noisy_image = ldm.scheduler.add_noise(latent, noise, t)
     try:
         # the reference repeats the context per image; a stride-0 expansion is the same tensor

@@ -27,8 +27,18 @@ class DDIMScheduler:
         ts = (np.arange(0, num_inference_steps) * ratio).round()[::-1].copy().astype(np.int64)
         self.timesteps = torch.from_numpy(ts + self.steps_offset)
 
+    def _alphas_cumprod_on(self, device, dtype):
+        """alphas_cumprod on the samples' device, uploaded once: a pageable host-to-device copy per
+        call waits for everything queued on the stream (hipMemcpyWithStream), which stalled the host
+        — and with it the GPU queue — at every capture."""
+        cache = self.__dict__.setdefault("_ac_cache", {})
+        key = (str(device), dtype)
+        if key not in cache:
+            cache[key] = self.alphas_cumprod.to(device=device, dtype=dtype)
+        return cache[key]
+
     def add_noise(self, original_samples, noise, timesteps):
-        ac = self.alphas_cumprod.to(device=original_samples.device, dtype=original_samples.dtype)
+        ac = self._alphas_cumprod_on(original_samples.device, original_samples.dtype)
         timesteps = timesteps.to(original_samples.device)
         sqrt_a = ac[timesteps] ** 0.5
         sqrt_1ma = (1 - ac[timesteps]) ** 0.5

@@ -55,6 +55,24 @@ def main():
         agg[r["Kernel_Name"]][0] += 1
         agg[r["Kernel_Name"]][1] += d
     total = sum(v[1] for v in agg.values())
+    # per stream: kernel busy time and the union of its kernels' intervals (the critical path is
+    # the main stream; the VAE prefetch runs on a side stream)
+    by_stream = collections.defaultdict(list)
+    for r in sel:
+        by_stream[r.get("Stream_Id", "0")].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+    for sid, iv in sorted(by_stream.items()):
+        iv.sort()
+        union, cur = 0, None
+        for a, b in iv:
+            if cur is None or a > cur[1]:
+                if cur:
+                    union += cur[1] - cur[0]
+                cur = [a, b]
+            else:
+                cur[1] = max(cur[1], b)
+        union += cur[1] - cur[0]
+        busy = sum(b - a for a, b in iv)
+        print(f"stream {sid}: {len(iv)} dispatches, kernel busy {busy / 1e6:.1f} ms, covered {union / 1e6:.1f} ms")
     items = sorted(agg.items(), key=lambda kv: -kv[1][1])
     print(f"timed region: {len(sel)} dispatches, span {(t1 - t0) / 1e6:.1f} ms, kernel busy {total / 1e6:.1f} ms, "
           f"{args.micro} micro-iterations -> {total / 1e6 / args.micro:.2f} ms kernel time per image")
