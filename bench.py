@@ -373,12 +373,11 @@ def main():
                     help="un-captured UNet attention: explicit fp32 GEMM+softmax (math) or torch SDPA")
     ap.add_argument("--micro-batch", type=int, default=0,
                     help="images per VAE/UNet pass (0 = all `accum` images of an optimiser step in one pass)")
-    ap.add_argument("--prefetch", type=int, default=2,
+    ap.add_argument("--prefetch", type=int, default=1,
                     help="VAE-encode the next PREFETCH passes' images on a side stream (TokenOptimizer.prefetch), "
-                         "so a pass never waits for its latents (depth 1 left a ~10 ms wait per step: the VAE "
-                         "shares the GPU with the UNet pass it overlaps); steady state: every timed step runs one "
-                         "UNet pass and one VAE pass, the warm-up's prefetches are balanced by the last timed "
-                         "steps' (0 = no prefetch)")
+                         "enqueued between the current pass's forward and backward; steady state: every timed step "
+                         "runs one UNet pass and one VAE pass, the warm-up's prefetches are balanced by the last "
+                         "timed steps' (0 = no prefetch)")
     ap.add_argument("--gc-freeze", type=int, default=1, help="gc.freeze() after the model is built (host overhead)")
     ap.add_argument("--stage", default="token_opt", choices=["token_opt", "find_indices", "tta"],
                     help="token_opt = the headline token-optimisation step; find_indices = "
@@ -452,14 +451,12 @@ def main():
         while done < args.accum:
             n = min(mb, args.accum - done)
             cur = batch_at(counter[0], n)
+            ahead = []
             if args.prefetch:
                 opt.prefetch(cur)                                   # no-op when already prefetched
-            opt.micro_steps(cur)
-            if args.prefetch:
-                # the next passes' VAE, enqueued behind this pass's backward: the side stream's queue
-                # then never holds the host while the main stream runs dry
-                for d in range(1, args.prefetch + 1):
-                    opt.prefetch(batch_at(counter[0] + d * n, min(mb, args.accum)))
+                ahead = [batch_at(counter[0] + d * n, min(mb, args.accum)) for d in range(1, args.prefetch + 1)]
+            # the next passes' VAE is enqueued between this pass's forward and backward
+            opt.micro_steps(cur, prefetch=ahead)
             counter[0] += n
             done += n
         return opt.optimizer_step()

@@ -230,7 +230,7 @@ class TokenOptimizer:
         self.run_sh = self.run_sh + sh.detach() / self.accum * self.w_sharp
         self.run_tot = self.run_tot + loss.detach() / self.accum
 
-    def micro_steps(self, images):
+    def micro_steps(self, images, prefetch=()):
         """``len(images)`` reference micro-iterations in ONE VAE/UNet pass of batch 2·k (every
         image and its warp) and ONE backward.
 
@@ -240,6 +240,10 @@ class TokenOptimizer:
         generator, and the selection and losses stay per image.  A batch of 2·k images fills
         the 256 CUs far better than k passes of 2 (the UNet's 64²-and-smaller convolutions and
         GEMMs are too small at batch 2).  Returns the per-image selected token indices.
+        ``prefetch``: image batches whose VAE encoding (``prefetch``) is enqueued on the side stream
+        between this pass's forward and its backward — the host issues those ~130 launches while
+        the main stream still works through the queued forward; issued after the backward they
+        left the main stream idle before Adam (≈7 ms per step, tools/stream_gaps.py).
         """
         if not self.batch_captures or len(images) == 1:
             return [self.micro_step(img) for img in images]
@@ -279,6 +283,8 @@ class TokenOptimizer:
             off += n
             self._account(loss, eq, sh)
             total = total + loss
+        for b in prefetch:
+            self.prefetch(b)
         (total / self.accum).backward()
         return sel
 

@@ -36,7 +36,7 @@ def batch(k):
     return [imgs[(k + i) % 16] for i in range(4)]
 
 
-ORDER = os.environ.get("HOST_ORDER", "after")
+ORDER = os.environ.get("HOST_ORDER", "mid")
 
 
 def step():
@@ -46,7 +46,8 @@ def step():
         for d in range(1, args.prefetch + 1):
             opt.prefetch(batch(c[0] + 4 * d))
     t.append(time.perf_counter())
-    opt.micro_steps(batch(c[0]))
+    opt.micro_steps(batch(c[0]), prefetch=[batch(c[0] + 4 * d) for d in range(1, args.prefetch + 1)]
+                    if ORDER == "mid" else ())
     t.append(time.perf_counter())
     if ORDER == "after":
         for d in range(1, args.prefetch + 1):
