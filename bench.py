@@ -378,6 +378,11 @@ def main():
                          "enqueued between the current pass's forward and backward; steady state: every timed step "
                          "runs one UNet pass and one VAE pass, the warm-up's prefetches are balanced by the last "
                          "timed steps' (0 = no prefetch)")
+    ap.add_argument("--graph", type=int, default=0,
+                    help="1 = replay each pass (capture forward, selection, losses, backward into the embedding) as "
+                         "one captured HIP graph (TokenOptimizer(graph=True)); measured neutral at the bench shape "
+                         "(39.47 vs 39.50 images/s, profiles/r03t_graph_ab.txt: the GPU, not the host, is the bound), "
+                         "so eager launches stay the default")
     ap.add_argument("--gc-freeze", type=int, default=1, help="gc.freeze() after the model is built (host overhead)")
     ap.add_argument("--stage", default="token_opt", choices=["token_opt", "find_indices", "tta"],
                     help="token_opt = the headline token-optimisation step; find_indices = "
@@ -432,7 +437,7 @@ def main():
     if args.stage != "token_opt":
         return stage_main(args, ldm, controllers, context.detach(), dev, world, rank, backend)
     torch.manual_seed(1234 + rank)
-    opt = TokenOptimizer(ldm, controllers, context, accum=args.accum, device=dev)
+    opt = TokenOptimizer(ldm, controllers, context, accum=args.accum, device=dev, graph=bool(args.graph))
     data = SyntheticDataset(n=16, size=args.res, seed=rank)
     imgs = [data[i]["img"][None].to(dev) for i in range(len(data))]
     timer = KernelTimer(["skp_aggregate", "skp_capture_fwd", "skp_capture_bwd", "skp_capture_maps_fwd",
@@ -485,6 +490,19 @@ def main():
         elapsed = float(t.item())
     images = world * args.accum * args.steps
     value = images / elapsed
+    timing_src = ("HIP events around every launch in the timed region, on the launching stream "
+                  "(bench.py KernelTimer)")
+    if args.graph:
+        # the timed steps replay a HIP graph, which runs no Python and so records no per-kernel
+        # events: the same pass runs once eagerly after the timed region (same shapes, same
+        # kernels) with the events around every libskp launch
+        opt.graph = False
+        timer.enabled = True
+        step()
+        torch.cuda.synchronize()
+        timer.enabled = False
+        timing_src = ("HIP events around every launch of one eager pass run after the timed region (the timed "
+                      "steps replay a HIP graph of the same kernels), on the launching stream (bench.py KernelTimer)")
 
     # roofline: the dominant hot-path kernel, skp_capture_maps_fwd (fused capture + per-image
     # aggregate), is VALU-bound (bicubic taps + exp + normalise per (pixel, token, layer, head));
@@ -494,8 +512,6 @@ def main():
     extra = {}
     fw = timer.summary("skp_capture_maps_fwd")
     valu_json = os.path.join(REPO, "profiles", "pmc_valu.json")
-    timing_src = ("HIP events around every launch in the timed region, on the launching stream "
-                  "(bench.py KernelTimer)")
     if fw:
         flops = fw["flop_per_launch"]   # ops.capture_maps_flops of the launch's (B, H, N, R, sizes)
         t = fw["avg_ms"] * 1e-3
@@ -576,7 +592,8 @@ def main():
                           "feature_upsample_res": args.upsample_res, "micro_batch": mb,
                           "parallelism": (f"dp{world} ({'RCCL' if backend == 'nccl' else backend} all-reduce of the "
                                           "token-embedding gradient)" if world > 1 else "dp1 (single process, no collective)"),
-                          "tuned_gemms": _tuned_gemms_in_use()},
+                          "tuned_gemms": _tuned_gemms_in_use(), "hip_graph": bool(args.graph),
+                          "vae_prefetch": args.prefetch},
                "roofline": roof, "cpu_baseline": cpu, "kernels": extra,
                "last_loss": float(rec["loss"])}
         print(json.dumps(out), flush=True)

@@ -110,8 +110,14 @@ class TokenOptimizer:
                  furthest_point_num_samples=25, sigma=2.0, num_subjects=1, sharpening_loss_weight=100,
                  equivariance_attn_loss_weight=1000.0, accum=4, noise_level=-1, layers=(0, 1, 2, 3),
                  from_where=("down_cross", "mid_cross", "up_cross"), augment_degrees=15, augment_scale=(0.8, 1.0),
-                 augment_translate=(0.25, 0.25), device="cuda", batch_captures=True):
+                 augment_translate=(0.25, 0.25), device="cuda", batch_captures=True, graph=False):
         self.ldm, self.controllers, self.device = ldm, controllers, device
+        # graph: replay the prefetched-latents pass (capture forward, selection, losses, backward)
+        # as ONE HIP graph (micro_steps); the host then issues one launch per pass instead of ~1500
+        self.graph = graph
+        self._g = None           # (key, HIPGraph, static inputs, static outputs) once captured
+        self._grad_acc = None
+        self._gstream = None
         # batch_captures: run each image with its warp in one VAE/UNet pass (micro_steps: all
         # of an optimiser step's images in one pass)
         # (run_and_find_attn_per_image); False = the reference's two sequential passes.
@@ -249,6 +255,10 @@ class TokenOptimizer:
             return [self.micro_step(img) for img in images]
         k = len(images)
         pre = self._take_prefetched(images)
+        if pre is not None and self.graph and ops.SEL_BWD:
+            thetas, inputs = pre
+            self.transform.last_params = {"theta": thetas.detach().cpu().float()}
+            return self._graph_pass(k, inputs, prefetch)
         if pre is not None:                              # latents of images + warps (prefetch)
             thetas, inputs = pre
             self.transform.last_params = {"theta": thetas.detach().cpu().float()}
@@ -286,6 +296,82 @@ class TokenOptimizer:
         for b in prefetch:
             self.prefetch(b)
         (total / self.accum).backward()
+        return sel
+
+    def _pass_body(self, k, inputs, th_inv):
+        """The prefetched-latents pass of micro_steps (sparse backward path): capture, selection,
+        losses, backward.  Returns (selected indices per image, (loss, eq, sh) per image)."""
+        got = ptp_utils.run_and_find_attn_per_image(
+            self.ldm, inputs, self.context, noise_level=self.kw["noise_level"], device=self.device,
+            layers=self.kw["layers"], controllers=self.controllers, stacked=True, captured=True)[0]
+        maps = got.maps
+        sel = [self._select(maps[i], maps[k + i]) for i in range(k)]
+        rows = got.select(sel + sel)
+        n = rows.shape[0] // 2
+        A, At = rows[:n], rows[n:]
+        total, off, parts = 0.0, 0, []
+        for i, idx in enumerate(sel):
+            m = idx.numel()
+            loss, eq, sh = self._losses(A[off:off + m], At[off:off + m], i, th_inv[i])
+            off += m
+            parts.append((loss, eq, sh))
+            total = total + loss
+        (total / self.accum).backward()
+        return sel, parts
+
+    def _graph_pass(self, k, inputs, prefetch):
+        """micro_steps as a replay of ONE captured HIP graph.
+
+        The pass has static shapes (k images + warps, N tokens, fixed top-k / FPS counts), so its
+        ~1500 kernels are captured once (torch.cuda.graph: the UNet/VAE GEMMs, MIOpen, and every
+        libskp launch, which all go to the current stream) and replayed with the new latents and
+        inverse warps copied into the graph's static inputs; the noise draw advances the CUDA
+        generator's offset per replay as in eager execution.  The first call runs the pass eagerly
+        (that step's real work) and then captures it; the gradient the graph writes is added to
+        this optimiser step's accumulator, so several passes per step still sum as in eager mode.
+        Same kernels and arithmetic as the eager pass (tests/test_gpu_graph.py)."""
+        th_inv = _upload(self.transform.theta_inverse(), self.device)
+        for b in prefetch:                      # the next passes' VAE, before this pass is issued
+            self.prefetch(b)
+        key = (tuple(inputs.shape), tuple(th_inv.shape))
+        if self._g is None or self._g[0] != key:
+            # eager pass (this step's work) on the capture stream — the warm-up torch's graph capture
+            # wants on the stream it captures on — then the same pass captured into a graph
+            main = torch.cuda.current_stream(self.device)
+            if self._gstream is None:
+                self._gstream = torch.cuda.Stream(device=self.device)
+            side = self._gstream
+            side.wait_stream(main)
+            inputs.record_stream(side)
+            th_inv.record_stream(side)
+            prev = self.context.grad
+            self.context.grad = None
+            with torch.cuda.stream(side):
+                sel, parts = self._pass_body(k, inputs, th_inv)
+                eager_grad = self.context.grad
+                s_in, s_th = inputs.clone(), th_inv.clone()
+            g = torch.cuda.CUDAGraph()
+            self.context.grad = None
+            with torch.cuda.stream(side):
+                with torch.cuda.graph(g, stream=side):
+                    s_sel, s_parts = self._pass_body(k, s_in, s_th)
+            main.wait_stream(side)
+            self._g = (key, g, (s_in, s_th), (s_sel, s_parts, self.context.grad))
+            grad = eager_grad
+        else:
+            _, g, (s_in, s_th), (s_sel, s_parts, s_grad) = self._g
+            prev = self.context.grad if self._grad_acc is not None else None
+            s_in.copy_(inputs)
+            s_th.copy_(th_inv)
+            g.replay()
+            sel = [x.clone() for x in s_sel]
+            parts = [tuple(x.clone() for x in p) for p in s_parts]
+            grad = s_grad
+        # this step's gradient: the pass's, plus what earlier passes of the step accumulated
+        self._grad_acc = grad.clone() if prev is None else prev + grad
+        self.context.grad = self._grad_acc
+        for loss, eq, sh in parts:
+            self._account(loss, eq, sh)
         return sel
 
     def image_loss(self, image):
@@ -342,6 +428,7 @@ class TokenOptimizer:
             self.run_tot, self.run_eq, self.run_sh = (stats / self.world).unbind(0)
         self.optimizer.step()
         self.optimizer.zero_grad()
+        self._grad_acc = None
         rec = {"loss": self.run_tot, "running_equivariance_attn_loss": self.run_eq,
                "running_sharpening_loss": self.run_sh}
         self.reset_running()

@@ -40,8 +40,11 @@ class DDIMScheduler:
     def add_noise(self, original_samples, noise, timesteps):
         ac = self._alphas_cumprod_on(original_samples.device, original_samples.dtype)
         timesteps = timesteps.to(original_samples.device)
-        sqrt_a = ac[timesteps] ** 0.5
-        sqrt_1ma = (1 - ac[timesteps]) ** 0.5
+        # index_select, not ac[t]: a 0-d index tensor is read back to the host (a sync, and not
+        # allowed inside a HIP graph capture)
+        a = ac.index_select(0, timesteps.reshape(-1)).reshape(timesteps.shape)
+        sqrt_a = a ** 0.5
+        sqrt_1ma = (1 - a) ** 0.5
         while sqrt_a.dim() < original_samples.dim():
             sqrt_a = sqrt_a.unsqueeze(-1)
             sqrt_1ma = sqrt_1ma.unsqueeze(-1)

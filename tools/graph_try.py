@@ -13,11 +13,18 @@ from stablekeypoints_amd.optimize import TokenOptimizer  # noqa: E402
 from stablekeypoints_amd.optimize_token import load_ldm  # noqa: E402
 
 dev = torch.device("cuda:0")
-ldm, ctls, _ = load_ldm(dev, "random", feature_upsample_res=128)
+TINY = "--tiny" in sys.argv
 torch.manual_seed(0)
-ctx = torch.randn(1, 500, 768).to(dev)
-opt = TokenOptimizer(ldm, ctls, ctx, accum=4, device=dev)
-data = SyntheticDataset(n=16, size=512)
+if TINY:       # the GPU tests' toy SD (tests/test_gpu_graph.py)
+    from stablekeypoints_amd.sd import TINY_CONFIG, TINY_IMAGE
+    ldm, ctls, _ = load_ldm(dev, "tiny", feature_upsample_res=32, config=TINY_CONFIG)
+    ctx = torch.randn(1, 16, 32).to(dev)
+    opt = TokenOptimizer(ldm, ctls, ctx, top_k=4, furthest_point_num_samples=8, accum=4, device=dev)
+else:
+    ldm, ctls, _ = load_ldm(dev, "random", feature_upsample_res=128)
+    ctx = torch.randn(1, 500, 768).to(dev)
+    opt = TokenOptimizer(ldm, ctls, ctx, accum=4, device=dev)
+data = SyntheticDataset(n=16, size=TINY_IMAGE if TINY else 512)
 imgs = [data[i]["img"][None].to(dev) for i in range(16)]
 k = 4
 with torch.no_grad():
