@@ -67,10 +67,11 @@ def main():
                 call("skp_capture_fwd", ptr(zb2[sz]), 2 * H, sz, N, R, ptr(scratch), ptr(st), stream(dev))
                 del scratch
             res[name] = timed(lambda: ops.capture_bwd(zb2[sz], sz, R, gmap, 0.03125, H, bstr, stats=st), args.iters)
-        elif name in ("maps8", "maps8_old"):   # fused capture + per-image aggregate at the bench shape
-            sizes = (16, 16, 16, 32)
+        elif name in ("maps8", "maps8_old", "maps8_s16", "maps8_s32"):   # fused capture + per-image aggregate, bench shape
+            # (_s16 / _s32: only the bench's s = 16 layers / its s = 32 layer, for per-layer PMC passes)
+            sizes = {"maps8_s16": (16, 16, 16), "maps8_s32": (32,)}.get(name, (16, 16, 16, 32))
             z8 = [torch.randn(8 * H, s * s, N, device=dev, generator=g) * 2 for s in sizes]
-            ops.FUSED_MAPS = name == "maps8"
+            ops.FUSED_MAPS = name != "maps8_old"
             with torch.no_grad():
                 res[name] = timed(lambda: ops.capture_maps(z8, sizes, 8, R), args.iters)
             ops.FUSED_MAPS = True

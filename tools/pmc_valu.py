@@ -6,6 +6,10 @@ VALU busy = 4·SQ_ACTIVE_INST_VALU (quad-cycles, summed over the chip) / (1024 S
 
 usage: python tools/pmc_valu.py COUNTERS.csv --kernel capture_maps_kernel --name skp_capture_maps_fwd \
            --flop 34078720000 --out profiles/pmc_valu.json
+
+``--kernel a,b,c``: one call made of several kernels (skp_capture_maps_bwd_sel = sel_gather, sel_dot,
+sel_adj, sel_dense): the call's VALU-busy is Σ 4·ACTIVE_INST_VALU / Σ 1024·GRBM_GUI_ACTIVE/8 over
+its kernels (each kernel's median launch), i.e. weighted by their active time.
 """
 import argparse
 import csv
@@ -23,17 +27,29 @@ def main():
     ap.add_argument("--workload", default="")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
-    per = collections.defaultdict(dict)
+    names = [k for k in args.kernel.split(",") if k]
+    per = {k: collections.defaultdict(dict) for k in names}
     for r in csv.DictReader(open(args.csv)):
-        if args.kernel in r["Kernel_Name"]:
-            per[r["Dispatch_Id"]][r["Counter_Name"]] = float(r["Counter_Value"])
-    busy = [4 * d["SQ_ACTIVE_INST_VALU"] / (1024 * d["GRBM_GUI_ACTIVE"] / 8) for d in per.values()
-            if "SQ_ACTIVE_INST_VALU" in d and d.get("GRBM_GUI_ACTIVE")]
-    if not busy:
-        raise SystemExit(f"no counters for {args.kernel}")
-    rec = {args.name: {"valu_busy": statistics.median(busy), "launches": len(busy), "flop_per_launch": args.flop,
+        for k in names:
+            if k in r["Kernel_Name"]:
+                per[k][r["Dispatch_Id"]][r["Counter_Name"]] = float(r["Counter_Value"])
+    num = den = 0.0
+    counts = []
+    for k in names:
+        rows = [d for d in per[k].values() if "SQ_ACTIVE_INST_VALU" in d and d.get("GRBM_GUI_ACTIVE")]
+        if not rows:
+            raise SystemExit(f"no counters for {k}")
+        counts.append(len(rows))
+        num += statistics.median(4 * d["SQ_ACTIVE_INST_VALU"] for d in rows)
+        den += statistics.median(1024 * d["GRBM_GUI_ACTIVE"] / 8 for d in rows)
+    busy = [num / den]
+    if len(names) == 1:
+        rows = [d for d in per[names[0]].values() if "SQ_ACTIVE_INST_VALU" in d and d.get("GRBM_GUI_ACTIVE")]
+        busy = [4 * d["SQ_ACTIVE_INST_VALU"] / (1024 * d["GRBM_GUI_ACTIVE"] / 8) for d in rows]
+    rec = {args.name: {"valu_busy": statistics.median(busy), "launches": min(counts), "kernels": names,
+                       "flop_per_launch": args.flop,
                        "method": "rocprofv3 --pmc SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE; 4*ACTIVE_INST_VALU / "
-                                 "(1024 SIMDs * GRBM_GUI_ACTIVE/8), median over launches (tools/pmc_valu.py)",
+                                 "(1024 SIMDs * GRBM_GUI_ACTIVE/8), median over launches; several kernels: active-time weighted (tools/pmc_valu.py)",
                        "workload": args.workload}}
     print(json.dumps(rec, indent=1))
     if args.out:
