@@ -76,7 +76,7 @@ def test_graph_pass_equals_eager_pass():
             for x, y in zip(a, b):
                 assert np.array_equal(x, y)
         elif ka == "grad":
-            assert np.allclose(a, b, rtol=1e-4, atol=1e-9), np.abs(a - b).max()
+            assert np.allclose(a, b, rtol=1e-4, atol=1e-8), np.abs(a - b).max()
         elif ka == "loss":
             assert abs(a - b) <= 1e-5 * abs(a)
         else:

@@ -13,11 +13,16 @@ import json
 import statistics
 
 
-def values(path, kernel, counter):
+def values(path, kernel, counter, launches=None):
+    """Counter values of the kernel's launches in dispatch order; ``launches`` = (a, b) keeps the
+    a-th … (b−1)-th of them (one kbench case of several that launch the same kernel)."""
     out = []
     for r in csv.DictReader(open(path)):
         if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
-            out.append(float(r["Counter_Value"]))
+            out.append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
+    out = [v for _, v in sorted(out)]
+    if launches:
+        out = out[launches[0]:launches[1]]
     if not out:
         raise SystemExit(f"no {counter} rows for {kernel} in {path}")
     return out
@@ -32,9 +37,11 @@ def main():
     ap.add_argument("--algorithmic", type=int, default=1081344000)
     ap.add_argument("--out", default=None, help="JSON file to update (other kernels' entries are kept)")
     ap.add_argument("--workload", default="tools/kbench.py --only agg (N=500, R=128, 4 distinct layers x 8 heads)")
+    ap.add_argument("--launches", default="", help="a:b = the kernel's a-th … (b−1)-th launches in dispatch order")
     args = ap.parse_args()
-    f = values(args.fetch, args.kernel, "FETCH_SIZE")
-    w = values(args.write, args.kernel, "WRITE_SIZE")
+    rng = tuple(int(x) for x in args.launches.split(":")) if args.launches else None
+    f = values(args.fetch, args.kernel, "FETCH_SIZE", rng)
+    w = values(args.write, args.kernel, "WRITE_SIZE", rng)
     fm, wm = statistics.median(f), statistics.median(w)
     fetch = fm * 1024 * 2
     write = wm * 1024
