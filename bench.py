@@ -378,6 +378,9 @@ def main():
                          "enqueued between the current pass's forward and backward; steady state: every timed step "
                          "runs one UNet pass and one VAE pass, the warm-up's prefetches are balanced by the last "
                          "timed steps' (0 = no prefetch)")
+    ap.add_argument("--prefetch-at", default="capture_bwd", choices=["capture_bwd", "bwd"],
+                    help="where the VAE prefetch is enqueued: after the sparse capture backward (the VAE overlaps "
+                         "the UNet backward) or before the whole backward")
     ap.add_argument("--graph", type=int, default=0,
                     help="1 = replay each pass (capture forward, selection, losses, backward into the embedding) as "
                          "one captured HIP graph (TokenOptimizer(graph=True)); measured neutral at the bench shape "
@@ -438,6 +441,7 @@ def main():
         return stage_main(args, ldm, controllers, context.detach(), dev, world, rank, backend)
     torch.manual_seed(1234 + rank)
     opt = TokenOptimizer(ldm, controllers, context, accum=args.accum, device=dev, graph=bool(args.graph))
+    opt.prefetch_at = args.prefetch_at
     data = SyntheticDataset(n=16, size=args.res, seed=rank)
     imgs = [data[i]["img"][None].to(dev) for i in range(len(data))]
     timer = KernelTimer(["skp_aggregate", "skp_capture_fwd", "skp_capture_bwd", "skp_capture_maps_fwd",
@@ -491,7 +495,8 @@ def main():
     images = world * args.accum * args.steps
     value = images / elapsed
     timing_src = ("HIP events around every launch in the timed region, on the launching stream "
-                  "(bench.py KernelTimer)")
+                  "(bench.py KernelTimer); launches that overlap the side-stream VAE prefetch share the GPU "
+                  "with it (isolated launch times: tools/kbench.py)")
     if args.graph:
         # the timed steps replay a HIP graph, which runs no Python and so records no per-kernel
         # events: the same pass runs once eagerly after the timed region (same shapes, same
@@ -593,7 +598,7 @@ def main():
                           "parallelism": (f"dp{world} ({'RCCL' if backend == 'nccl' else backend} all-reduce of the "
                                           "token-embedding gradient)" if world > 1 else "dp1 (single process, no collective)"),
                           "tuned_gemms": _tuned_gemms_in_use(), "hip_graph": bool(args.graph),
-                          "vae_prefetch": args.prefetch},
+                          "vae_prefetch": args.prefetch, "prefetch_at": args.prefetch_at},
                "roofline": roof, "cpu_baseline": cpu, "kernels": extra,
                "last_loss": float(rec["loss"])}
         print(json.dumps(out), flush=True)

@@ -53,16 +53,29 @@ constexpr int floor_div(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) /
 constexpr int lo_rel(int t, int ratio) { return floor_div(2 * t + 1 - ratio, 2 * ratio) - 1; }
 
 // ------------------------------------------------------------------------------ sel_gather
-__global__ void sel_gather_kernel(const float* __restrict__ z, int BH, int SS, int N, int H,
-                                  const long long* __restrict__ tok, int K, float* __restrict__ zsel) {
+// The small per-layer kernels (sel_gather, sel_dot, sel_adj) each run every layer in ONE launch:
+// per-layer pointers and sizes by value, the layer found from the block / element index (12 short
+// launches per step → 3, so no launch tail per layer).
+struct SelSmall {
+  const float* z[SKP_MAX_LAYERS];
+  const float2* stats[SKP_MAX_LAYERS];
+  int s[SKP_MAX_LAYERS];
+  long long zoff[SKP_MAX_LAYERS + 1];   // zsel prefix offsets (floats): Σ BH·s²·K
+};
+
+__global__ void sel_gather_kernel(SelSmall t, int L, int BH, int N, int H, const long long* __restrict__ tok, int K,
+                                  float* __restrict__ zsel) {
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long total = (long long)BH * SS * K;
-  if (e >= total) return;
-  const int k = (int)(e % K);
-  const long long bq = e / K;   // bh·SS + q
+  if (e >= t.zoff[L]) return;
+  int l = 0;
+  while (l + 1 < L && e >= t.zoff[l + 1]) ++l;
+  const long long le = e - t.zoff[l];
+  const int SS = t.s[l] * t.s[l];
+  const int k = (int)(le % K);
+  const long long bq = le / K;   // bh·SS + q
   const int bh = (int)(bq / SS);
-  const long long t = tok[(long long)(bh / H) * K + k];
-  zsel[e] = (t >= 0 && t < N) ? z[bq * N + t] : 0.0f;
+  const long long tk = tok[(long long)(bh / H) * K + k];
+  zsel[e] = (tk >= 0 && tk < N) ? t.z[l][bq * N + tk] : 0.0f;
 }
 
 // output indices whose taps can reach low-res index j: src ∈ [j − 2, j + 2) (clamped edges included)
@@ -78,16 +91,22 @@ __device__ __forceinline__ void adj_range(int j, int S, int R, int& lo, int& hi)
 // one block per (bh, y); threads over x.  Per pixel: a_k, e_k = a_k·g_k (E[bh][k][p]) and dot →
 // pix[bh][p] = (mb, −dot) with mb = log2(1/Σ) − max·log2e, so a = exp2(z·log2e + mb).
 // LDS: the vertical pass Vs[S][K] of the selected logits.
-__global__ __launch_bounds__(256) void sel_dot_kernel(const float* __restrict__ zsel, int S, int R, int H, int K,
-                                                      const long long* __restrict__ tok,
+__global__ __launch_bounds__(256) void sel_dot_kernel(SelSmall t, const float* __restrict__ zsel, int BH, int R,
+                                                      int H, int K, const long long* __restrict__ tok,
                                                       const float* __restrict__ gsel, float gscale,
-                                                      const float2* __restrict__ stats, float* __restrict__ E,
-                                                      float2* __restrict__ pix) {
+                                                      float* __restrict__ E, float2* __restrict__ pix) {
   extern __shared__ float Vs[];   // S × K
-  const int bh = blockIdx.x / R, y = blockIdx.x % R;
+  const int l = blockIdx.x / (BH * R);
+  const int rem = blockIdx.x - l * (BH * R);
+  const int bh = rem / R, y = rem % R;
   const int b = bh / H;
+  const int S = t.s[l];
+  const size_t RRl = (size_t)R * R;
+  E += (size_t)l * BH * K * RRl;
+  pix += (size_t)l * BH * RRl;
+  const float2* stats = t.stats[l];
   const Taps4 ty = bicubic_taps(y, S, R);
-  const float* zb = zsel + (size_t)bh * S * S * K;
+  const float* zb = zsel + t.zoff[l] + (size_t)bh * S * S * K;
   for (int e = threadIdx.x; e < S * K; e += blockDim.x) {
     const int j = e / K, k = e - j * K;
     float v = ty.w[0] * zb[((size_t)ty.i[0] * S + j) * K + k];
@@ -128,15 +147,18 @@ __global__ __launch_bounds__(256) void sel_dot_kernel(const float* __restrict__ 
 // take consecutive rows of the tile, so one wave reads 32 different banks), then
 // es[i][j] = Σ_y A[i][y]·Hs[y][j].  Fixed summation order (x, then y ascending).
 constexpr int SEL_ADJ_TILE = 32;
-__global__ __launch_bounds__(256) void sel_adj_kernel(const float* __restrict__ E, int S, int R,
-                                                      float* __restrict__ es) {
+__global__ __launch_bounds__(256) void sel_adj_kernel(SelSmall t, const float* __restrict__ E, int BHK, int smax,
+                                                      int R, float* __restrict__ es) {
   extern __shared__ float sh[];
   const int RP = R + 1;
+  const int l = blockIdx.x / BHK;
+  const int S = t.s[l];
   float* A = sh;                 // S × (R + 1)
   float* Hs = A + S * RP;        // R × S
   float* Et = Hs + R * S;        // SEL_ADJ_TILE × (R + 1)
-  const size_t bk = blockIdx.x;  // bh·K + k
-  const float* Eb = E + bk * (size_t)R * R;
+  const size_t bk = blockIdx.x - (size_t)l * BHK;  // bh·K + k
+  const float* Eb = E + ((size_t)l * BHK + bk) * (size_t)R * R;
+  es += (size_t)l * BHK * smax * smax;
   for (int e = threadIdx.x; e < S * RP; e += blockDim.x) A[e] = 0.0f;
   __syncthreads();
   for (int x = threadIdx.x; x < R; x += blockDim.x) {
@@ -436,9 +458,11 @@ SelWs sel_ws(const int* sizes, int L, int B, int H, int R, int K) {
   for (int l = 0; l < L; ++l) smax = std::max(smax, (size_t)sizes[l]);
   const size_t smax2 = smax * smax;
   const size_t BH = (size_t)B * H, RR = (size_t)R * R;
+  size_t zs = 0;
+  for (int l = 0; l < L; ++l) zs += BH * (size_t)sizes[l] * sizes[l] * K;
   w.zsel = 0;
-  w.E = w.zsel + ((BH * smax2 * K + 3) & ~(size_t)3);
-  w.pix = w.E + ((BH * K * RR + 3) & ~(size_t)3);
+  w.E = w.zsel + ((zs + 3) & ~(size_t)3);
+  w.pix = w.E + (size_t)L * BH * K * RR;
   w.es = w.pix + (size_t)L * BH * RR * 2;
   w.total = w.es + (size_t)L * BH * K * smax2;
   return w;
@@ -500,21 +524,24 @@ extern "C" int skp_capture_maps_bwd_sel(const float* const* z_low, const int* si
   float* es = workspace + wsz.es;
   int smax = 1;
   for (int l = 0; l < L; ++l) smax = std::max(smax, sizes[l]);
+  SelSmall t{};
+  t.zoff[0] = 0;
   for (int l = 0; l < L; ++l) {
-    const int S = sizes[l];
-    const long long tot = (long long)BH * S * S * K;
-    hipLaunchKernelGGL(sel_gather_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, z_low[l], BH, S * S, N,
-                       H, sel_tok, K, zsel);
-    SKP_LAUNCH_CHECK();
-    hipLaunchKernelGGL(sel_dot_kernel, dim3((unsigned)(BH * R)), dim3(std::min(R, 256)), (size_t)S * K * sizeof(float),
-                       st, zsel, S, R, H, K, sel_tok, gsel, gscale, reinterpret_cast<const float2*>(stats[l]), E,
-                       pix + (size_t)l * BH * RR);
-    SKP_LAUNCH_CHECK();
-    hipLaunchKernelGGL(sel_adj_kernel, dim3((unsigned)(BH * K)), dim3(256),
-                       (size_t)(S * (R + 1) + R * S + SEL_ADJ_TILE * (R + 1)) * sizeof(float), st, E, S, R,
-                       es + (size_t)l * BH * K * smax * smax);
-    SKP_LAUNCH_CHECK();
+    t.z[l] = z_low[l];
+    t.stats[l] = reinterpret_cast<const float2*>(stats[l]);
+    t.s[l] = sizes[l];
+    t.zoff[l + 1] = t.zoff[l] + (long long)BH * sizes[l] * sizes[l] * K;
   }
+  hipLaunchKernelGGL(sel_gather_kernel, dim3((unsigned)((t.zoff[L] + 255) / 256)), dim3(256), 0, st, t, L, BH, N, H,
+                     sel_tok, K, zsel);
+  SKP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(sel_dot_kernel, dim3((unsigned)(L * BH * R)), dim3(std::min(R, 256)),
+                     (size_t)smax * K * sizeof(float), st, t, zsel, BH, R, H, K, sel_tok, gsel, gscale, E, pix);
+  SKP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(sel_adj_kernel, dim3((unsigned)(L * BH * K)), dim3(256),
+                     (size_t)(smax * (R + 1) + R * smax + SEL_ADJ_TILE * (R + 1)) * sizeof(float), st, t, E, BH * K,
+                     smax, R, es);
+  SKP_LAUNCH_CHECK();
   // the dense part: layers of equal s share a launch (up to 4 per launch)
   bool done[SKP_MAX_LAYERS] = {};
   for (int l = 0; l < L; ++l) {

@@ -329,6 +329,9 @@ class CapturedMaps:
 
     def __init__(self, zs, sizes, B, R):
         self.zs = list(zs)
+        # called once by select()'s backward right after the capture backward is enqueued (on the
+        # autograd thread, the main stream current), then cleared
+        self.after_backward = None
         self.sizes = tuple(int(s) for s in sizes)
         self.B, self.R = int(B), int(R)
         with torch.no_grad():
@@ -430,6 +433,9 @@ class _SelectMaps(torch.autograd.Function):
             dense.index_add_(0, img * N + tok, g)
             dzs = CaptureMaps._dense_bwd([_c(z) for z in cm.zs], cm.stats, (B, cm.H, R, N, list(cm.sizes)),
                                          dense.view(B, N, R, R))
+        cb, cm.after_backward = cm.after_backward, None
+        if cb is not None:    # e.g. TokenOptimizer's VAE prefetch, enqueued behind the capture backward
+            cb()
         return (None, None, None) + tuple(dzs)
 
 

@@ -115,6 +115,9 @@ class TokenOptimizer:
         # graph: replay the prefetched-latents pass (capture forward, selection, losses, backward)
         # as ONE HIP graph (micro_steps); the host then issues one launch per pass instead of ~1500
         self.graph = graph
+        # where micro_steps enqueues the next passes' VAE prefetch: "capture_bwd" = right after the
+        # sparse capture backward, "bwd" = between the forward and the backward
+        self.prefetch_at = "capture_bwd"
         self._g = None           # (key, HIPGraph, static inputs, static outputs) once captured
         self._grad_acc = None
         self._gstream = None
@@ -293,6 +296,16 @@ class TokenOptimizer:
             off += n
             self._account(loss, eq, sh)
             total = total + loss
+        if sparse and prefetch and self.prefetch_at == "capture_bwd":
+            # the next passes' VAE enqueued right behind the sparse capture backward (select()'s
+            # backward calls it): the VAE then shares the GPU with the UNet backward's GEMMs and
+            # convolutions rather than with the capture backward's VALU kernels
+            got.after_backward = lambda: [self.prefetch(b) for b in prefetch]
+            (total / self.accum).backward()
+            if got.after_backward is not None:    # the hook did not run (no selected rows)
+                got.after_backward()
+                got.after_backward = None
+            return sel
         for b in prefetch:
             self.prefetch(b)
         (total / self.accum).backward()
