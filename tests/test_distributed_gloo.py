@@ -1,4 +1,5 @@
-"""Multi-rank semantics of the token optimisation on CPU (gloo, world sizes 2 and 4).
+"""Multi-rank semantics of the token optimisation on CPU (gloo, world sizes 2 and 4; 8 for the
+sharded step and the eval stages).
 
 The reference runs one replica per GPU under nn.DataParallel and averages the per-replica
 losses (optimize.py:428-443).  Here each rank is a process; TokenOptimizer all-reduces the
@@ -101,9 +102,9 @@ def _worker(rank, world, port, n_img, steps, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", WORLDS)
+@pytest.mark.parametrize("world", WORLDS + (8,))
 def test_sharded_grad_allreduce_equals_single_rank(world):
-    n_img, steps = 4, 3
+    n_img, steps = max(4, world), 3
     ref_ctx, ref_recs, _ = _reference_single(n_img, steps)
     out = _spawn(_worker, world, n_img, steps)
     for rank, c, recs in out:
@@ -166,13 +167,13 @@ class _DS(torch.utils.data.Dataset):
         return {"img": torch.rand(3, 8, 8, generator=g), "kpts": torch.zeros(2, 2)}
 
     def __len__(self):
-        return 6
+        return 16   # ≥ 8: every world size below gets whole replica batches
 
 
 def _eval_stages(num_gpus):
     from stablekeypoints_amd import keypoint_regressor as kr, eval as ev
     torch.manual_seed(11)
-    idx = kr.find_best_indices(None, None, num_steps=6, device="cpu", top_k=4, furthest_point_num_samples=8,
+    idx = kr.find_best_indices(None, None, num_steps=max(6, num_gpus), device="cpu", top_k=4, furthest_point_num_samples=8,
                                controllers={"cpu": None}, num_gpus=num_gpus, top_k_strategy="gaussian",
                                dataset=_DS())
     img = _DS()[0]["img"]
@@ -192,7 +193,7 @@ def _eval_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", WORLDS)
+@pytest.mark.parametrize("world", WORLDS + (8,))
 def test_sharded_eval_stages_equal_replicas_in_one_process(monkeypatch, world):
     _stub_eval_stages(monkeypatch.setattr)
     ref_idx, ref_tta = _eval_stages(world)
