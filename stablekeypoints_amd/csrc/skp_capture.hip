@@ -571,195 +571,201 @@ void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nc
 
   const int total = B * R * nchunks;
   const int per = (total + 7) / 8;
-  const int job = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
-  if (job >= total) return;
-  const int xc = job % nchunks;
-  const int y = (job / nchunks) % R;
-  const int b = job / (nchunks * R);
-  const int x0 = xc * P;
-  const int np = min(P, R - x0);
-
+  // XCD x takes jobs [x·per, (x + 1)·per); its workgroups stride through them (one job each on a
+  // full grid; with a persistent grid of 2 workgroups per CU the XCD's workgroups start together
+  // and walk the same (layer, head) slabs in step, so the rows they share stay in that XCD's L2)
+  const int xcd = blockIdx.x & 7, nper = gridDim.x >> 3;
+  const int jfirst = xcd * per + (blockIdx.x >> 3), jend = min(total, (xcd + 1) * per);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int row = lane >> 4, li = lane & 15;
-  f4 acc[G][QPL];
-#pragma unroll
-  for (int g = 0; g < G; ++g)
-#pragma unroll
-    for (int c = 0; c < QPL; ++c) acc[g][c] = (f4)0.0f;
+  for (int job = jfirst; job < jend; job += nper) {
+    if (job != jfirst) __syncthreads();   // the previous job's store tile (in V) fully read
+    const int xc = job % nchunks;
+    const int y = (job / nchunks) % R;
+    const int b = job / (nchunks * R);
+    const int x0 = xc * P;
+    const int np = min(P, R - x0);
 
-  const bool vec = (N & 3) == 0;
-  // Per (layer, head) slab: stage the tap table (first head of a layer) and the vertical pass,
-  // then the pixel work; two workgroups per CU overlap one's staging with the other's pixels.
-  // (A software pipeline with double-buffered V measured slower: 1.03 vs 0.94 ms.)
-  auto layer_cols = [&](int l, int& s, int& c0, int& nc) {
-    s = cl.s[l];
-    c0 = max(bicubic_taps(x0, s, R).lo, 0);
-    nc = min(bicubic_taps(x0 + np - 1, s, R).lo + 3, s - 1) - c0 + 1;
-  };
-  auto stage = [&](int it) {   // tap table (first head of a layer) + vertical pass of slab it
-    const int l = it / H, h = it - l * H;
-    int s, c0, nc;
-    layer_cols(l, s, c0, nc);
-    const int buf = it & 1;
-    if (h == 0) {
-      float4* tw = TW + (l & 1) * P;
-      int4* tiw = TI + (l & 1) * P;
-      for (int x = tid; x < P; x += kMapThreads) {
-        const Taps4 t = bicubic_taps(x0 + min(x, np - 1), s, R);
-        tw[x] = make_float4(t.w[0], t.w[1], t.w[2], t.w[3]);
-        tiw[x] = make_int4((t.i[0] - c0) * Npq, (t.i[1] - c0) * Npq, (t.i[2] - c0) * Npq, (t.i[3] - c0) * Npq);
-      }
-    }
-    const Taps4 ty = bicubic_taps(y, s, R);
-    const float* zb = cl.z[l] + (size_t)(b * H + h) * s * s * N;
-    float* Vb = V + buf * vstride;
-    // V[jj][n] = Σ_k wy_k · z[iy_k][c0 + jj][n]
-    if (vec) {
-      const f4* r0 = reinterpret_cast<const f4*>(zb + ((size_t)ty.i[0] * s + c0) * N);
-      const f4* r1 = reinterpret_cast<const f4*>(zb + ((size_t)ty.i[1] * s + c0) * N);
-      const f4* r2 = reinterpret_cast<const f4*>(zb + ((size_t)ty.i[2] * s + c0) * N);
-      const f4* r3 = reinterpret_cast<const f4*>(zb + ((size_t)ty.i[3] * s + c0) * N);
-      const int nq = N >> 2;
-      f4* V4 = reinterpret_cast<f4*>(Vb);
-      // up to VPT outputs per thread with all 4·VPT loads in flight before the first FMA
-#ifndef SKP_MAPS_VPT
-#define SKP_MAPS_VPT 1   // vertical outputs per thread per batch (2, 3 measured 1-2% slower)
-#endif
-      constexpr int VPT = SKP_MAPS_VPT;
-      const int tot = nc * Npq;
-      for (int e0 = tid; e0 < tot; e0 += VPT * kMapThreads) {
-        f4 a[VPT][4];
-#pragma unroll
-        for (int k = 0; k < VPT; ++k) {
-          const int e = e0 + k * kMapThreads;
-          const int jj = e / Npq, q = e - jj * Npq;
-          if (e < tot && q < nq) {
-            const int o = jj * nq + q;
-            a[k][0] = r0[o];
-            a[k][1] = r1[o];
-            a[k][2] = r2[o];
-            a[k][3] = r3[o];
-          }
+    f4 acc[G][QPL];
+  #pragma unroll
+    for (int g = 0; g < G; ++g)
+  #pragma unroll
+      for (int c = 0; c < QPL; ++c) acc[g][c] = (f4)0.0f;
+
+    const bool vec = (N & 3) == 0;
+    // Per (layer, head) slab: stage the tap table (first head of a layer) and the vertical pass,
+    // then the pixel work; two workgroups per CU overlap one's staging with the other's pixels.
+    // (A software pipeline with double-buffered V measured slower: 1.03 vs 0.94 ms.)
+    auto layer_cols = [&](int l, int& s, int& c0, int& nc) {
+      s = cl.s[l];
+      c0 = max(bicubic_taps(x0, s, R).lo, 0);
+      nc = min(bicubic_taps(x0 + np - 1, s, R).lo + 3, s - 1) - c0 + 1;
+    };
+    auto stage = [&](int it) {   // tap table (first head of a layer) + vertical pass of slab it
+      const int l = it / H, h = it - l * H;
+      int s, c0, nc;
+      layer_cols(l, s, c0, nc);
+      const int buf = it & 1;
+      if (h == 0) {
+        float4* tw = TW + (l & 1) * P;
+        int4* tiw = TI + (l & 1) * P;
+        for (int x = tid; x < P; x += kMapThreads) {
+          const Taps4 t = bicubic_taps(x0 + min(x, np - 1), s, R);
+          tw[x] = make_float4(t.w[0], t.w[1], t.w[2], t.w[3]);
+          tiw[x] = make_int4((t.i[0] - c0) * Npq, (t.i[1] - c0) * Npq, (t.i[2] - c0) * Npq, (t.i[3] - c0) * Npq);
         }
-#pragma unroll
-        for (int k = 0; k < VPT; ++k) {
-          const int e = e0 + k * kMapThreads;
-          const int jj = e / Npq, q = e - jj * Npq;
-          if (e < tot) {
-            f4 v = (f4)kPadLogit;
-            if (q < nq) {
-              v = a[k][0] * ty.w[0];
-              v = __builtin_elementwise_fma(a[k][1], (f4)ty.w[1], v);
-              v = __builtin_elementwise_fma(a[k][2], (f4)ty.w[2], v);
-              v = __builtin_elementwise_fma(a[k][3], (f4)ty.w[3], v);
+      }
+      const Taps4 ty = bicubic_taps(y, s, R);
+      const float* zb = cl.z[l] + (size_t)(b * H + h) * s * s * N;
+      float* Vb = V + buf * vstride;
+      // V[jj][n] = Σ_k wy_k · z[iy_k][c0 + jj][n]
+      if (vec) {
+        const f4* r0 = reinterpret_cast<const f4*>(zb + ((size_t)ty.i[0] * s + c0) * N);
+        const f4* r1 = reinterpret_cast<const f4*>(zb + ((size_t)ty.i[1] * s + c0) * N);
+        const f4* r2 = reinterpret_cast<const f4*>(zb + ((size_t)ty.i[2] * s + c0) * N);
+        const f4* r3 = reinterpret_cast<const f4*>(zb + ((size_t)ty.i[3] * s + c0) * N);
+        const int nq = N >> 2;
+        f4* V4 = reinterpret_cast<f4*>(Vb);
+        // up to VPT outputs per thread with all 4·VPT loads in flight before the first FMA
+  #ifndef SKP_MAPS_VPT
+  #define SKP_MAPS_VPT 1   // vertical outputs per thread per batch (2, 3 measured 1-2% slower)
+  #endif
+        constexpr int VPT = SKP_MAPS_VPT;
+        const int tot = nc * Npq;
+        for (int e0 = tid; e0 < tot; e0 += VPT * kMapThreads) {
+          f4 a[VPT][4];
+  #pragma unroll
+          for (int k = 0; k < VPT; ++k) {
+            const int e = e0 + k * kMapThreads;
+            const int jj = e / Npq, q = e - jj * Npq;
+            if (e < tot && q < nq) {
+              const int o = jj * nq + q;
+              a[k][0] = r0[o];
+              a[k][1] = r1[o];
+              a[k][2] = r2[o];
+              a[k][3] = r3[o];
             }
-            V4[e] = v;
+          }
+  #pragma unroll
+          for (int k = 0; k < VPT; ++k) {
+            const int e = e0 + k * kMapThreads;
+            const int jj = e / Npq, q = e - jj * Npq;
+            if (e < tot) {
+              f4 v = (f4)kPadLogit;
+              if (q < nq) {
+                v = a[k][0] * ty.w[0];
+                v = __builtin_elementwise_fma(a[k][1], (f4)ty.w[1], v);
+                v = __builtin_elementwise_fma(a[k][2], (f4)ty.w[2], v);
+                v = __builtin_elementwise_fma(a[k][3], (f4)ty.w[3], v);
+              }
+              V4[e] = v;
+            }
           }
         }
-      }
-    } else {
-#pragma unroll 1
-      for (int e = tid; e < nc * Np; e += kMapThreads) {
-        const int jj = e / Np, n = e - jj * Np;
-        float v = kPadLogit;
-        if (n < N) {
-          const int j = c0 + jj;
-          v = ty.w[0] * zb[((size_t)ty.i[0] * s + j) * N + n];
-          v += ty.w[1] * zb[((size_t)ty.i[1] * s + j) * N + n];
-          v += ty.w[2] * zb[((size_t)ty.i[2] * s + j) * N + n];
-          v += ty.w[3] * zb[((size_t)ty.i[3] * s + j) * N + n];
+      } else {
+  #pragma unroll 1
+        for (int e = tid; e < nc * Np; e += kMapThreads) {
+          const int jj = e / Np, n = e - jj * Np;
+          float v = kPadLogit;
+          if (n < N) {
+            const int j = c0 + jj;
+            v = ty.w[0] * zb[((size_t)ty.i[0] * s + j) * N + n];
+            v += ty.w[1] * zb[((size_t)ty.i[1] * s + j) * N + n];
+            v += ty.w[2] * zb[((size_t)ty.i[2] * s + j) * N + n];
+            v += ty.w[3] * zb[((size_t)ty.i[3] * s + j) * N + n];
+          }
+          Vb[e] = v;
         }
-        Vb[e] = v;
+      }
+    };
+    const int nslab = L * H;
+    for (int it = 0; it < nslab; ++it) {
+      if (it > 0) __syncthreads();   // V (and at a layer change the tap table) of slab it − 1 consumed
+  #if SKP_MAPS_PRIO
+      __builtin_amdgcn_s_setprio(SKP_MAPS_PRIO);   // the staging's loads ahead of the other workgroup's pixels
+  #endif
+      stage(it);
+  #if SKP_MAPS_PRIO
+      __builtin_amdgcn_s_setprio(0);
+  #endif
+      __syncthreads();
+      const int l = it / H, bh = b * H + (it - l * H);
+      const f4* V4 = reinterpret_cast<const f4*>(V + (it & 1) * vstride) + li;
+      const float4* tw = TW + (l & 1) * P;
+      const int4* tiw = TI + (l & 1) * P;
+      float2* st = cl.stats[l];
+  #pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const int xl = wid * PXW + 4 * g + row;              // pixel of this 16-lane row
+        const int xr = min(xl, np - 1);                        // past-the-edge rows redo a valid one
+        const float4 w = tw[xr];
+        const int4 ti = tiw[xr];
+        f4 zc[QPL];
+        float m = kPadLogit;
+  #pragma unroll
+        for (int c = 0; c < QPL; ++c) {
+          const f4 a0 = V4[ti.x + 16 * c], a1 = V4[ti.y + 16 * c];
+          const f4 a2 = V4[ti.z + 16 * c], a3 = V4[ti.w + 16 * c];
+          // token pairs on the packed f32 VALU: z = ((w0·a0 + w1·a1) + w2·a2) + w3·a3
+          f4 v = a0 * w.x;
+          v = __builtin_elementwise_fma(a1, (f4)w.y, v);
+          v = __builtin_elementwise_fma(a2, (f4)w.z, v);
+          v = __builtin_elementwise_fma(a3, (f4)w.w, v);
+          zc[c] = v;
+          m = __builtin_fmaxf(__builtin_fmaxf(m, v.x), v.y);
+          m = __builtin_fmaxf(__builtin_fmaxf(m, v.z), v.w);
+          if (QPL > 4 || (c & 1)) __builtin_amdgcn_sched_barrier(0);   // bound the LDS reads in flight (registers)
+        }
+        m = row16_max(m);
+        const f4 mb = (f4)(-m * L2E);
+        f4 sv = (f4)0.0f;
+  #pragma unroll
+        for (int c = 0; c < QPL; ++c) {
+          f4 t = __builtin_elementwise_fma(zc[c], (f4)L2E, mb);
+          t.x = __builtin_amdgcn_exp2f(t.x);
+          t.y = __builtin_amdgcn_exp2f(t.y);
+          t.z = __builtin_amdgcn_exp2f(t.z);
+          t.w = __builtin_amdgcn_exp2f(t.w);
+          zc[c] = t;
+          sv += t;
+        }
+        const float inv = __builtin_amdgcn_rcpf(row16_sum((sv.x + sv.y) + (sv.z + sv.w)));
+  #pragma unroll
+        for (int c = 0; c < QPL; ++c) acc[g][c] = __builtin_elementwise_fma(zc[c], (f4)inv, acc[g][c]);
+        if (st && li == 0 && xl < np) st[((size_t)bh * R + y) * R + x0 + xl] = make_float2(m, inv);
+        __builtin_amdgcn_sched_barrier(0);   // keep the next pixels' LDS reads from being hoisted (registers)
       }
     }
-  };
-  const int nslab = L * H;
-  for (int it = 0; it < nslab; ++it) {
-    if (it > 0) __syncthreads();   // V (and at a layer change the tap table) of slab it − 1 consumed
-#if SKP_MAPS_PRIO
-    __builtin_amdgcn_s_setprio(SKP_MAPS_PRIO);   // the staging's loads ahead of the other workgroup's pixels
-#endif
-    stage(it);
-#if SKP_MAPS_PRIO
-    __builtin_amdgcn_s_setprio(0);
-#endif
-    __syncthreads();
-    const int l = it / H, bh = b * H + (it - l * H);
-    const f4* V4 = reinterpret_cast<const f4*>(V + (it & 1) * vstride) + li;
-    const float4* tw = TW + (l & 1) * P;
-    const int4* tiw = TI + (l & 1) * P;
-    float2* st = cl.stats[l];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const int xl = wid * PXW + 4 * g + row;              // pixel of this 16-lane row
-      const int xr = min(xl, np - 1);                        // past-the-edge rows redo a valid one
-      const float4 w = tw[xr];
-      const int4 ti = tiw[xr];
-      f4 zc[QPL];
-      float m = kPadLogit;
-#pragma unroll
-      for (int c = 0; c < QPL; ++c) {
-        const f4 a0 = V4[ti.x + 16 * c], a1 = V4[ti.y + 16 * c];
-        const f4 a2 = V4[ti.z + 16 * c], a3 = V4[ti.w + 16 * c];
-        // token pairs on the packed f32 VALU: z = ((w0·a0 + w1·a1) + w2·a2) + w3·a3
-        f4 v = a0 * w.x;
-        v = __builtin_elementwise_fma(a1, (f4)w.y, v);
-        v = __builtin_elementwise_fma(a2, (f4)w.z, v);
-        v = __builtin_elementwise_fma(a3, (f4)w.w, v);
-        zc[c] = v;
-        m = __builtin_fmaxf(__builtin_fmaxf(m, v.x), v.y);
-        m = __builtin_fmaxf(__builtin_fmaxf(m, v.z), v.w);
-        if (QPL > 4 || (c & 1)) __builtin_amdgcn_sched_barrier(0);   // bound the LDS reads in flight (registers)
+    // token-major store: round r stages tokens [128r, 128r + 128) of all P pixels in LDS; lane li
+    // of a row holds quads li + 16c, so round r takes c = 2r and 2r + 1
+    constexpr int TS = 128 + 4;   // tile row stride (floats): 16-B aligned, b128 reads conflict-free
+    float* tile = V;
+    float* ob = maps + (size_t)b * N * R * R + (size_t)y * R + x0;
+    const float rc = 1.0f / count;
+  #pragma unroll
+    for (int r = 0; r < (QPL + 1) / 2; ++r) {
+      __syncthreads();
+  #pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const int xl = wid * PXW + 4 * g + row;
+  #pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const int c = 2 * r + h2;
+          if (c < QPL) *reinterpret_cast<f4*>(tile + xl * TS + 4 * (li + 16 * h2)) = acc[g][c] * rc;
+        }
       }
-      m = row16_max(m);
-      const f4 mb = (f4)(-m * L2E);
-      f4 sv = (f4)0.0f;
-#pragma unroll
-      for (int c = 0; c < QPL; ++c) {
-        f4 t = __builtin_elementwise_fma(zc[c], (f4)L2E, mb);
-        t.x = __builtin_amdgcn_exp2f(t.x);
-        t.y = __builtin_amdgcn_exp2f(t.y);
-        t.z = __builtin_amdgcn_exp2f(t.z);
-        t.w = __builtin_amdgcn_exp2f(t.w);
-        zc[c] = t;
-        sv += t;
+      __syncthreads();
+      const int nr = min(128, Np - 128 * r) / 4;   // quads staged this round
+      for (int e = tid; e < P * nr; e += kMapThreads) {
+        const int xl = e % P, jq = e / P;
+        if (xl >= np) continue;
+        const f4 v = *reinterpret_cast<const f4*>(tile + xl * TS + 4 * jq);
+        const int n = 128 * r + 4 * jq;
+        if (n < N) ob[(size_t)n * R * R + xl] = v.x;
+        if (n + 1 < N) ob[(size_t)(n + 1) * R * R + xl] = v.y;
+        if (n + 2 < N) ob[(size_t)(n + 2) * R * R + xl] = v.z;
+        if (n + 3 < N) ob[(size_t)(n + 3) * R * R + xl] = v.w;
       }
-      const float inv = __builtin_amdgcn_rcpf(row16_sum((sv.x + sv.y) + (sv.z + sv.w)));
-#pragma unroll
-      for (int c = 0; c < QPL; ++c) acc[g][c] = __builtin_elementwise_fma(zc[c], (f4)inv, acc[g][c]);
-      if (st && li == 0 && xl < np) st[((size_t)bh * R + y) * R + x0 + xl] = make_float2(m, inv);
-      __builtin_amdgcn_sched_barrier(0);   // keep the next pixels' LDS reads from being hoisted (registers)
-    }
-  }
-  // token-major store: round r stages tokens [128r, 128r + 128) of all P pixels in LDS; lane li
-  // of a row holds quads li + 16c, so round r takes c = 2r and 2r + 1
-  constexpr int TS = 128 + 4;   // tile row stride (floats): 16-B aligned, b128 reads conflict-free
-  float* tile = V;
-  float* ob = maps + (size_t)b * N * R * R + (size_t)y * R + x0;
-  const float rc = 1.0f / count;
-#pragma unroll
-  for (int r = 0; r < (QPL + 1) / 2; ++r) {
-    __syncthreads();
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const int xl = wid * PXW + 4 * g + row;
-#pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2) {
-        const int c = 2 * r + h2;
-        if (c < QPL) *reinterpret_cast<f4*>(tile + xl * TS + 4 * (li + 16 * h2)) = acc[g][c] * rc;
-      }
-    }
-    __syncthreads();
-    const int nr = min(128, Np - 128 * r) / 4;   // quads staged this round
-    for (int e = tid; e < P * nr; e += kMapThreads) {
-      const int xl = e % P, jq = e / P;
-      if (xl >= np) continue;
-      const f4 v = *reinterpret_cast<const f4*>(tile + xl * TS + 4 * jq);
-      const int n = 128 * r + 4 * jq;
-      if (n < N) ob[(size_t)n * R * R + xl] = v.x;
-      if (n + 1 < N) ob[(size_t)(n + 1) * R * R + xl] = v.y;
-      if (n + 2 < N) ob[(size_t)(n + 2) * R * R + xl] = v.z;
-      if (n + 3 < N) ob[(size_t)(n + 3) * R * R + xl] = v.w;
     }
   }
 }
@@ -1328,7 +1334,20 @@ void launch_maps(const CapLayers& cl, int L, int B, int H, int N, int R, int vst
   const int P = WAVES * maps_pxw(QPL);
   const int nchunks = (R + P - 1) / P;
   const int total = B * R * nchunks;
-  const int grid = 8 * ((total + 7) / 8);
+  int grid = 8 * ((total + 7) / 8);
+  // persistent grid (default; SKP_MAPS_PERSIST=0: one job per workgroup, read per call): 2
+  // workgroups per CU walk their XCD's rows in step — 1003 vs 1013 µs, FETCH_SIZE 955 vs 1070 MB
+  // at the bench shape (profiles/r03ad_maps_persist_ab.txt)
+  const char* env = getenv("SKP_MAPS_PERSIST");
+  if (!(env && atoi(env) == 0)) {
+    static const int ncu = [] {
+      int dev = 0, n = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        n = 256;
+      return std::max(8, n / 8 * 8);
+    }();
+    grid = std::min(grid, (WAVES == 8 ? 2 : 1) * ncu);   // multiple of 8
+  }
   hipLaunchKernelGGL((capture_maps_kernel<QPL, WAVES>), dim3(grid), dim3(WAVES * WAVE), lds, st, cl, L, B, H, N, R,
                      nchunks, vstride, (float)L * (float)H, maps);
 }

@@ -443,6 +443,23 @@ def test_capture_maps_fwd_vs_oracle(B, H, sizes, R, Nn):
         assert np.abs(st[..., 1] * np.exp(zu - st[..., :1]).sum(-1) - 1).max() < 2e-5
 
 
+@pytest.mark.parametrize("B,H,sizes,R,Nn", [(8, 8, (16, 16, 16, 32), 128, 500), (3, 2, (7, 13), 100, 256),
+                                            (1, 2, (8,), 32, 40)])
+def test_capture_maps_persistent_grid_equals_full_grid(monkeypatch, B, H, sizes, R, Nn):
+    """SKP_MAPS_PERSIST=1 (2 workgroups per CU striding through their XCD's jobs) gives
+    bit-identical maps and stats to the one-job-per-workgroup grid: same arithmetic and order."""
+    g = torch.Generator().manual_seed(Nn + R + B)
+    zs = [(torch.randn(B * H, s * s, Nn, generator=g) * 3).to(DEV) for s in sizes]
+    monkeypatch.setenv("SKP_MAPS_PERSIST", "1")
+    m1, s1 = _capture_maps_abi(zs, list(sizes), B, H, R)
+    monkeypatch.setenv("SKP_MAPS_PERSIST", "0")
+    m0, s0 = _capture_maps_abi(zs, list(sizes), B, H, R)
+    torch.cuda.synchronize()
+    assert torch.equal(m1, m0), (m1 - m0).abs().max().item()
+    for a, b in zip(s1, s0):
+        assert torch.equal(a, b)
+
+
 def test_capture_maps_fwd_equals_two_kernel_path_full_size():
     """At the bench shape (B=8 images × 8 heads, s = 16,16,16,32, R=128, N=500) the fused launch
     equals skp_capture_fwd + skp_aggregate per image (the r01 path, itself oracle-pinned) to
