@@ -511,6 +511,7 @@ __global__ __launch_bounds__(kColThreads) void capture_bwd_cols_kernel(const flo
 // so each XCD walks consecutive rows of one image and its L2 serves their shared z_low rows.
 constexpr float kPadLogit = -1e30f;   // Σ taps ≈ 1, so padded tokens interpolate to ≈ −1e30
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));
 
 struct CapLayers {
   const float* z[SKP_MAX_LAYERS];
@@ -552,6 +553,17 @@ constexpr int maps_pxw(int qpl) { return (32 / qpl) < 4 ? 4 : ((32 / qpl) > 16 ?
 
 #ifndef SKP_MAPS_PRIO
 #define SKP_MAPS_PRIO 1   // s_setprio level of the staging phase (0: off; 1, 2, 3 measured 972, 983, 982 vs 1003 us)
+#endif
+#ifndef SKP_MAPS_NT
+// 1: the maps and stats leave with non-temporal stores, so the 296 MB write stream does not evict
+// the z_low rows the XCD's other workgroups are about to read: 975 vs 994 µs, FETCH_SIZE 823 vs
+// 1002 MB at the bench shape (profiles/r03ae_maps_nt_ab.txt); 0 = plain stores (A/B build)
+#define SKP_MAPS_NT 1
+#endif
+#if SKP_MAPS_NT
+#define SKP_MAPS_ST(dst, v) __builtin_nontemporal_store((v), &(dst))
+#else
+#define SKP_MAPS_ST(dst, v) ((dst) = (v))
 #endif
 template <int QPL, int WAVES>
 __global__ __launch_bounds__(WAVES * WAVE) __attribute__((amdgpu_waves_per_eu(4)))
@@ -732,7 +744,10 @@ void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nc
         const float inv = __builtin_amdgcn_rcpf(row16_sum((sv.x + sv.y) + (sv.z + sv.w)));
   #pragma unroll
         for (int c = 0; c < QPL; ++c) acc[g][c] = __builtin_elementwise_fma(zc[c], (f4)inv, acc[g][c]);
-        if (st && li == 0 && xl < np) st[((size_t)bh * R + y) * R + x0 + xl] = make_float2(m, inv);
+        if (st && li == 0 && xl < np) {
+        const f2v mi = {m, inv};
+        SKP_MAPS_ST(reinterpret_cast<f2v*>(st)[((size_t)bh * R + y) * R + x0 + xl], mi);
+      }
         __builtin_amdgcn_sched_barrier(0);   // keep the next pixels' LDS reads from being hoisted (registers)
       }
     }
@@ -761,10 +776,10 @@ void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nc
         if (xl >= np) continue;
         const f4 v = *reinterpret_cast<const f4*>(tile + xl * TS + 4 * jq);
         const int n = 128 * r + 4 * jq;
-        if (n < N) ob[(size_t)n * R * R + xl] = v.x;
-        if (n + 1 < N) ob[(size_t)(n + 1) * R * R + xl] = v.y;
-        if (n + 2 < N) ob[(size_t)(n + 2) * R * R + xl] = v.z;
-        if (n + 3 < N) ob[(size_t)(n + 3) * R * R + xl] = v.w;
+        if (n < N) SKP_MAPS_ST(ob[(size_t)n * R * R + xl], v.x);
+        if (n + 1 < N) SKP_MAPS_ST(ob[(size_t)(n + 1) * R * R + xl], v.y);
+        if (n + 2 < N) SKP_MAPS_ST(ob[(size_t)(n + 2) * R * R + xl], v.z);
+        if (n + 3 < N) SKP_MAPS_ST(ob[(size_t)(n + 3) * R * R + xl], v.w);
       }
     }
   }
