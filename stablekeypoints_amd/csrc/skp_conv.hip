@@ -928,7 +928,8 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
         const float bv = (EPI & 1) ? bias[k] : 0.0f;
         const size_t o = (((size_t)img * K + k) * Ho + y0 / 2 + row) * Wo + x0 / 2 + 4 * c4;
         const float4 v = make_float4(pp[0] + bv, pp[2] + bv, pp[4] + bv, pp[6] + bv);
-        if (!(dbg & 64)) *reinterpret_cast<float4*>(y + o) = v;
+        if (dbg & 128) __builtin_nontemporal_store(f32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<f32x4*>(y + o));
+        else if (!(dbg & 64)) *reinterpret_cast<float4*>(y + o) = v;
       }
       if (blk == 0) __syncthreads();
       continue;
@@ -957,7 +958,8 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
         v.z += rv.z;
         v.w += rv.w;
       }
-      if (!(dbg & 64)) *reinterpret_cast<float4*>(y + o) = v;
+      if (dbg & 128) __builtin_nontemporal_store(f32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<f32x4*>(y + o));
+      else if (!(dbg & 64)) *reinterpret_cast<float4*>(y + o) = v;
     }
     if (blk == 0) __syncthreads();
   }
@@ -1053,6 +1055,21 @@ extern "C" int skp_wino2_weights(const float* w, int K, int C, int flip, float* 
 // zero row / column past the bottom-right edge, which is exactly the stride-1, pad-1 convolution sampled at
 // the odd positions (2oy + 1, 2ox + 1).  The Winograd kernel computes the 32×32 blocks and its epilogue
 // stores only the odd rows / columns (+ bias): no padded copy, no NCHW↔NHWC transposes, no bias pass.
+namespace {
+// flag 128 of the kernels' dbg word: non-temporal output stores, for outputs larger than the
+// Infinity Cache (the next layer re-reads them from HBM either way; the stream then does not
+// evict the input regions / weights the other workgroups re-read from L2).  SKP_WINO_NT: 0 off,
+// 2 always, default 1 = outputs ≥ SKP_WINO_NT_MB (256) MB; read per call.
+int wino_nt_flag(long long out_bytes, int nsplit) {
+  if (nsplit > 1) return 0;   // split-K partials are re-read by the reduction
+  const char* e = getenv("SKP_WINO_NT");
+  const int mode = e ? atoi(e) : 1;
+  const char* m = getenv("SKP_WINO_NT_MB");
+  const long long thr = (m ? atoll(m) : 256) << 20;
+  return (mode == 2 || (mode == 1 && out_bytes >= thr)) ? 128 : 0;
+}
+}  // namespace
+
 extern "C" int skp_conv3x3s2_wino2(const float* x, const float* U, const float* bias, float* y, int B, int C, int K,
                                    int H, int W, int nsplit, float* ws, void* stream) {
   SKP_CHECK_ARG(x && U && y, "null pointer");
@@ -1072,12 +1089,13 @@ extern "C" int skp_conv3x3s2_wino2(const float* x, const float* U, const float* 
   float* out = nsplit > 1 ? ws : y;
   hipStream_t st = as_stream(stream);
   const dim3 grid((unsigned)(nblk * nkb * nsplit));
+  const int fl = dbg | wino_nt_flag((long long)B * K * (H / 2) * (W / 2) * 4, nsplit);
   if (nsplit == 1 && bias)
     hipLaunchKernelGGL((wino2_kernel<5, 8>), grid, dim3(w2::kThreads), 0, st, x, U, bias, nullptr, out, B, C, K, H, W,
-                       bw, bpi, (int)nblk, nkb, 0, C / nsplit, dbg);
+                       bw, bpi, (int)nblk, nkb, 0, C / nsplit, fl);
   else
     hipLaunchKernelGGL((wino2_kernel<4, 8>), grid, dim3(w2::kThreads), 0, st, x, U, nullptr, nullptr, out, B, C, K, H,
-                       W, bw, bpi, (int)nblk, nkb, 0, C / nsplit, dbg);
+                       W, bw, bpi, (int)nblk, nkb, 0, C / nsplit, fl);
   SKP_LAUNCH_CHECK();
   if (nsplit > 1) return splitk_reduce(ws, nsplit, B, K, (H / 2) * (W / 2), bias, nullptr, y, st);
   return SKP_OK;
@@ -1113,13 +1131,14 @@ extern "C" int skp_conv3x3_wino2(const float* x, const float* U, const float* bi
   float* out = nsplit > 1 ? ws : y;
   hipStream_t st = as_stream(stream);
   const dim3 grid((unsigned)(nblk * nkb * nsplit));
+  const int fl = dbg | wino_nt_flag((long long)B * K * H * W * 4, nsplit);
 #define SKP_WG2(E)                                                                                            \
   if (g16)                                                                                                    \
     hipLaunchKernelGGL((wino2_kernel<E, 4>), grid, dim3(w2::kThreads), 0, st, x, U, bias, residual, out, B, C, K, \
-                       H, W, bw, bpi, (int)nblk, nkb, kb_major, C / nsplit, dbg);                             \
+                       H, W, bw, bpi, (int)nblk, nkb, kb_major, C / nsplit, fl);                              \
   else                                                                                                        \
     hipLaunchKernelGGL((wino2_kernel<E, 8>), grid, dim3(w2::kThreads), 0, st, x, U, bias, residual, out, B, C, K, \
-                       H, W, bw, bpi, (int)nblk, nkb, kb_major, C / nsplit, dbg)
+                       H, W, bw, bpi, (int)nblk, nkb, kb_major, C / nsplit, fl)
   switch (epi) {
     case 0: SKP_WG2(0); break;
     case 1: SKP_WG2(1); break;
