@@ -669,6 +669,48 @@ def test_prefetched_vae_pass_equals_inline():
     assert np.allclose(res[False][2], res[True][2], rtol=1e-4, atol=1e-8)
 
 
+def test_prefetch_behind_capture_backward_equals_prefetch_before_backward():
+    """micro_steps(images, prefetch=[next]) with the next pass's VAE enqueued by the sparse capture
+    backward's hook (prefetch_at="capture_bwd", the default) or before the backward ("bwd"): the
+    same thetas (CPU generator order unchanged), indices, losses and gradients over two passes."""
+    from stablekeypoints_amd.optimize import TokenOptimizer
+    from stablekeypoints_amd.optimize_token import load_ldm
+    from stablekeypoints_amd.sd import TINY_CONFIG, TINY_IMAGE
+    lat = TINY_IMAGE // 8
+    noise = torch.randn(4, 4, lat, lat, generator=torch.Generator().manual_seed(4)).to(DEV)
+    imgs = [torch.from_numpy(recipes.uniform(90 + i, (1, 3, TINY_IMAGE, TINY_IMAGE))).to(DEV) for i in range(4)]
+    res = {}
+    for where in ("capture_bwd", "bwd"):
+        ldm, ctls, _ = load_ldm(DEV, "tiny", feature_upsample_res=32, config=TINY_CONFIG)
+        inner = ldm.scheduler
+
+        class Sched:
+            timesteps = inner.timesteps
+
+            def add_noise(self, x, n, t):
+                return inner.add_noise(x, noise, t)
+        ldm.scheduler = Sched()
+        ctx = torch.from_numpy(recipes.random_logits(53, (1, 16, 32))).to(DEV)
+        torch.manual_seed(7)
+        opt = TokenOptimizer(ldm, ctls, ctx, top_k=4, furthest_point_num_samples=8, accum=4, device=DEV)
+        opt.prefetch_at = where
+        a, b = imgs[:2], imgs[2:]
+        opt.prefetch(a)
+        i1 = opt.micro_steps(a, prefetch=[b])
+        assert len(opt._prefetched) == 1          # b's VAE is queued
+        th1 = opt.transform.last_params["theta"].clone()
+        i2 = opt.micro_steps(b)
+        assert not opt._prefetched
+        th2 = opt.transform.last_params["theta"].clone()
+        res[where] = ([N(t) for t in i1 + i2], float(opt.run_tot), N(opt.context.grad), N(th1), N(th2))
+    x, y = res["capture_bwd"], res["bwd"]
+    for p, q in zip(x[0], y[0]):
+        assert np.array_equal(p, q)
+    assert np.array_equal(x[3], y[3]) and np.array_equal(x[4], y[4])
+    assert abs(x[1] - y[1]) <= 1e-6 * abs(y[1])
+    assert np.allclose(x[2], y[2], rtol=1e-4, atol=1e-8)
+
+
 # ----------------------------------------------------------------------------- UNet-side GroupNorm(+SiLU)
 @pytest.mark.parametrize("B,C,H,W,G,act,shifted", [(2, 320, 64, 64, 32, True, True), (2, 1280, 8, 8, 32, False, False),
                                                    (1, 128, 256, 256, 32, True, False), (2, 12, 5, 7, 4, True, True),
