@@ -69,6 +69,8 @@ def _case(seed, B, H, sizes, R, Nn, K, dup=False, ragged=False):
     (1, 2, (8,), 128, 132, 3, False, False),              # R = 16·s, N past one 128-token chunk
     (2, 3, (5, 3), 40, 36, 4, True, True),                # no compiled kernel: dense fallback
     (1, 2, (16,), 32, 20, 2, False, False),               # R = 2·s: dense fallback
+    (2, 2, (4, 8, 16), 64, 64, 32, True, True),           # K = 32 (the maximum), three sizes in one launch
+    (1, 3, (16, 8, 16, 32), 128, 8, 1, False, False),     # K = 1, N = 8 (one short token chunk), mixed sizes
 ])
 def test_capture_maps_bwd_sel_vs_oracle(B, H, sizes, R, Nn, K, dup, ragged):
     zs, tok, gsel = _case(500 + Nn + R, B, H, sizes, R, Nn, K, dup, ragged)
