@@ -503,12 +503,20 @@ template <>
 struct Geo<4> {
   static constexpr int NI = 4, RR = 18, RC = 6, CHF = 1744;
 };
-template <int TXB>
-struct GeoT : Geo<TXB> {
-  using Geo<TXB>::NI;
-  using Geo<TXB>::RR;
-  using Geo<TXB>::RC;
-  using Geo<TXB>::CHF;
+// NW = 4 with TXB 8: a half-height block (8 × 4 tiles = 32 × 16 pixels, 4 waves), so that two
+// workgroups share a CU and one's prologue / epilogue overlaps the other's stage loop
+template <int TXB, int NW>
+struct GeoN : Geo<TXB> {};
+template <>
+struct GeoN<8, 4> {
+  static constexpr int NI = 1, RR = 18, RC = 10, CHF = 768;   // same bank residues as 1408
+};
+template <int TXB, int NW = 8>
+struct GeoT : GeoN<TXB, NW> {
+  using GeoN<TXB, NW>::NI;
+  using GeoN<TXB, NW>::RR;
+  using GeoN<TXB, NW>::RC;
+  using GeoN<TXB, NW>::CHF;
   static constexpr int RF = 4 * RC;                                   // floats per region row
   static constexpr int RAWF = (4 * CHF + 255) / 256 * 256;            // raw slot, whole 1-KB chunks
   static constexpr int RAW_INSTR = RAWF / 256;
@@ -687,6 +695,10 @@ struct W2Smem {
 __device__ __forceinline__ void w2_vmcnt(int n) {
   switch (n) {
     case 0: W2_VMCNT(0); break;
+    case 1: W2_VMCNT(1); break;
+    case 2: W2_VMCNT(2); break;
+    case 3: W2_VMCNT(3); break;
+    case 4: W2_VMCNT(4); break;
     case 5: W2_VMCNT(5); break;
     case 6: W2_VMCNT(6); break;
     case 7: W2_VMCNT(7); break;
@@ -708,24 +720,29 @@ __device__ __forceinline__ void w2_vmcnt(int n) {
 
 // One wave's whole program for transform half HH (rows 3HH..3HH+2); the kernel branches once
 // on the wave's half so the stage loop is straight-line code for each.
-template <int EPI, int HH, int TXB>
+template <int EPI, int HH, int TXB, int NW>
 __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __restrict__ x, const float* __restrict__ U,
                                            const float* __restrict__ bias, const float* __restrict__ res,
                                            float* __restrict__ y, int C, int K, int H, int W, int img, int x0,
                                            int y0, int kb, int c0, int csplit, int wv, int dbg) {
-  using Geo = w2::GeoT<TXB>;
+  using Geo = w2::GeoT<TXB, NW>;
   constexpr int kChF = Geo::CHF, kRowF = Geo::RF, kRawInstr = Geo::RAW_INSTR, NI = Geo::NI, RR = Geo::RR,
                 RC = Geo::RC;
   constexpr int kInstr = kRawInstr + w2::kUInstr;
-  constexpr int kMaxRaw = (kRawInstr + 7) / 8;
+  constexpr int kMaxRaw = (kRawInstr + NW - 1) / NW;
+  constexpr int kMaxU = (w2::kUInstr + NW - 1) / NW + 1;
+  constexpr int NT = NW * WAVE;
+  // weight ring: 3 slots (lead 2) with 8 waves; 2 (lead 1) in the half-height form, whose LDS must
+  // leave room for a second workgroup on the CU
+  constexpr int US = NW == 4 ? 2 : 3;
   using w2::kUF;
   using w2::kUP;
   // raw-input ring of RS slots (lead RS − 1 stages: the input streams from HBM), weight ring
   // of 3 (lead 2: the weights are re-read by every tile block and hit L2)
-  constexpr int RS = (TXB == 8 && SKP_W2_RS4) ? 4 : 3;
+  constexpr int RS = (TXB == 8 && NW == 8 && SKP_W2_RS4) ? 4 : 3;
   float *R0 = sm.R0, *R1 = sm.R1, *R2 = sm.R2, *U0 = sm.U0, *U1 = sm.U1, *U2 = sm.U2;
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wm = wv & 3;
+  const int wm = wv % (NW / 2);
   const size_t plane = (size_t)H * W;
   const size_t ximg = (size_t)img * C * plane;
 
@@ -735,7 +752,7 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
   int nraw = 0;
 #pragma unroll
   for (int m = 0; m < kMaxRaw; ++m) {
-    const int gi = wv + 8 * m;
+    const int gi = wv + NW * m;
     voff[m] = w2::kOOB;
     if (gi < kRawInstr) {
       ++nraw;
@@ -749,12 +766,13 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
         voff[m] = (unsigned)((ximg + ((size_t)ii * C + ch) * plane + (size_t)yy * W + xx) * 4);
     }
   }
-  const int nuw = (kInstr - 1 - wv) / 8 + 1 - nraw;   // U chunks of this wave
-  const int ufirst = wv + 8 * nraw - kRawInstr;       // its first U chunk
+  const int nuw = (kInstr - 1 - wv) / NW + 1 - nraw;  // U chunks of this wave
+  const int ufirst = wv + NW * nraw - kRawInstr;      // its first U chunk
   // vmcnt allowances (in-order counter; per step the wave issues U(s+2) then raw(s+RS)):
   // top of step s needs U(s) and raw(s+1) landed; the prologue needs raw(0)
-  const int allow_step = RS == 4 ? nuw + 2 * nraw : nuw + nraw;
-  const int allow_pro = RS == 4 ? 2 * nuw + 3 * nraw : 2 * nuw + 2 * nraw;
+  // (US = 2: per step U(s+1) then raw(s+3); the top of step s needs U(s) and raw(s+1), the prologue raw(0))
+  const int allow_step = US == 2 ? nraw : RS == 4 ? nuw + 2 * nraw : nuw + nraw;
+  const int allow_pro = US == 2 ? nuw + 2 * nraw : RS == 4 ? 2 * nuw + 3 * nraw : 2 * nuw + 2 * nraw;
   const size_t xend = (size_t)(img + NI) * C * plane; // the buffer ends with the block's last image
   const float* Ub = U + ((size_t)kb * C + c0) * w2::kNC * kUP;
   const int nst = csplit / w2::kCK;
@@ -768,15 +786,15 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
 #pragma unroll
     for (int m = 0; m < kMaxRaw; ++m)
       if (m < nraw && !(dbg & 4))
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)(rs_lds + 256 * (wv + 8 * m)), 16, voff[m], 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)(rs_lds + 256 * (wv + NW * m)), 16, voff[m], 0, 0, 0);
   };
   auto issue_u = [&](int t, float* us_lds) {
     const __amdgpu_buffer_rsrc_t ru =
         __builtin_amdgcn_make_buffer_rsrc((void*)(Ub + (size_t)t * kUF), (short)0, kUF * 4, 0x00020000);
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
+    for (int m = 0; m < kMaxU; ++m)
       if (m < nuw && !(dbg & 8)) {
-        const int q = ufirst + 8 * m;
+        const int q = ufirst + NW * m;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(ru, (lds_ptr_t)(us_lds + 256 * q), 16, lane * 16, q * 1024, 0, 0);
       }
   };
@@ -824,7 +842,7 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
   if (RS == 4) issue_raw(1, R1);
   issue_u(0, U0);
   issue_raw(RS - 2, RS == 4 ? R2 : R1);
-  if (nst > 1) issue_u(1, U1);
+  if (US == 3 && nst > 1) issue_u(1, U1);
   issue_raw(RS - 1, RS == 4 ? sm.R3 : R2);
   w2_vmcnt(nst > 1 ? allow_pro : 0);
   __syncthreads();
@@ -836,7 +854,7 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
   auto step = [&](int s, float* Rn, float* Us, float* Ri, float* Ui, const float (&acur)[18], float (&anext)[18]) {
     w2_vmcnt(s + 1 < nst ? allow_step : 0);
     __syncthreads();
-    if (s + 2 < nst) issue_u(s + 2, Ui);
+    if (s + US - 1 < nst) issue_u(s + US - 1, Ui);
     issue_raw(s + RS, Ri);   // past the last stage: empty (zero-length) loads keep the counts
     const bool tr = s + 1 < nst && !(dbg & 1);
     if (HH == 0) {
@@ -852,12 +870,12 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
   float* const Rsl[4] = {R0, R1, R2, sm.R3};
   float* const Usl[3] = {U0, U1, U2};
   for (int s0 = 0; s0 < ((dbg & 16) ? 0 : nst); s0 += PER) {
-    step(s0, Rsl[1 % RS], Usl[0], Rsl[0], Usl[2], a0, a1);
+    step(s0, Rsl[1 % RS], Usl[0], Rsl[0], Usl[US - 1], a0, a1);
 #pragma unroll
     for (int j = 1; j < PER; ++j) {
       if (s0 + j < nst) {
-        if ((j & 1) == 0) step(s0 + j, Rsl[(j + 1) % RS], Usl[j % 3], Rsl[j % RS], Usl[(j + 2) % 3], a0, a1);
-        else step(s0 + j, Rsl[(j + 1) % RS], Usl[j % 3], Rsl[j % RS], Usl[(j + 2) % 3], a1, a0);
+        if ((j & 1) == 0) step(s0 + j, Rsl[(j + 1) % RS], Usl[j % US], Rsl[j % RS], Usl[(j + US - 1) % US], a0, a1);
+        else step(s0 + j, Rsl[(j + 1) % RS], Usl[j % US], Rsl[j % RS], Usl[(j + US - 1) % US], a1, a0);
       }
     }
   }
@@ -871,9 +889,10 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
   if (dbg & 32) return;
   // channel c of a block: a 32×32-float plane in R0/R1/R2/U0 (four channels each, skewed by 16
   // floats per buffer so the 8-lane store groups hit distinct banks)
+  constexpr int PH = (TXB == 8 && NW == 4) ? 16 : 32;   // plane rows (TXB 8: the block's pixel rows)
   auto plane_of = [&](int c) -> float* {
     float* b = (c >> 2) == 0 ? R0 : (c >> 2) == 1 ? R1 : (c >> 2) == 2 ? R2 : U0;
-    return b + (c & 3) * 1028 + (c >> 2) * 16;
+    return b + (c & 3) * (PH * 32 + 4) + (c >> 2) * 16;
   };
   // this lane's output tile row within the 1024-float plane: TXB 8: tiles (2wm + lane>>5, 4((lane>>4)&1)
   // + r) of the 32×32 block; TXB 4: image wm (256 floats), tile row lane>>4, tiles r = 0..3
@@ -916,12 +935,13 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
     if constexpr ((EPI & 4) != 0) {
       // stride-2 output (EPI bit 2, TXB 8): the block's odd rows / columns, a 16×16 block of the
       // (H/2, W/2) output per channel = 16 channels × 64 float4, two per thread
-      static_assert(TXB == 8 && (EPI & 2) == 0, "stride-2 output: 32×32 blocks, no residual");
+      static_assert(TXB == 8 && (EPI & 2) == 0, "stride-2 output: 32-wide blocks, no residual");
       const int Ho = H / 2, Wo = W / 2;
+      constexpr int PC2 = (PH / 2) * 4;   // float4 per channel of the block's stride-2 output
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int idx = i * w2::kThreads + tid;
-        const int c = idx >> 6, q = idx & 63;
+      for (int i = 0; i < 16 * PC2 / NT; ++i) {
+        const int idx = i * NT + tid;
+        const int c = idx / PC2, q = idx % PC2;
         const int row = q >> 2, c4 = q & 3;
         const float* pp = plane_of(c) + (2 * row + 1) * 32 + 8 * c4 + 1;
         const int k = kb * w2::kNC + 16 * blk + c;
@@ -936,10 +956,11 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
     }
     // 16 channels × 1024 floats in 16-B chunks; a wave instruction = 1 KB of one channel:
     // TXB 8: 8 whole rows of the 32×32 block; TXB 4: one whole 16×16 image plane
+    constexpr int PCF = TXB == 8 ? PH * 8 : 256;   // float4 per channel plane
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int idx = i * w2::kThreads + tid;
-      const int c = idx >> 8, q = idx & 255;
+    for (int i = 0; i < 16 * PCF / NT; ++i) {
+      const int idx = i * NT + tid;
+      const int c = idx / PCF, q = idx % PCF;
       const float4 v0 = *reinterpret_cast<const float4*>(plane_of(c) + 4 * q);
       const int k = kb * w2::kNC + 16 * blk + c;
       const float bv = (EPI & 1) ? bias[k] : 0.0f;
@@ -965,16 +986,16 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
   }
 }
 
-template <int EPI, int TXB>
-__global__ __launch_bounds__(w2::kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void wino2_kernel(
+template <int EPI, int TXB, int NW = 8>
+__global__ __launch_bounds__(NW * WAVE) __attribute__((amdgpu_waves_per_eu(2, 2))) void wino2_kernel(
     const float* __restrict__ x, const float* __restrict__ U, const float* __restrict__ bias,
     const float* __restrict__ res, float* __restrict__ y, int nimg, int C, int K, int H, int W, int bw, int bpi,
     int nblk, int nkb, int kb_major, int csplit, int dbg) {
   // separate LDS objects per ring slot: the compiler tells a DMA into one slot from a ds_read of
   // another and does not wait for outstanding DMAs before every LDS read
-  __shared__ __attribute__((aligned(16))) float R0[w2::GeoT<TXB>::RAWF], R1[w2::GeoT<TXB>::RAWF],
-      R2[w2::GeoT<TXB>::RAWF], R3[(TXB == 8 && SKP_W2_RS4) ? w2::GeoT<TXB>::RAWF : 4];
-  __shared__ __attribute__((aligned(16))) float U0[w2::kUF], U1[w2::kUF], U2[w2::kUF];
+  __shared__ __attribute__((aligned(16))) float R0[w2::GeoT<TXB, NW>::RAWF], R1[w2::GeoT<TXB, NW>::RAWF],
+      R2[w2::GeoT<TXB, NW>::RAWF], R3[(TXB == 8 && NW == 8 && SKP_W2_RS4) ? w2::GeoT<TXB, NW>::RAWF : 4];
+  __shared__ __attribute__((aligned(16))) float U0[w2::kUF], U1[w2::kUF], U2[NW == 4 ? 4 : w2::kUF];
   // workgroup → (input-channel split, 32×32-pixel block, channel block); consecutive logical ids
   // share one XCD.  A split sums its csplit input channels into slab sp of y (the workspace).
   const int G = gridDim.x;
@@ -998,15 +1019,15 @@ __global__ __launch_bounds__(w2::kThreads) __attribute__((amdgpu_waves_per_eu(2,
     const int br = tb - img * bpi;
     const int by = br / bw;
     x0 = 32 * (br - by * bw);
-    y0 = 32 * by;
+    y0 = (NW == 4 ? 16 : 32) * by;
   } else {
     img = 4 * tb;
   }
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const W2Smem sm{R0, R1, R2, R3, U0, U1, U2};
   const int c0 = sp * csplit;
-  if (wv < 4) wino2_body<EPI, 0, TXB>(sm, x, U, bias, res, y, C, K, H, W, img, x0, y0, kb, c0, csplit, wv, dbg);
-  else wino2_body<EPI, 1, TXB>(sm, x, U, bias, res, y, C, K, H, W, img, x0, y0, kb, c0, csplit, wv, dbg);
+  if (wv < NW / 2) wino2_body<EPI, 0, TXB, NW>(sm, x, U, bias, res, y, C, K, H, W, img, x0, y0, kb, c0, csplit, wv, dbg);
+  else wino2_body<EPI, 1, TXB, NW>(sm, x, U, bias, res, y, C, K, H, W, img, x0, y0, kb, c0, csplit, wv, dbg);
 }
 
 // U2[kb][c][k%32][40]: positions 0..17 at 0..17, 18..35 at 20..37, the rest zero
@@ -1081,7 +1102,9 @@ extern "C" int skp_conv3x3s2_wino2(const float* x, const float* U, const float* 
   SKP_CHECK_ARG(nsplit == 1 || ws, "split-K needs a workspace of nsplit·B·K·(H/2)·(W/2) floats");
   SKP_CHECK_ARG(aligned16(x) && aligned16(U) && aligned16(y) && (!ws || aligned16(ws)), "tensors must be 16-byte aligned");
   SKP_CHECK_ARG((long long)B * C * H * W * 4 < 0x7fffffffLL, "input larger than 2 GiB (32-bit buffer offsets)");
-  const int bw = W / 32, bpi = (H / 32) * bw;
+  const char* he = getenv("SKP_WINO2_HALF");   // half-height blocks (see skp_conv3x3_wino2)
+  const bool half = !(he && atoi(he) == 0);
+  const int bw = W / 32, bpi = (H / (half ? 16 : 32)) * bw;
   const long long nblk = (long long)B * bpi;
   const int nkb = K / w2::kNC;
   SKP_CHECK_ARG(nblk * nkb * nsplit <= 0x7fffffffLL, "grid too large");
@@ -1090,7 +1113,13 @@ extern "C" int skp_conv3x3s2_wino2(const float* x, const float* U, const float* 
   hipStream_t st = as_stream(stream);
   const dim3 grid((unsigned)(nblk * nkb * nsplit));
   const int fl = dbg | wino_nt_flag((long long)B * K * (H / 2) * (W / 2) * 4, nsplit);
-  if (nsplit == 1 && bias)
+  if (half && nsplit == 1 && bias)
+    hipLaunchKernelGGL((wino2_kernel<5, 8, 4>), grid, dim3(4 * WAVE), 0, st, x, U, bias, nullptr, out, B, C, K, H, W,
+                       bw, bpi, (int)nblk, nkb, 0, C / nsplit, fl);
+  else if (half)
+    hipLaunchKernelGGL((wino2_kernel<4, 8, 4>), grid, dim3(4 * WAVE), 0, st, x, U, nullptr, nullptr, out, B, C, K, H,
+                       W, bw, bpi, (int)nblk, nkb, 0, C / nsplit, fl);
+  else if (nsplit == 1 && bias)
     hipLaunchKernelGGL((wino2_kernel<5, 8>), grid, dim3(w2::kThreads), 0, st, x, U, bias, nullptr, out, B, C, K, H, W,
                        bw, bpi, (int)nblk, nkb, 0, C / nsplit, fl);
   else
@@ -1116,7 +1145,12 @@ extern "C" int skp_conv3x3_wino2(const float* x, const float* U, const float* bi
                     (!ws || aligned16(ws)),
                 "tensors must be 16-byte aligned");
   SKP_CHECK_ARG((long long)B * C * H * W * 4 < 0x7fffffffLL, "input larger than 2 GiB (32-bit buffer offsets)");
-  const int bw = W / 32, bpi = (H / 32) * bw;
+  // half-height blocks (32 × 16 pixels, 4 waves, two workgroups per CU: one's prologue / epilogue
+  // overlaps the other's stage loop): the default, 5-11% faster at every VAE / UNet shape
+  // (profiles/r03al_wino_half_ab.txt); SKP_WINO2_HALF=0 = the 32 × 32 single-workgroup form
+  const char* he = getenv("SKP_WINO2_HALF");
+  const bool half = !g16 && !(he && atoi(he) == 0);
+  const int bw = W / 32, bpi = (H / (half ? 16 : 32)) * bw;
   const long long nblk = g16 ? B / 4 : (long long)B * bpi;
   const int nkb = K / w2::kNC;
   SKP_CHECK_ARG(nblk * nkb * nsplit <= 0x7fffffffLL, "grid too large");
@@ -1135,6 +1169,9 @@ extern "C" int skp_conv3x3_wino2(const float* x, const float* U, const float* bi
 #define SKP_WG2(E)                                                                                            \
   if (g16)                                                                                                    \
     hipLaunchKernelGGL((wino2_kernel<E, 4>), grid, dim3(w2::kThreads), 0, st, x, U, bias, residual, out, B, C, K, \
+                       H, W, bw, bpi, (int)nblk, nkb, kb_major, C / nsplit, fl);                              \
+  else if (half)                                                                                              \
+    hipLaunchKernelGGL((wino2_kernel<E, 8, 4>), grid, dim3(4 * WAVE), 0, st, x, U, bias, residual, out, B, C, K,  \
                        H, W, bw, bpi, (int)nblk, nkb, kb_major, C / nsplit, fl);                              \
   else                                                                                                        \
     hipLaunchKernelGGL((wino2_kernel<E, 8>), grid, dim3(w2::kThreads), 0, st, x, U, bias, residual, out, B, C, K, \
