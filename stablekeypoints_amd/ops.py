@@ -1097,6 +1097,10 @@ WINO_MIN_WORKGROUPS = 128
 WINO_KERNEL = os.environ.get("SKP_WINO", "auto")
 WINO_SPLIT = os.environ.get("SKP_WINO_SPLIT", "1") != "0"
 WINO_WIDE = os.environ.get("SKP_WINO_WIDE", "1") != "0"   # must match skp_conv3x3_wino's rule
+# half-height Winograd blocks (libskp's default for H, W multiples of 32; SKP_WINO2_HALF=0 off):
+# the split-K planner models two co-resident workgroups per CU for them
+WINO2_HALF = os.environ.get("SKP_WINO2_HALF", "1") != "0"
+WINO_PLAN_HALF = os.environ.get("SKP_WINO_PLAN_HALF", "1") != "0"   # 0: the one-workgroup-per-CU cost model (A/B)
 
 
 def _wino_v2(H, W, B=None):
@@ -1140,8 +1144,16 @@ def _wino_plan_uncached(B, C, K, H, W, force):
     else:
         wgs = -(-(B * (H // 4) * (W // 4)) // 64) * (K // 32)
     out_bytes = B * K * H * W * 4
+    half = v2 and H != 16 and WINO2_HALF and WINO_PLAN_HALF
 
     def cost(s):
+        if half:
+            # half-height blocks (2·wgs workgroups, two co-resident per CU): a CU holding k of them
+            # runs ⌊k/2⌋ pairs at ≈1.72 µs per stage and a lone one at ≈1.48; the partial sums
+            # cost (s + 1) passes at ≈2 TB/s (fitted to the split sweep, profiles/r03am_split_sweep.txt)
+            k = -(-2 * wgs * s // 256)
+            st = C // s // 4
+            return (k // 2) * st * 1.72e-6 + (k % 2) * st * 1.48e-6 + (s > 1) * (s + 1) * out_bytes / 2e12
         rounds = -(-wgs * s // 256)
         return rounds * ((C // s // 4) * 2.4e-6 + 5e-6) + (s > 1) * (s + 1) * out_bytes / 5e12
 
@@ -1161,7 +1173,7 @@ def _wino_plan(B, C, K, H, W):
     """_wino_plan_uncached, memoised per shape (and the module switches it reads): the planner's
     32-candidate cost loop ran in Python on every convolution call, ~1500 launches per step."""
     force = int(os.environ.get("SKP_WINO_NSPLIT", "0"))
-    key = (B, C, K, H, W, force, WINO_KERNEL, WINO_SPLIT, WINO_WIDE)
+    key = (B, C, K, H, W, force, WINO_KERNEL, WINO_SPLIT, WINO_WIDE, WINO2_HALF, WINO_PLAN_HALF)
     plan = _WINO_PLANS.get(key)
     if plan is None:
         plan = _WINO_PLANS[key] = _wino_plan_uncached(B, C, K, H, W, force)
