@@ -511,6 +511,12 @@ template <>
 struct GeoN<8, 4> {
   static constexpr int NI = 1, RR = 18, RC = 10, CHF = 768;   // same bank residues as 1408
 };
+// NW = 4 with TXB 4: two whole 16×16 images per workgroup (4 waves); CHF/4 ≡ 12 (mod 16) keeps
+// the patch reads' ds_read_b128 lane groups conflict-free like 1744 (≡ 4)
+template <>
+struct GeoN<4, 4> {
+  static constexpr int NI = 2, RR = 18, RC = 6, CHF = 880;
+};
 template <int TXB, int NW = 8>
 struct GeoT : GeoN<TXB, NW> {
   using GeoN<TXB, NW>::NI;
@@ -739,7 +745,7 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
   using w2::kUP;
   // raw-input ring of RS slots (lead RS − 1 stages: the input streams from HBM), weight ring
   // of 3 (lead 2: the weights are re-read by every tile block and hit L2)
-  constexpr int RS = (TXB == 8 && NW == 8 && SKP_W2_RS4) ? 4 : 3;
+  constexpr int RS = (TXB == 4 && NW == 4) ? 2 : (TXB == 8 && NW == 8 && SKP_W2_RS4) ? 4 : 3;
   float *R0 = sm.R0, *R1 = sm.R1, *R2 = sm.R2, *U0 = sm.U0, *U1 = sm.U1, *U2 = sm.U2;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wm = wv % (NW / 2);
@@ -771,8 +777,10 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
   // vmcnt allowances (in-order counter; per step the wave issues U(s+2) then raw(s+RS)):
   // top of step s needs U(s) and raw(s+1) landed; the prologue needs raw(0)
   // (US = 2: per step U(s+1) then raw(s+3); the top of step s needs U(s) and raw(s+1), the prologue raw(0))
-  const int allow_step = US == 2 ? nraw : RS == 4 ? nuw + 2 * nraw : nuw + nraw;
-  const int allow_pro = US == 2 ? nuw + 2 * nraw : RS == 4 ? 2 * nuw + 3 * nraw : 2 * nuw + 2 * nraw;
+  // (RS = 2, US = 2: per step U(s+1) then raw(s+2), the top of step s waits for both of the
+  // previous step's; the prologue issues raw(0), U(0), raw(1) and waits for raw(0))
+  const int allow_step = RS == 2 ? 0 : US == 2 ? nraw : RS == 4 ? nuw + 2 * nraw : nuw + nraw;
+  const int allow_pro = RS == 2 ? nuw + nraw : US == 2 ? nuw + 2 * nraw : RS == 4 ? 2 * nuw + 3 * nraw : 2 * nuw + 2 * nraw;
   const size_t xend = (size_t)(img + NI) * C * plane; // the buffer ends with the block's last image
   const float* Ub = U + ((size_t)kb * C + c0) * w2::kNC * kUP;
   const int nst = csplit / w2::kCK;
@@ -841,9 +849,9 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
   issue_raw(0, R0);
   if (RS == 4) issue_raw(1, R1);
   issue_u(0, U0);
-  issue_raw(RS - 2, RS == 4 ? R2 : R1);
+  if (RS >= 3) issue_raw(RS - 2, RS == 4 ? R2 : R1);
   if (US == 3 && nst > 1) issue_u(1, U1);
-  issue_raw(RS - 1, RS == 4 ? sm.R3 : R2);
+  issue_raw(RS - 1, RS == 4 ? sm.R3 : RS == 3 ? R2 : R1);
   w2_vmcnt(nst > 1 ? allow_pro : 0);
   __syncthreads();
   w2::W2_TRANSFORM<HH, kRowF>(R0 + roff, a0);
@@ -866,7 +874,7 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
     }
   };
   // unrolled by lcm(RS, 3, 2): raw slot s%RS, U slot s%3, A-operand buffer s%2
-  constexpr int PER = RS == 4 ? 12 : 6;
+  constexpr int PER = RS == 4 ? 12 : RS == 2 ? 2 : 6;
   float* const Rsl[4] = {R0, R1, R2, sm.R3};
   float* const Usl[3] = {U0, U1, U2};
   for (int s0 = 0; s0 < ((dbg & 16) ? 0 : nst); s0 += PER) {
@@ -890,9 +898,13 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
   // channel c of a block: a 32×32-float plane in R0/R1/R2/U0 (four channels each, skewed by 16
   // floats per buffer so the 8-lane store groups hit distinct banks)
   constexpr int PH = (TXB == 8 && NW == 4) ? 16 : 32;   // plane rows (TXB 8: the block's pixel rows)
+  // plane stride: TXB 8 the block's PH × 32 pixels, TXB 4 its NI 16×16 images (+4 skew); with a
+  // 2-slot raw ring the third plane buffer is U1 (no R2)
+  constexpr int PLS = (TXB == 8 ? PH * 32 : NI * 256) + 4;
+  float* const P2 = RS == 2 ? U1 : R2;
   auto plane_of = [&](int c) -> float* {
-    float* b = (c >> 2) == 0 ? R0 : (c >> 2) == 1 ? R1 : (c >> 2) == 2 ? R2 : U0;
-    return b + (c & 3) * (PH * 32 + 4) + (c >> 2) * 16;
+    float* b = (c >> 2) == 0 ? R0 : (c >> 2) == 1 ? R1 : (c >> 2) == 2 ? P2 : U0;
+    return b + (c & 3) * PLS + (c >> 2) * 16;
   };
   // this lane's output tile row within the 1024-float plane: TXB 8: tiles (2wm + lane>>5, 4((lane>>4)&1)
   // + r) of the 32×32 block; TXB 4: image wm (256 floats), tile row lane>>4, tiles r = 0..3
@@ -956,7 +968,7 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
     }
     // 16 channels × 1024 floats in 16-B chunks; a wave instruction = 1 KB of one channel:
     // TXB 8: 8 whole rows of the 32×32 block; TXB 4: one whole 16×16 image plane
-    constexpr int PCF = TXB == 8 ? PH * 8 : 256;   // float4 per channel plane
+    constexpr int PCF = TXB == 8 ? PH * 8 : NI * 64;   // float4 per channel plane
 #pragma unroll
     for (int i = 0; i < 16 * PCF / NT; ++i) {
       const int idx = i * NT + tid;
@@ -994,7 +1006,8 @@ __global__ __launch_bounds__(NW * WAVE) __attribute__((amdgpu_waves_per_eu(2, 2)
   // separate LDS objects per ring slot: the compiler tells a DMA into one slot from a ds_read of
   // another and does not wait for outstanding DMAs before every LDS read
   __shared__ __attribute__((aligned(16))) float R0[w2::GeoT<TXB, NW>::RAWF], R1[w2::GeoT<TXB, NW>::RAWF],
-      R2[w2::GeoT<TXB, NW>::RAWF], R3[(TXB == 8 && NW == 8 && SKP_W2_RS4) ? w2::GeoT<TXB, NW>::RAWF : 4];
+      R2[(TXB == 4 && NW == 4) ? 4 : w2::GeoT<TXB, NW>::RAWF],
+      R3[(TXB == 8 && NW == 8 && SKP_W2_RS4) ? w2::GeoT<TXB, NW>::RAWF : 4];
   __shared__ __attribute__((aligned(16))) float U0[w2::kUF], U1[w2::kUF], U2[NW == 4 ? 4 : w2::kUF];
   // workgroup → (input-channel split, 32×32-pixel block, channel block); consecutive logical ids
   // share one XCD.  A split sums its csplit input channels into slab sp of y (the workspace).
@@ -1021,7 +1034,7 @@ __global__ __launch_bounds__(NW * WAVE) __attribute__((amdgpu_waves_per_eu(2, 2)
     x0 = 32 * (br - by * bw);
     y0 = (NW == 4 ? 16 : 32) * by;
   } else {
-    img = 4 * tb;
+    img = (NW == 4 ? 2 : 4) * tb;
   }
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const W2Smem sm{R0, R1, R2, R3, U0, U1, U2};
@@ -1149,9 +1162,14 @@ extern "C" int skp_conv3x3_wino2(const float* x, const float* U, const float* bi
   // overlaps the other's stage loop): the default, 5-11% faster at every VAE / UNet shape
   // (profiles/r03al_wino_half_ab.txt); SKP_WINO2_HALF=0 = the 32 × 32 single-workgroup form
   const char* he = getenv("SKP_WINO2_HALF");
-  const bool half = !g16 && !(he && atoi(he) == 0);
+  const bool half = !(he && atoi(he) == 0);
+  // the 16×16 geometry's 4-wave form (two images per workgroup, two workgroups per CU; 2-slot
+  // raw and weight rings): the default, SKP_WINO2_HALF16=0 = four images per workgroup
+  // (profiles/r03ap_wino_half16_ab.txt)
+  const char* h16 = getenv("SKP_WINO2_HALF16");
+  const bool half16 = g16 && !(h16 && atoi(h16) == 0);
   const int bw = W / 32, bpi = (H / (half ? 16 : 32)) * bw;
-  const long long nblk = g16 ? B / 4 : (long long)B * bpi;
+  const long long nblk = g16 ? B / (half16 ? 2 : 4) : (long long)B * bpi;
   const int nkb = K / w2::kNC;
   SKP_CHECK_ARG(nblk * nkb * nsplit <= 0x7fffffffLL, "grid too large");
   // dev switches (SKP_WINO2_DEBUG): 1 skip transforms, 2 skip MFMAs, 4 skip input DMA, 8 skip weight DMA,
@@ -1167,7 +1185,10 @@ extern "C" int skp_conv3x3_wino2(const float* x, const float* U, const float* bi
   const dim3 grid((unsigned)(nblk * nkb * nsplit));
   const int fl = dbg | wino_nt_flag((long long)B * K * H * W * 4, nsplit);
 #define SKP_WG2(E)                                                                                            \
-  if (g16)                                                                                                    \
+  if (half16)                                                                                                 \
+    hipLaunchKernelGGL((wino2_kernel<E, 4, 4>), grid, dim3(4 * WAVE), 0, st, x, U, bias, residual, out, B, C, K,  \
+                       H, W, bw, bpi, (int)nblk, nkb, kb_major, C / nsplit, fl);                              \
+  else if (g16)                                                                                               \
     hipLaunchKernelGGL((wino2_kernel<E, 4>), grid, dim3(w2::kThreads), 0, st, x, U, bias, residual, out, B, C, K, \
                        H, W, bw, bpi, (int)nblk, nkb, kb_major, C / nsplit, fl);                              \
   else if (half)                                                                                              \

@@ -1100,6 +1100,7 @@ WINO_WIDE = os.environ.get("SKP_WINO_WIDE", "1") != "0"   # must match skp_conv3
 # half-height Winograd blocks (libskp's default for H, W multiples of 32; SKP_WINO2_HALF=0 off):
 # the split-K planner models two co-resident workgroups per CU for them
 WINO2_HALF = os.environ.get("SKP_WINO2_HALF", "1") != "0"
+WINO2_HALF16 = os.environ.get("SKP_WINO2_HALF16", "1") != "0"   # the 16×16 geometry's 4-wave form
 WINO_PLAN_HALF = os.environ.get("SKP_WINO_PLAN_HALF", "1") != "0"   # 0: the one-workgroup-per-CU cost model (A/B)
 
 
@@ -1144,7 +1145,7 @@ def _wino_plan_uncached(B, C, K, H, W, force):
     else:
         wgs = -(-(B * (H // 4) * (W // 4)) // 64) * (K // 32)
     out_bytes = B * K * H * W * 4
-    half = v2 and H != 16 and WINO2_HALF and WINO_PLAN_HALF
+    half = v2 and (WINO2_HALF16 if H == 16 else WINO2_HALF) and WINO_PLAN_HALF
 
     def cost(s):
         if half:
@@ -1173,7 +1174,7 @@ def _wino_plan(B, C, K, H, W):
     """_wino_plan_uncached, memoised per shape (and the module switches it reads): the planner's
     32-candidate cost loop ran in Python on every convolution call, ~1500 launches per step."""
     force = int(os.environ.get("SKP_WINO_NSPLIT", "0"))
-    key = (B, C, K, H, W, force, WINO_KERNEL, WINO_SPLIT, WINO_WIDE, WINO2_HALF, WINO_PLAN_HALF)
+    key = (B, C, K, H, W, force, WINO_KERNEL, WINO_SPLIT, WINO_WIDE, WINO2_HALF, WINO2_HALF16, WINO_PLAN_HALF)
     plan = _WINO_PLANS.get(key)
     if plan is None:
         plan = _WINO_PLANS[key] = _wino_plan_uncached(B, C, K, H, W, force)
