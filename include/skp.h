@@ -137,6 +137,13 @@ int skp_gaussian_target(const float* pos, int num, int T, int size, float sigma,
 int skp_topk_gaussian(const float* maps, int T, int h, int w, int top_k, float sigma, float epsilon,
                       int num_subjects, long long* out, double* kl, void* workspace, void* stream);
 
+/* skp_topk_gaussian for nb images in one launch (each image's top-k chosen as the reference's
+ * find_top_k_gaussian on that image, ptp_utils.py:86-112; optimize.py:403-410 per replica):
+ * maps (nb, T, h, w), out (nb, top_k), kl (nb, T) optional, workspace >= 16*nb*T bytes.      */
+int skp_topk_gaussian_batch(const float* maps, int nb, int T, int h, int w, int top_k, float sigma,
+                            float epsilon, int num_subjects, long long* out, double* kl, void* workspace,
+                            void* stream);
+
 /* ptp_utils.entropy_sort (ptp_utils.py:165-187): ascending softmax entropy.     */
 int skp_entropy_sort(const float* maps, int T, int h, int w, int top_k, long long* out, double* ent,
                      void* workspace, void* stream);
@@ -147,6 +154,11 @@ int skp_entropy_sort(const float* maps, int T, int h, int w, int top_k, long lon
  * workspace >= 16 * n_cand bytes.                                              */
 int skp_fps(const float* maps, int T, int h, int w, const long long* cand, int n_cand, int top_k,
             long long* out, int* n_out, void* workspace, void* stream);
+/* skp_fps for nb images in one launch (ptp_utils.py:115-159 per replica, optimize.py:419-424):
+ * maps (nb, T, h, w), cand (nb, n_cand) token ids of each image, out (nb, top_k), n_out (nb),
+ * workspace >= 8 * nb * n_cand bytes.                                                        */
+int skp_fps_batch(const float* maps, int nb, int T, int h, int w, const long long* cand, int n_cand, int top_k,
+                  long long* out, int* n_out, void* workspace, void* stream);
 
 /* ---------------------------------------------------------------- A11 sharpening
  * optimize.sharpening_loss (optimize.py:166-206): pos = k-max of A / w,

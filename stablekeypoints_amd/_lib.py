@@ -35,8 +35,11 @@ _SIGS = {
     "skp_weighted_avg": [_p, _c_int, _c_int, _c_int, _c_float, _c_int, _p, _p],
     "skp_gaussian_target": [_p, _c_int, _c_int, _c_int, _c_float, _p, _p],
     "skp_topk_gaussian": [_p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_float, _c_int, _p, _p, _p, _p],
+    "skp_topk_gaussian_batch": [_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _c_float, _c_int, _p, _p, _p,
+                                _p],
     "skp_entropy_sort": [_p, _c_int, _c_int, _c_int, _c_int, _p, _p, _p, _p],
     "skp_fps": [_p, _c_int, _c_int, _c_int, _p, _c_int, _c_int, _p, _p, _p, _p],
+    "skp_fps_batch": [_p, _c_int, _c_int, _c_int, _c_int, _p, _c_int, _c_int, _p, _p, _p, _p],
     "skp_sharpen_fwd": [_p, _c_int, _c_int, _c_int, _c_float, _c_int, _p, _p, _p, _p],
     "skp_sharpen_bwd": [_p, _c_int, _c_int, _c_int, _c_float, _c_int, _p, _p, _p, _p],
     "skp_affine_warp": [_p, _c_int, _c_int, _c_int, _c_int, _p, _p, _p],

@@ -54,11 +54,13 @@ __device__ void row_argmax_masked(const float* __restrict__ m, int h, int w, con
 }
 
 __global__ __launch_bounds__(kRowThreads) void argmax_kernel(const float* __restrict__ maps, int T, int h, int w,
-                                                          const long long* __restrict__ rows, float* __restrict__ pos,
-                                                          long long* __restrict__ idx) {
+                                                          const long long* __restrict__ rows, int seg_len,
+                                                          float* __restrict__ pos, long long* __restrict__ idx) {
   __shared__ float sv[kRowThreads / 64];
   __shared__ int si[kRowThreads / 64];
+  // with row ids, block i reads row rows[i] of map stack i / seg_len (T rows each)
   const long long row = rows ? rows[blockIdx.x] : blockIdx.x;
+  const long long seg = rows ? (long long)(blockIdx.x / seg_len) : 0;
   if (row < 0 || row >= T) {  // invalid row id: poison the output instead of reading out of bounds
     if (threadIdx.x == 0) {
       if (pos) { pos[2 * blockIdx.x] = NAN; pos[2 * blockIdx.x + 1] = NAN; }
@@ -68,7 +70,7 @@ __global__ __launch_bounds__(kRowThreads) void argmax_kernel(const float* __rest
   }
   float best;
   int bi;
-  row_argmax_masked(maps + row * (long long)h * w, h, w, nullptr, nullptr, 0, 0.0f, best, bi, sv, si);
+  row_argmax_masked(maps + (seg * T + row) * (long long)h * w, h, w, nullptr, nullptr, 0, 0.0f, best, bi, sv, si);
   if (threadIdx.x == 0) {
     if (pos) {
       pos[2 * blockIdx.x] = (float)(bi / w) + 0.5f;
@@ -240,6 +242,91 @@ __global__ __launch_bounds__(kRowThreads) void kl_gauss_kernel(const float* __re
   if (threadIdx.x == 0) kl[blockIdx.x] = acc;
 }
 
+// kl_gauss_kernel with the row resident in registers: one 16-B load per float4 the thread owns
+// (the multi-pass kernel streams the 64-KB row four times), and exp((v+eps)−max) and the target
+// kept from the Σ pass for the KL pass.  Each thread visits its elements in for_row's order
+// (float4 q = tid + j·1024) with the same float operations and the same double accumulation
+// order, and the block reductions are the same: bit-identical KL values.  HW ≤ 4·NV·1024, 16-B
+// aligned rows with HW % 4 == 0 (the launcher checks); blockIdx.x = row of a (rows, HW) stack,
+// so several images' maps are one launch.
+template <int NV>
+__global__ __launch_bounds__(kRowThreads) void kl_gauss_reg_kernel(const float* __restrict__ maps, int h, int w,
+                                                                int num, float radius2, float two_sig2, float eps,
+                                                                double* __restrict__ kl) {
+  __shared__ float sv[kRowThreads / 64];
+  __shared__ int si[kRowThreads / 64];
+  __shared__ double sd[kRowThreads / 64];
+  __shared__ float sf[kRowThreads / 64];
+  __shared__ float pr[kMaxSubjects], pc[kMaxSubjects];
+  const int HW = h * w, nq = HW >> 2;
+  const float4* m4 = reinterpret_cast<const float4*>(maps + (size_t)blockIdx.x * HW);
+  float4 v[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int q = threadIdx.x + j * kRowThreads;
+    v[j] = q < nq ? m4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  auto visit = [&](auto&& f) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int q = threadIdx.x + j * kRowThreads;
+      if (q < nq) {
+        f(j, 0, 4 * q, v[j].x);
+        f(j, 1, 4 * q + 1, v[j].y);
+        f(j, 2, 4 * q + 2, v[j].z);
+        f(j, 3, 4 * q + 3, v[j].w);
+      }
+    }
+  };
+  for (int q = 0; q < num; ++q) {   // find_k_max_pixels with the cumulative radius masks
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    visit([&](int, int, int e, float x) {
+      if (q) {
+        const float cx = (float)(e % w), cy = (float)(e / w);
+        for (int p = 0; p < q; ++p) {
+          const float dx = cx - pc[p], dy = cy - pr[p];
+          x = x * ((dx * dx + dy * dy > radius2) ? 1.0f : 0.0f);
+        }
+      }
+      if (argmax_better(x, e, best, bi)) { best = x; bi = e; }
+    });
+    block_argmax(best, bi, sv, si);
+    if (threadIdx.x == 0) {
+      pr[q] = (float)(bi / w) + 0.5f;
+      pc[q] = (float)(bi % w) + 0.5f;
+    }
+    __syncthreads();
+  }
+  float p0[kMaxSubjects], p1[kMaxSubjects];
+  for (int q = 0; q < num; ++q) {
+    p0[q] = (pr[q] / (float)h) * (float)h;
+    p1[q] = (pc[q] / (float)h) * (float)h;
+  }
+  float mx = -INFINITY;
+  visit([&](int, int, int, float x) { mx = fmaxf(mx, x + eps); });
+  mx = block_max(mx, sf);
+  float ex[NV][4], tg[NV][4];
+  double se = 0.0, sg = 0.0;
+  visit([&](int j, int c, int e, float x) {
+    ex[j][c] = expf((x + eps) - mx);
+    tg[j][c] = gauss_at(e / w, e % w, p0, p1, num, two_sig2) + eps;
+    se += (double)ex[j][c];
+    sg += (double)tg[j][c];
+  });
+  se = block_sum(se, sd);
+  sg = block_sum(sg, sd);
+  const float sef = (float)se, sgf = (float)sg;
+  double acc = 0.0;
+  visit([&](int j, int c, int, float) {
+    const float P = ex[j][c] / sef;
+    const float t = tg[j][c] / sgf;
+    acc += (double)t * ((double)logf(t) - (double)logf(P));
+  });
+  acc = block_sum(acc, sd);
+  if (threadIdx.x == 0) kl[blockIdx.x] = acc;
+}
+
 // entropy of softmax(map) (ptp_utils.py:179-182; torch Categorical renormalises and clamps)
 __global__ __launch_bounds__(kRowThreads) void entropy_kernel(const float* __restrict__ maps, int h, int w,
                                                            double* __restrict__ ent) {
@@ -276,11 +363,14 @@ __device__ __forceinline__ bool key_less(double a, int ia, double b, int ib) {
   return a < b || (a == b && ia < ib);
 }
 
+// blockIdx.x = segment: keys[b·T …], out[b·top_k …] (one launch sorts every image's keys)
 __global__ __launch_bounds__(1024) void sort_topk_kernel(const double* __restrict__ keys, int T, int n2, int top_k,
                                                          long long* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* k = reinterpret_cast<double*>(smem);
   int* id = reinterpret_cast<int*>(k + n2);
+  keys += (size_t)blockIdx.x * T;
+  out += (size_t)blockIdx.x * top_k;
   for (int i = threadIdx.x; i < n2; i += blockDim.x) {
     k[i] = i < T ? keys[i] : INFINITY;
     id[i] = i < T ? i : 0x7fffffff;
@@ -317,6 +407,10 @@ __global__ __launch_bounds__(64) void fps_kernel(const float* __restrict__ cpos,
   float* spr = reinterpret_cast<float*>(sel + top_k);
   float* spc = spr + top_k;
   const int lane = threadIdx.x;
+  cpos += (size_t)blockIdx.x * 2 * C;   // blockIdx.x = image of a batched launch
+  cand += (size_t)blockIdx.x * C;
+  out += (size_t)blockIdx.x * top_k;
+  if (n_out) n_out += blockIdx.x;
   for (int i = lane; i < C; i += 64) {
     pr[i] = cpos[2 * i] / (float)h;
     pc[i] = cpos[2 * i + 1] / (float)h;
@@ -452,7 +546,8 @@ extern "C" int skp_argmax2d(const float* maps, int T, int h, int w, const long l
   SKP_CHECK_ARG(T > 0 && h > 0 && w > 0, "non-positive shape");
   const int nr = rows ? n_rows : T;
   SKP_CHECK_ARG(nr > 0, "no rows");
-  hipLaunchKernelGGL(argmax_kernel, dim3(nr), dim3(kRowThreads), 0, as_stream(stream), maps, T, h, w, rows, pos, idx);
+  hipLaunchKernelGGL(argmax_kernel, dim3(nr), dim3(kRowThreads), 0, as_stream(stream), maps, T, h, w, rows, nr, pos,
+                     idx);
   SKP_LAUNCH_CHECK();
   return SKP_OK;
 }
@@ -501,20 +596,25 @@ extern "C" int skp_gaussian_target(const float* pos, int num, int T, int size, f
   return SKP_OK;
 }
 
-static int launch_sort(const double* keys, int T, int top_k, long long* out, hipStream_t st) {
+static int launch_sort(const double* keys, int T, int top_k, long long* out, hipStream_t st, int nb = 1) {
   int n2 = 1;
   while (n2 < T) n2 <<= 1;
   SKP_CHECK_ARG(n2 <= 8192, "T > 8192 tokens is not supported by the selection sort");
   const size_t lds = (size_t)n2 * (sizeof(double) + sizeof(int));
-  hipLaunchKernelGGL(sort_topk_kernel, dim3(1), dim3(1024), lds, st, keys, T, n2, top_k, out);
+  hipLaunchKernelGGL(sort_topk_kernel, dim3(nb), dim3(1024), lds, st, keys, T, n2, top_k, out);
   SKP_LAUNCH_CHECK();
   return SKP_OK;
 }
 
-extern "C" int skp_topk_gaussian(const float* maps, int T, int h, int w, int top_k, float sigma, float epsilon,
-                                 int num_subjects, long long* out, double* kl, void* workspace, void* stream) {
+#ifndef SKP_KL_REG
+#define SKP_KL_REG 1   // 0: the four-pass kl_gauss_kernel for every shape (A/B build)
+#endif
+
+extern "C" int skp_topk_gaussian_batch(const float* maps, int nb, int T, int h, int w, int top_k, float sigma,
+                                       float epsilon, int num_subjects, long long* out, double* kl, void* workspace,
+                                       void* stream) {
   SKP_CHECK_ARG(maps && out && workspace, "null pointer");
-  SKP_CHECK_ARG(T > 0 && h > 0 && w > 0, "non-positive shape");
+  SKP_CHECK_ARG(nb > 0 && T > 0 && h > 0 && w > 0, "non-positive shape");
   SKP_CHECK_ARG(top_k >= 0 && top_k <= T, "top_k out of range");
   SKP_CHECK_ARG(num_subjects >= 1 && num_subjects <= kMaxSubjects, "num_subjects out of range [1, 16]");
   double* keys = kl ? kl : reinterpret_cast<double*>(workspace);
@@ -522,11 +622,28 @@ extern "C" int skp_topk_gaussian(const float* maps, int T, int h, int w, int top
   const float radius2 = (float)(rad * rad);
   const float two_sig2 = (float)(2.0 * (double)sigma * (double)sigma);
   hipStream_t st = as_stream(stream);
-  hipLaunchKernelGGL(kl_gauss_kernel, dim3(T), dim3(kRowThreads), 0, st, maps, h, w, num_subjects, radius2, two_sig2,
-                     epsilon, keys);
+  const int rows = nb * T, HW = h * w;
+  const bool reg = SKP_KL_REG && (HW & 3) == 0 && (reinterpret_cast<uintptr_t>(maps) & 15) == 0;
+  if (reg && HW <= 4 * 1 * kRowThreads)
+    hipLaunchKernelGGL(kl_gauss_reg_kernel<1>, dim3(rows), dim3(kRowThreads), 0, st, maps, h, w, num_subjects,
+                       radius2, two_sig2, epsilon, keys);
+  else if (reg && HW <= 4 * 2 * kRowThreads)
+    hipLaunchKernelGGL(kl_gauss_reg_kernel<2>, dim3(rows), dim3(kRowThreads), 0, st, maps, h, w, num_subjects,
+                       radius2, two_sig2, epsilon, keys);
+  else if (reg && HW <= 4 * 4 * kRowThreads)
+    hipLaunchKernelGGL(kl_gauss_reg_kernel<4>, dim3(rows), dim3(kRowThreads), 0, st, maps, h, w, num_subjects,
+                       radius2, two_sig2, epsilon, keys);
+  else
+    hipLaunchKernelGGL(kl_gauss_kernel, dim3(rows), dim3(kRowThreads), 0, st, maps, h, w, num_subjects, radius2,
+                       two_sig2, epsilon, keys);
   SKP_LAUNCH_CHECK();
   if (top_k == 0) return SKP_OK;
-  return launch_sort(keys, T, top_k, out, st);
+  return launch_sort(keys, T, top_k, out, st, nb);
+}
+
+extern "C" int skp_topk_gaussian(const float* maps, int T, int h, int w, int top_k, float sigma, float epsilon,
+                                 int num_subjects, long long* out, double* kl, void* workspace, void* stream) {
+  return skp_topk_gaussian_batch(maps, 1, T, h, w, top_k, sigma, epsilon, num_subjects, out, kl, workspace, stream);
 }
 
 extern "C" int skp_entropy_sort(const float* maps, int T, int h, int w, int top_k, long long* out, double* ent,
@@ -542,23 +659,28 @@ extern "C" int skp_entropy_sort(const float* maps, int T, int h, int w, int top_
   return launch_sort(keys, T, top_k, out, st);
 }
 
-extern "C" int skp_fps(const float* maps, int T, int h, int w, const long long* cand, int n_cand, int top_k,
-                       long long* out, int* n_out, void* workspace, void* stream) {
+extern "C" int skp_fps_batch(const float* maps, int nb, int T, int h, int w, const long long* cand, int n_cand,
+                             int top_k, long long* out, int* n_out, void* workspace, void* stream) {
   SKP_CHECK_ARG(maps && cand && out && workspace, "null pointer");
-  SKP_CHECK_ARG(T > 0 && h > 0 && w > 0, "non-positive shape");
+  SKP_CHECK_ARG(nb > 0 && T > 0 && h > 0 && w > 0, "non-positive shape");
   SKP_CHECK_ARG(n_cand >= 2, "furthest_point_sampling needs at least two candidates");
   SKP_CHECK_ARG(n_cand <= 4096, "n_cand > 4096");
   SKP_CHECK_ARG(top_k >= 2 && top_k <= 1024, "top_k out of range [2, 1024]");
   hipStream_t st = as_stream(stream);
   float* cpos = reinterpret_cast<float*>(workspace);
-  hipLaunchKernelGGL(argmax_kernel, dim3(n_cand), dim3(kRowThreads), 0, st, maps, T, h, w, cand, cpos,
+  hipLaunchKernelGGL(argmax_kernel, dim3(nb * n_cand), dim3(kRowThreads), 0, st, maps, T, h, w, cand, n_cand, cpos,
                      (long long*)nullptr);
   SKP_LAUNCH_CHECK();
   const size_t lds = (size_t)n_cand * 8 + (size_t)n_cand * 8 + (size_t)top_k * 8 + (size_t)top_k * 8;
   SKP_CHECK_ARG(lds <= 64 * 1024, "fps LDS budget exceeded");
-  hipLaunchKernelGGL(fps_kernel, dim3(1), dim3(64), lds, st, cpos, cand, n_cand, h, top_k, out, n_out);
+  hipLaunchKernelGGL(fps_kernel, dim3(nb), dim3(64), lds, st, cpos, cand, n_cand, h, top_k, out, n_out);
   SKP_LAUNCH_CHECK();
   return SKP_OK;
+}
+
+extern "C" int skp_fps(const float* maps, int T, int h, int w, const long long* cand, int n_cand, int top_k,
+                       long long* out, int* n_out, void* workspace, void* stream) {
+  return skp_fps_batch(maps, 1, T, h, w, cand, n_cand, top_k, out, n_out, workspace, stream);
 }
 
 extern "C" int skp_sharpen_fwd(const float* A, int T, int h, int w, float sigma, int num_subjects, float* pos,

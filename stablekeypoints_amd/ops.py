@@ -546,6 +546,37 @@ def find_top_k_gaussian(maps, top_k, sigma=3, epsilon=1e-5, num_subjects=1, retu
     return (out, kl) if return_kl else out
 
 
+def find_top_k_gaussian_batch(maps, top_k, sigma=3, epsilon=1e-5, num_subjects=1):
+    """find_top_k_gaussian of every image of a (nb, T, h, w) stack in one launch each for the KL
+    ranking and the sort: (nb, top_k) int64, row b = find_top_k_gaussian(maps[b], ...)."""
+    _lib.require_device(maps)
+    maps = _c(maps)
+    nb, T, h, w = maps.shape
+    top_k = min(int(top_k), T)
+    out = torch.empty(nb, top_k, device=maps.device, dtype=torch.int64)
+    kl = torch.empty(nb, T, device=maps.device, dtype=torch.float64)
+    call("skp_topk_gaussian_batch", ptr(maps), nb, T, h, w, int(top_k), float(sigma), float(epsilon),
+         int(num_subjects), ptr(out), ptr(kl), ptr(kl), stream(maps.device))
+    return out
+
+
+def furthest_point_sampling_batch(maps, top_k, candidates):
+    """furthest_point_sampling of every image of a (nb, T, h, w) stack, candidates (nb, C) token
+    ids per image, in one argmax and one FPS launch.  Returns ((nb, top_k) int64, (nb,) int32)."""
+    _lib.require_device(maps)
+    maps = _c(maps)
+    nb, T, h, w = maps.shape
+    cand = candidates.to(device=maps.device, dtype=torch.int64).contiguous()
+    if cand.dim() != 2 or cand.shape[0] != nb:
+        raise ValueError(f"candidates {tuple(cand.shape)} for {nb} images")
+    out = torch.empty(nb, top_k, device=maps.device, dtype=torch.int64)
+    n_out = torch.empty(nb, device=maps.device, dtype=torch.int32)
+    ws = torch.empty(2 * cand.numel() + 2, device=maps.device, dtype=F32)
+    call("skp_fps_batch", ptr(maps), nb, T, h, w, ptr(cand), cand.shape[1], int(top_k), ptr(out), ptr(n_out),
+         ptr(ws), stream(maps.device))
+    return out, n_out
+
+
 def entropy_sort(maps, top_k, return_entropy=False):
     _lib.require_device(maps)
     maps = _c(maps)

@@ -8,6 +8,7 @@ once per optimiser step, which reproduces the reference's mean over replicas
 (``optimize.py:428-443``).  See DESIGN.md §Multi-GPU.
 """
 import json
+import os
 import time
 
 import torch
@@ -16,6 +17,9 @@ import torch.nn.functional as F
 from . import ops, ptp_utils
 from . import eval as skp_eval
 from .invertable_transform import RandomAffineWithInverse
+
+# A/B: 0 = select per image (one top-k / FPS launch chain per image, r03ao and before)
+SEL_BATCH = os.environ.get("SKP_SEL_BATCH", "1") != "0"
 
 
 def _upload(t, device):
@@ -275,7 +279,7 @@ class TokenOptimizer:
             layers=self.kw["layers"], controllers=self.controllers, stacked=True, captured=sparse)[0]
         maps = got.maps if sparse else got        # (2k, N, R, R); the selection needs no gradient
         th_inv = _upload(self.transform.theta_inverse(), self.device)   # all k warps, one upload
-        sel = [self._select(maps[i], maps[k + i]) for i in range(k)]
+        sel = self._select_batch(maps[:k], maps[k:])
         if sparse:
             # every image's selected rows in ONE gather whose backward is the sparse capture backward
             # (skp_capture_maps_bwd_sel): the rows' gradient goes straight to the kernel, no
@@ -318,7 +322,7 @@ class TokenOptimizer:
             self.ldm, inputs, self.context, noise_level=self.kw["noise_level"], device=self.device,
             layers=self.kw["layers"], controllers=self.controllers, stacked=True, captured=True)[0]
         maps = got.maps
-        sel = [self._select(maps[i], maps[k + i]) for i in range(k)]
+        sel = self._select_batch(maps[:k], maps[k:])
         rows = got.select(sel + sel)
         n = rows.shape[0] // 2
         A, At = rows[:n], rows[n:]
@@ -406,6 +410,21 @@ class TokenOptimizer:
         idx = self._select(attn_map, attention_map_transformed)
         loss, eq, sh = self._losses(attn_map[idx], attention_map_transformed[idx], index)
         return loss, eq, sh, idx
+
+    def _select_batch(self, maps, maps_t):
+        """_select for k images at once: maps / maps_t (k, N, R, R) = the images' and their warps'
+        maps.  The Gaussian top-k ranking and the furthest-point sampling run as one launch each
+        over the k images (skp_topk_gaussian_batch / skp_fps_batch); each image's selection is the
+        reference's for that image (optimize.py:403-424 per replica).  Falls back to per-image
+        _select where the batched form does not apply (other strategies, fewer candidates than
+        top_k)."""
+        k, N = maps.shape[0], maps.shape[1]
+        n_cand = min(int(self.fps_n), N)
+        if not (SEL_BATCH and k > 1 and self.top_k_strategy == "gaussian" and 2 <= self.top_k <= n_cand):
+            return [self._select(maps[i], maps_t[i]) for i in range(k)]
+        cand = ops.find_top_k_gaussian_batch(maps, n_cand, sigma=self.sigma, num_subjects=self.num_subjects)
+        sel, _ = ops.furthest_point_sampling_batch(maps_t, self.top_k, cand)
+        return list(sel.unbind(0))
 
     def _select(self, attn_map, attention_map_transformed):
         """optimize.py:403-424: top-k candidates on the image's map, FPS on its warp's map."""

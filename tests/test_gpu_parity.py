@@ -204,6 +204,54 @@ def test_selection_vs_golden_full_shape():
     assert np.array_equal(N(sel2), g["fps10_same"])
 
 
+@pytest.mark.parametrize("num_subjects", [1, 2])
+def test_selection_batched_equals_per_image(num_subjects):
+    """skp_topk_gaussian_batch / skp_fps_batch (one launch over the images of a pass) select what
+    the per-image calls select, image by image; image 0 carries the reference golden's maps."""
+    from stablekeypoints_amd import ops
+    g = load_golden("select")
+    maps = np.stack([recipes.attention_like_maps(31, 500, 128)] +
+                    [recipes.attention_like_maps(40 + i, 500, 128) for i in range(3)])
+    maps_t = np.stack([recipes.attention_like_maps(32, 500, 128)] +
+                      [recipes.attention_like_maps(50 + i, 500, 128) for i in range(3)])
+    cand = ops.find_top_k_gaussian_batch(T(maps), 25, sigma=2.0, num_subjects=num_subjects)
+    for i in range(4):
+        one = ops.find_top_k_gaussian(T(maps[i]), 25, sigma=2.0, num_subjects=num_subjects)
+        assert torch.equal(cand[i], one)
+    gold = g["topk_gauss25"] if num_subjects == 1 else g["topk_gauss25_s2"]
+    assert np.array_equal(N(cand[0]), gold)
+    sel, n = ops.furthest_point_sampling_batch(T(maps_t), 10, cand)
+    assert N(n).tolist() == [10] * 4
+    for i in range(4):
+        one, _ = ops.furthest_point_sampling(T(maps_t[i]), 10, cand[i])
+        assert torch.equal(sel[i], one)
+    if num_subjects == 1:
+        assert np.array_equal(N(sel[0]), g["fps10"])
+
+
+@pytest.mark.parametrize("hw", [(64, 64), (90, 90), (128, 128), (256, 256)])
+def test_topk_gaussian_register_kernel_vs_four_pass(hw):
+    """The register-resident KL kernel (16-B aligned rows, h·w ≤ 16384) against the four-pass
+    kernel the launcher takes for a misaligned row: same ranking, KL within double rounding;
+    (256, 256) exercises the four-pass kernel on both sides and the batched launch."""
+    from stablekeypoints_amd import ops
+    h, w = hw
+    rng = np.random.default_rng(h)
+    maps = rng.random((3, 40, h, w), dtype=np.float32) ** 8
+    a = T(maps)
+    buf = torch.empty(a.numel() + 1, device=a.device, dtype=torch.float32)
+    mis = buf[1:].view_as(a)
+    mis.copy_(a)
+    for i in range(3):
+        idx_r, kl_r = ops.find_top_k_gaussian(a[i], 12, sigma=2.0, return_kl=True)
+        idx_m, kl_m = ops.find_top_k_gaussian(mis[i], 12, sigma=2.0, return_kl=True)
+        assert torch.equal(idx_r, idx_m)
+        assert torch.allclose(kl_r, kl_m, rtol=1e-12, atol=0)
+    batch = ops.find_top_k_gaussian_batch(a, 12, sigma=2.0)
+    for i in range(3):
+        assert torch.equal(batch[i], ops.find_top_k_gaussian(a[i], 12, sigma=2.0))
+
+
 def test_entropy_sort_raw_maps_pinned_expectation():
     """entropy_sort on raw (near-uniform) maps (ptp_utils.py:165-187).  The reference ranks
     fp32 Categorical entropies of softmax over 16384 pixels; on these maps those carry 2.25e-6 of
