@@ -373,11 +373,14 @@ def main():
                     help="un-captured UNet attention: explicit fp32 GEMM+softmax (math) or torch SDPA")
     ap.add_argument("--micro-batch", type=int, default=0,
                     help="images per VAE/UNet pass (0 = all `accum` images of an optimiser step in one pass)")
-    ap.add_argument("--prefetch", type=int, default=1,
+    ap.add_argument("--prefetch", type=int, default=0,
                     help="VAE-encode the next PREFETCH passes' images on a side stream (TokenOptimizer.prefetch), "
                          "enqueued between the current pass's forward and backward; steady state: every timed step "
                          "runs one UNet pass and one VAE pass, the warm-up's prefetches are balanced by the last "
-                         "timed steps' (0 = no prefetch)")
+                         "timed steps' (0 = no prefetch: each pass encodes its own images on the main stream, "
+                         "measured 0.3-0.5%% faster than 1 on the current tree in three A/B sessions, "
+                         "profiles/r03ar_prefetch_ab.txt, profiles/r03at_ab.txt: the GPU is saturated either way "
+                         "and the side stream's large convolutions delay the UNet's small launches)")
     ap.add_argument("--prefetch-at", default="capture_bwd", choices=["capture_bwd", "bwd"],
                     help="where the VAE prefetch is enqueued: after the sparse capture backward (the VAE overlaps "
                          "the UNet backward) or before the whole backward")

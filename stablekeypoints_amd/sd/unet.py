@@ -111,8 +111,15 @@ class CrossAttention(nn.Module):
         if mask is None and USE_FUSED_GROUPNORM and x.is_cuda and CrossAttention.backend == "math":
             from .. import ops   # attention straight on the (B, S, H·d) projections: no head permutes
             qf = self.to_q(x)
-            kf, vf = kv_projection(self, context)
+            one = _shared_context(context)
+            if one is not None:   # one sequence for the whole batch: projected once
+                k1, v1 = self.to_k(one), self.to_v(one)
+                kf, vf = k1.expand(x.shape[0], -1, -1), v1.expand(x.shape[0], -1, -1)
+            else:
+                kf, vf = kv_projection(self, context)
             out = ops.attention_heads(qf, kf, vf, self.heads, self.scale)
+            if out is None and one is not None and SHARED_HEAD_MAJOR and torch.is_grad_enabled():
+                out = shared_context_attention(qf, k1, v1, self.heads, self.scale)
             if out is not None:
                 return self.to_out[1](self.to_out[0](out))
             q = self.reshape_heads_to_batch_dim(qf)
@@ -128,6 +135,32 @@ class CrossAttention(nn.Module):
 
 
 SHARED_KV = os.environ.get("SKP_SHARED_KV", "1") != "0"   # A/B switch for kv_projection
+# A/B switch: 0 = a batch-shared context's k / v are expanded to the batch and head-permuted with it
+SHARED_HEAD_MAJOR = os.environ.get("SKP_SHARED_HEAD_MAJOR", "1") != "0"
+
+
+def _shared_context(context):
+    """The one (1, L, C) sequence of a context whose batch is a stride-0 expansion (the token
+    embedding every image of a batched pass shares), else None."""
+    if SHARED_KV and context.dim() == 3 and context.shape[0] > 1 and context.stride(0) == 0:
+        return context[:1]
+    return None
+
+
+def shared_context_attention(qf, k1, v1, H, scale):
+    """softmax(q kᵀ·scale) v per head for (B, S, H·d) queries against ONE (1, L, H·d) key / value
+    sequence shared by the batch, with the heads outermost: q as (H, B·S, d), k / v as (H, L, d),
+    so each head is one GEMM over all B·S query rows (no per-image copy of the shared keys and
+    values, and their gradients come out of the GEMMs already summed over the batch — no
+    batch-expanded gradient and no reduction over it).  Same per-(query, head) arithmetic as the
+    (B·H, S, d) form.  Returns (B, S, H·d)."""
+    B, S, C = qf.shape
+    L, d = k1.shape[1], C // H
+    q = qf.reshape(B, S, H, d).permute(2, 0, 1, 3).reshape(H, B * S, d)
+    k = k1.reshape(L, H, d).transpose(0, 1).contiguous()
+    v = v1.reshape(L, H, d).transpose(0, 1).contiguous()
+    o = attention_core(q, k, v, scale)
+    return o.reshape(H, B, S, d).permute(1, 2, 0, 3).reshape(B, S, C)
 
 
 def kv_projection(attn, context):

@@ -114,3 +114,31 @@ def test_unet_cross_attention_module_uses_bshd_and_matches_permuting_path(monkey
     out2 = m(x, ctx.expand(2, -1, -1))
     out2.square().sum().backward()
     assert _rel(out, out2) < 2e-5 and _rel(gx, x.grad) < 2e-5 and _rel(gc, ctx.grad) < 2e-5
+
+
+@pytest.mark.parametrize("B,H,S,L,d", [
+    (8, 8, 256, 500, 160),     # the 16² cross-attention layers at the bench shape (d = 160)
+    (8, 8, 1024, 500, 80),     # the 32² cross-attention layers (d = 80)
+    (3, 8, 64, 77, 160),       # a ragged key count, an odd batch
+])
+def test_shared_context_head_major_vs_torch(B, H, S, L, d):
+    """sd.unet.shared_context_attention (heads outermost, one GEMM per head over all B·S query
+    rows against the ONE shared key / value sequence) against the batch-expanded, head-permuted
+    plain fp32 form: output and the gradients of q and of the single k / v sequence (the
+    expanded form's gradients summed over the batch, as the expand's backward does)."""
+    from stablekeypoints_amd.sd import unet
+    g = torch.Generator(device="cpu").manual_seed(d + S)
+    C = H * d
+    scale = d ** -0.5
+    q = torch.randn(B, S, C, generator=g).to(DEV).requires_grad_()
+    k1 = torch.randn(1, L, C, generator=g).to(DEV).requires_grad_()
+    v1 = torch.randn(1, L, C, generator=g).to(DEV).requires_grad_()
+    do = torch.randn(B, S, C, generator=g).to(DEV)
+    out = unet.shared_context_attention(q, k1, v1, H, scale)
+    dq, dk, dv = torch.autograd.grad(out, (q, k1, v1), do)
+    qr, kr, vr = (t.detach().clone().requires_grad_() for t in (q, k1, v1))
+    ref = _ref(qr, kr.expand(B, -1, -1), vr.expand(B, -1, -1), H, scale)
+    rq, rk, rv = torch.autograd.grad(ref, (qr, kr, vr), do)
+    assert out.shape == (B, S, C)
+    for a, b, name in ((out, ref, "out"), (dq, rq, "dq"), (dk, rk, "dk"), (dv, rv, "dv")):
+        assert _rel(a, b) < 2e-5, (name, _rel(a, b))
