@@ -169,6 +169,13 @@ int skp_sharpen_fwd(const float* A, int T, int h, int w, float sigma, int num_su
 /* dA = gout[0] · 2(A − G)/numel.                                               */
 int skp_sharpen_bwd(const float* A, int T, int h, int w, float sigma, int num_subjects, const float* pos,
                      const float* gout, float* dA, void* stream);
+/* The sharpening loss of nb images at once (optimize.py:425-437 per replica): A (nb, T, h, w),
+ * loss (nb) = each image's mean, pos (num, nb·T, 2), partial >= nb·T doubles; backward with
+ * gout (nb).  Each image's loss and gradient are the single-image call's, bit for bit.        */
+int skp_sharpen_fwd_batch(const float* A, int nb, int T, int h, int w, float sigma, int num_subjects, float* pos,
+                          double* partial, float* loss, void* stream);
+int skp_sharpen_bwd_batch(const float* A, int nb, int T, int h, int w, float sigma, int num_subjects,
+                          const float* pos, const float* gout, float* dA, void* stream);
 
 /* ---------------------------------------------------------------- A12 warp / equivariance
  * F.grid_sample(x, F.affine_grid(theta), bilinear, zeros, align_corners=False)
@@ -186,6 +193,12 @@ int skp_equiv_fwd(const float* A, const float* At, int T, int h, int w, const fl
 /* dA = gout·2(A−A')/numel (optional), dAt = warpᵀ(−dA) (overwritten).          */
 int skp_equiv_bwd(const float* A, const float* At, int T, int h, int w, const float* theta_inv,
                   const float* gout, float* dA, float* dAt, void* stream);
+/* The equivariance loss of nb replicas at once: A, At (nb, T, h, w), theta_inv (nb, 2, 3),
+ * loss (nb), partial >= nb·T doubles; backward with gout (nb).  Same per-image values.       */
+int skp_equiv_fwd_batch(const float* A, const float* At, int nb, int T, int h, int w, const float* theta_inv,
+                        double* partial, float* loss, void* stream);
+int skp_equiv_bwd_batch(const float* A, const float* At, int nb, int T, int h, int w, const float* theta_inv,
+                        const float* gout, float* dA, float* dAt, void* stream);
 
 /* ---------------------------------------------------------------- Q·Kᵀ (fp32 MFMA)
  * C[b,m,n] = alpha · Σ_k A[b,m,k] · B[b,k,n] (+ C if accumulate), arbitrary element

@@ -42,10 +42,14 @@ _SIGS = {
     "skp_fps_batch": [_p, _c_int, _c_int, _c_int, _c_int, _p, _c_int, _c_int, _p, _p, _p, _p],
     "skp_sharpen_fwd": [_p, _c_int, _c_int, _c_int, _c_float, _c_int, _p, _p, _p, _p],
     "skp_sharpen_bwd": [_p, _c_int, _c_int, _c_int, _c_float, _c_int, _p, _p, _p, _p],
+    "skp_sharpen_fwd_batch": [_p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_int, _p, _p, _p, _p],
+    "skp_sharpen_bwd_batch": [_p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_int, _p, _p, _p, _p],
     "skp_affine_warp": [_p, _c_int, _c_int, _c_int, _c_int, _p, _p, _p],
     "skp_affine_warp_bwd": [_p, _c_int, _c_int, _c_int, _c_int, _p, _p, _p],
     "skp_equiv_fwd": [_p, _p, _c_int, _c_int, _c_int, _p, _p, _p, _p],
     "skp_equiv_bwd": [_p, _p, _c_int, _c_int, _c_int, _p, _p, _p, _p, _p],
+    "skp_equiv_fwd_batch": [_p, _p, _c_int, _c_int, _c_int, _c_int, _p, _p, _p, _p],
+    "skp_equiv_bwd_batch": [_p, _p, _c_int, _c_int, _c_int, _c_int, _p, _p, _p, _p, _p],
     "skp_bgemm_f32": [_p, _c_ll, _c_ll, _c_ll, _p, _c_ll, _c_ll, _c_ll, _p, _c_ll, _c_ll, _c_ll, _c_int, _c_int,
                       _c_int, _c_int, _c_float, _c_int, _p],
     "skp_groupnorm_workspace": [_c_int, _c_int, _c_ll, _c_int],

@@ -513,15 +513,18 @@ __global__ __launch_bounds__(kRowThreads) void sharpen_fwd_kernel(const float* _
   if (threadIdx.x == 0) partial[row] = acc;
 }
 
+// blockIdx.x = image: out[b] = Σ partial[b·n …] / numel (fixed order; one block per image)
 __global__ void finalize_mean_kernel(const double* __restrict__ partial, int n, double numel, float* __restrict__ out) {
   __shared__ double sd[kThreads / 64];
+  partial += (size_t)blockIdx.x * n;
   double acc = 0.0;
   for (int i = threadIdx.x; i < n; i += blockDim.x) acc += partial[i];
   acc = block_sum(acc, sd);
-  if (threadIdx.x == 0) out[0] = (float)(acc / numel);
+  if (threadIdx.x == 0) out[blockIdx.x] = (float)(acc / numel);
 }
 
-__global__ void sharpen_bwd_kernel(const float* __restrict__ A, int T, int h, int w, int num, float two_sig2,
+// rows of image b = [b·seg, (b + 1)·seg): its loss gradient is gout[b]
+__global__ void sharpen_bwd_kernel(const float* __restrict__ A, int T, int seg, int h, int w, int num, float two_sig2,
                                    const float* __restrict__ pos, const float* __restrict__ gout, float norm,
                                    float* __restrict__ dA) {
   const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -534,7 +537,7 @@ __global__ void sharpen_bwd_kernel(const float* __restrict__ A, int T, int h, in
     p1[q] = pos[((size_t)q * T + t) * 2 + 1] * (float)h;
   }
   const float d = A[e] - gauss_at(p / w, p % w, p0, p1, num, two_sig2);
-  dA[e] = (d * norm) * gout[0];
+  dA[e] = (d * norm) * gout[t / seg];
 }
 
 }  // namespace
@@ -683,33 +686,43 @@ extern "C" int skp_fps(const float* maps, int T, int h, int w, const long long* 
   return skp_fps_batch(maps, 1, T, h, w, cand, n_cand, top_k, out, n_out, workspace, stream);
 }
 
-extern "C" int skp_sharpen_fwd(const float* A, int T, int h, int w, float sigma, int num_subjects, float* pos,
-                               double* partial, float* loss, void* stream) {
+extern "C" int skp_sharpen_fwd_batch(const float* A, int nb, int T, int h, int w, float sigma, int num_subjects,
+                                     float* pos, double* partial, float* loss, void* stream) {
   SKP_CHECK_ARG(A && pos && partial && loss, "null pointer");
-  SKP_CHECK_ARG(T > 0 && h > 0 && w > 0, "non-positive shape");
+  SKP_CHECK_ARG(nb > 0 && T > 0 && h > 0 && w > 0, "non-positive shape");
   SKP_CHECK_ARG(num_subjects >= 1 && num_subjects <= kMaxSubjects, "num_subjects out of range [1, 16]");
   const double rad = 0.05 * (double)h;
   const float radius2 = (float)(rad * rad);
   const float two_sig2 = (float)(2.0 * (double)sigma * (double)sigma);
   hipStream_t st = as_stream(stream);
-  hipLaunchKernelGGL(sharpen_fwd_kernel, dim3(T), dim3(kRowThreads), 0, st, A, T, h, w, num_subjects, radius2, two_sig2,
-                     pos, partial);
+  hipLaunchKernelGGL(sharpen_fwd_kernel, dim3(nb * T), dim3(kRowThreads), 0, st, A, nb * T, h, w, num_subjects, radius2,
+                     two_sig2, pos, partial);
   SKP_LAUNCH_CHECK();
-  hipLaunchKernelGGL(finalize_mean_kernel, dim3(1), dim3(kThreads), 0, st, partial, T, (double)T * h * w, loss);
+  hipLaunchKernelGGL(finalize_mean_kernel, dim3(nb), dim3(kThreads), 0, st, partial, T, (double)T * h * w, loss);
+  SKP_LAUNCH_CHECK();
+  return SKP_OK;
+}
+
+extern "C" int skp_sharpen_fwd(const float* A, int T, int h, int w, float sigma, int num_subjects, float* pos,
+                               double* partial, float* loss, void* stream) {
+  return skp_sharpen_fwd_batch(A, 1, T, h, w, sigma, num_subjects, pos, partial, loss, stream);
+}
+
+extern "C" int skp_sharpen_bwd_batch(const float* A, int nb, int T, int h, int w, float sigma, int num_subjects,
+                                     const float* pos, const float* gout, float* dA, void* stream) {
+  SKP_CHECK_ARG(A && pos && gout && dA, "null pointer");
+  SKP_CHECK_ARG(nb > 0 && T > 0 && h > 0 && w > 0, "non-positive shape");
+  SKP_CHECK_ARG(num_subjects >= 1 && num_subjects <= kMaxSubjects, "num_subjects out of range [1, 16]");
+  const float two_sig2 = (float)(2.0 * (double)sigma * (double)sigma);
+  const float norm = (float)(2.0 / ((double)T * h * w));
+  const size_t total = (size_t)nb * T * h * w;
+  hipLaunchKernelGGL(sharpen_bwd_kernel, dim3((total + 255) / 256), dim3(256), 0, as_stream(stream), A, nb * T, T, h,
+                     w, num_subjects, two_sig2, pos, gout, norm, dA);
   SKP_LAUNCH_CHECK();
   return SKP_OK;
 }
 
 extern "C" int skp_sharpen_bwd(const float* A, int T, int h, int w, float sigma, int num_subjects, const float* pos,
                                const float* gout, float* dA, void* stream) {
-  SKP_CHECK_ARG(A && pos && gout && dA, "null pointer");
-  SKP_CHECK_ARG(T > 0 && h > 0 && w > 0, "non-positive shape");
-  SKP_CHECK_ARG(num_subjects >= 1 && num_subjects <= kMaxSubjects, "num_subjects out of range [1, 16]");
-  const float two_sig2 = (float)(2.0 * (double)sigma * (double)sigma);
-  const float norm = (float)(2.0 / ((double)T * h * w));
-  const size_t total = (size_t)T * h * w;
-  hipLaunchKernelGGL(sharpen_bwd_kernel, dim3((total + 255) / 256), dim3(256), 0, as_stream(stream), A, T, h, w,
-                     num_subjects, two_sig2, pos, gout, norm, dA);
-  SKP_LAUNCH_CHECK();
-  return SKP_OK;
+  return skp_sharpen_bwd_batch(A, 1, T, h, w, sigma, num_subjects, pos, gout, dA, stream);
 }

@@ -89,11 +89,13 @@ __global__ void warp_bwd_kernel(const float* __restrict__ gout, int B, int C, in
 constexpr int kThreads = 256;
 constexpr int kRowThreads = 1024;   // one workgroup per map row
 
+// rows of image b = [b·seg, (b + 1)·seg) warp with th[6b …] (and, backward, scale by gout[b])
 __global__ __launch_bounds__(kRowThreads) void equiv_fwd_kernel(const float* __restrict__ A, const float* __restrict__ At,
-                                                             int h, int w, const float* __restrict__ th,
+                                                             int seg, int h, int w, const float* __restrict__ th,
                                                              double* __restrict__ partial) {
   __shared__ double sd[kRowThreads / 64];
   const int t = blockIdx.x;
+  th += 6 * (t / seg);
   const size_t HW = (size_t)h * w;
   const float* a = A + t * HW;
   const float* at = At + t * HW;
@@ -106,26 +108,28 @@ __global__ __launch_bounds__(kRowThreads) void equiv_fwd_kernel(const float* __r
   if (threadIdx.x == 0) partial[t] = acc;
 }
 
-__global__ void equiv_bwd_kernel(const float* __restrict__ A, const float* __restrict__ At, int T, int h, int w,
-                                 const float* __restrict__ th, const float* __restrict__ gout, float norm,
+__global__ void equiv_bwd_kernel(const float* __restrict__ A, const float* __restrict__ At, int T, int seg, int h,
+                                 int w, const float* __restrict__ th, const float* __restrict__ gout, float norm,
                                  float* __restrict__ dA, float* __restrict__ dAt) {
   const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t HW = (size_t)h * w;
   if (e >= (size_t)T * HW) return;
   const int t = e / HW, p = e % HW;
-  const Bilin g = grid_point(th, p / w, p % w, h, w);
+  const Bilin g = grid_point(th + 6 * (t / seg), p / w, p % w, h, w);
   const float d = A[e] - sample(At + t * HW, g, h, w);
-  const float gd = (d * norm) * gout[0];
+  const float gd = (d * norm) * gout[t / seg];
   if (dA) dA[e] = gd;
   scatter(dAt + t * HW, g, h, w, -gd);
 }
 
+// blockIdx.x = image: out[b] = Σ partial[b·n …] / numel (fixed order; one block per image)
 __global__ void finalize_mean_kernel(const double* __restrict__ partial, int n, double numel, float* __restrict__ out) {
   __shared__ double sd[kThreads / 64];
+  partial += (size_t)blockIdx.x * n;
   double acc = 0.0;
   for (int i = threadIdx.x; i < n; i += blockDim.x) acc += partial[i];
   acc = block_sum(acc, sd);
-  if (threadIdx.x == 0) out[0] = (float)(acc / numel);
+  if (threadIdx.x == 0) out[blockIdx.x] = (float)(acc / numel);
 }
 
 }  // namespace
@@ -156,31 +160,41 @@ extern "C" int skp_affine_warp_bwd(const float* gout, int B, int C, int H, int W
   return SKP_OK;
 }
 
+extern "C" int skp_equiv_fwd_batch(const float* A, const float* At, int nb, int T, int h, int w,
+                                   const float* theta_inv, double* partial, float* loss, void* stream) {
+  SKP_CHECK_ARG(A && At && theta_inv && partial && loss, "null pointer");
+  SKP_CHECK_ARG(nb > 0 && T > 0 && h > 0 && w > 0, "non-positive shape");
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(equiv_fwd_kernel, dim3(nb * T), dim3(kRowThreads), 0, st, A, At, T, h, w, theta_inv, partial);
+  SKP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(finalize_mean_kernel, dim3(nb), dim3(kThreads), 0, st, partial, T, (double)T * h * w, loss);
+  SKP_LAUNCH_CHECK();
+  return SKP_OK;
+}
+
 extern "C" int skp_equiv_fwd(const float* A, const float* At, int T, int h, int w, const float* theta_inv,
                              double* partial, float* loss, void* stream) {
-  SKP_CHECK_ARG(A && At && theta_inv && partial && loss, "null pointer");
-  SKP_CHECK_ARG(T > 0 && h > 0 && w > 0, "non-positive shape");
+  return skp_equiv_fwd_batch(A, At, 1, T, h, w, theta_inv, partial, loss, stream);
+}
+
+extern "C" int skp_equiv_bwd_batch(const float* A, const float* At, int nb, int T, int h, int w,
+                                   const float* theta_inv, const float* gout, float* dA, float* dAt, void* stream) {
+  SKP_CHECK_ARG(A && At && theta_inv && gout && dAt, "null pointer");
+  SKP_CHECK_ARG(nb > 0 && T > 0 && h > 0 && w > 0, "non-positive shape");
   hipStream_t st = as_stream(stream);
-  hipLaunchKernelGGL(equiv_fwd_kernel, dim3(T), dim3(kRowThreads), 0, st, A, At, h, w, theta_inv, partial);
-  SKP_LAUNCH_CHECK();
-  hipLaunchKernelGGL(finalize_mean_kernel, dim3(1), dim3(kThreads), 0, st, partial, T, (double)T * h * w, loss);
+  const size_t total = (size_t)nb * T * h * w;
+  if (hipMemsetAsync(dAt, 0, total * sizeof(float), st) != hipSuccess) {
+    set_error("skp_equiv_bwd: memset failed");
+    return SKP_ELAUNCH;
+  }
+  const float norm = (float)(2.0 / ((double)T * h * w));
+  hipLaunchKernelGGL(equiv_bwd_kernel, dim3((total + 255) / 256), dim3(256), 0, st, A, At, nb * T, T, h, w, theta_inv,
+                     gout, norm, dA, dAt);
   SKP_LAUNCH_CHECK();
   return SKP_OK;
 }
 
 extern "C" int skp_equiv_bwd(const float* A, const float* At, int T, int h, int w, const float* theta_inv,
                              const float* gout, float* dA, float* dAt, void* stream) {
-  SKP_CHECK_ARG(A && At && theta_inv && gout && dAt, "null pointer");
-  SKP_CHECK_ARG(T > 0 && h > 0 && w > 0, "non-positive shape");
-  hipStream_t st = as_stream(stream);
-  if (hipMemsetAsync(dAt, 0, (size_t)T * h * w * sizeof(float), st) != hipSuccess) {
-    set_error("skp_equiv_bwd: memset failed");
-    return SKP_ELAUNCH;
-  }
-  const float norm = (float)(2.0 / ((double)T * h * w));
-  const size_t total = (size_t)T * h * w;
-  hipLaunchKernelGGL(equiv_bwd_kernel, dim3((total + 255) / 256), dim3(256), 0, st, A, At, T, h, w, theta_inv, gout,
-                     norm, dA, dAt);
-  SKP_LAUNCH_CHECK();
-  return SKP_OK;
+  return skp_equiv_bwd_batch(A, At, 1, T, h, w, theta_inv, gout, dA, dAt, stream);
 }

@@ -632,6 +632,43 @@ def sharpening_loss(A, sigma=1.0, num_subjects=1):
     return SharpeningLoss.apply(A, float(sigma), int(num_subjects))
 
 
+class SharpeningLossBatch(torch.autograd.Function):
+    """SharpeningLoss of nb images' selected rows at once: A (nb·T, h, w) → (nb,) losses, each the
+    single-image loss (skp_sharpen_fwd_batch / _bwd_batch: one launch per direction)."""
+
+    @staticmethod
+    def forward(ctx, A, nb, sigma, num_subjects):
+        A = _c(A)
+        R, h, w = A.shape
+        T = R // nb
+        pos = torch.empty(num_subjects, R, 2, device=A.device, dtype=F32)
+        part = torch.empty(R, device=A.device, dtype=torch.float64)
+        loss = torch.empty(nb, device=A.device, dtype=F32)
+        call("skp_sharpen_fwd_batch", ptr(A), nb, T, h, w, float(sigma), int(num_subjects), ptr(pos), ptr(part),
+             ptr(loss), stream(A.device))
+        ctx.save_for_backward(A, pos)
+        ctx.meta = (nb, T, sigma, num_subjects)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        A, pos = ctx.saved_tensors
+        nb, T, sigma, num = ctx.meta
+        _, h, w = A.shape
+        dA = torch.empty_like(A)
+        call("skp_sharpen_bwd_batch", ptr(A), nb, T, h, w, float(sigma), int(num), ptr(pos), ptr(_c(g.reshape(nb))),
+             ptr(dA), stream(A.device))
+        return dA, None, None, None
+
+
+def sharpening_loss_batch(A, nb, sigma=1.0, num_subjects=1):
+    """(nb,) sharpening losses of nb images whose T selected rows each are stacked in A (nb·T, h, w)."""
+    _lib.require_device(A)
+    if A.shape[0] % nb:
+        raise ValueError(f"{A.shape[0]} rows for {nb} images")
+    return SharpeningLossBatch.apply(A, int(nb), float(sigma), int(num_subjects))
+
+
 class AffineWarp(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, theta):
@@ -686,6 +723,43 @@ def equivariance_loss_single(A, At, theta_inv):
     """mean((A − warp(At, theta_inv))²) with gradients into A and At."""
     _lib.require_device(A, At)
     return EquivarianceLoss.apply(A, At, theta_inv)
+
+
+class EquivarianceLossBatch(torch.autograd.Function):
+    """EquivarianceLoss of nb replicas at once: A, At (nb·T, h, w), theta_inv (nb, 2, 3) → (nb,)
+    losses, each the single-replica loss (skp_equiv_fwd_batch / _bwd_batch)."""
+
+    @staticmethod
+    def forward(ctx, A, At, theta_inv, nb):
+        A, At = _c(A), _c(At)
+        R, h, w = A.shape
+        T = R // nb
+        th = _c(theta_inv.to(A.device)).reshape(nb * 6)
+        part = torch.empty(R, device=A.device, dtype=torch.float64)
+        loss = torch.empty(nb, device=A.device, dtype=F32)
+        call("skp_equiv_fwd_batch", ptr(A), ptr(At), nb, T, h, w, ptr(th), ptr(part), ptr(loss), stream(A.device))
+        ctx.save_for_backward(A, At, th)
+        ctx.meta = (nb, T)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        A, At, th = ctx.saved_tensors
+        nb, T = ctx.meta
+        _, h, w = A.shape
+        dA = torch.empty_like(A) if ctx.needs_input_grad[0] else None
+        dAt = torch.empty_like(At)
+        call("skp_equiv_bwd_batch", ptr(A), ptr(At), nb, T, h, w, ptr(th), ptr(_c(g.reshape(nb))), ptr(dA), ptr(dAt),
+             stream(A.device))
+        return dA, (dAt if ctx.needs_input_grad[1] else None), None, None
+
+
+def equivariance_loss_batch(A, At, theta_inv, nb):
+    """(nb,) equivariance losses of nb replicas (T selected rows each, stacked in A / At)."""
+    _lib.require_device(A, At)
+    if A.shape[0] % nb or theta_inv.numel() != 6 * nb:
+        raise ValueError(f"{A.shape[0]} rows / theta_inv {tuple(theta_inv.shape)} for {nb} images")
+    return EquivarianceLossBatch.apply(A, At, theta_inv, int(nb))
 
 
 # --------------------------------------------------------------------------- UNet-side GroupNorm(+SiLU)

@@ -293,13 +293,9 @@ class TokenOptimizer:
             img = torch.cat([torch.full_like(idx, i) for i, idx in enumerate(sel)])
             tok = torch.cat(sel)
             A, At = maps[img, tok], maps[img + k, tok]
-        total, off = 0.0, 0
-        for i, idx in enumerate(sel):
-            n = idx.numel()
-            loss, eq, sh = self._losses(A[off:off + n], At[off:off + n], i, th_inv[i])
-            off += n
+        total, parts = self._pass_losses(sel, A, At, th_inv)
+        for loss, eq, sh in parts:
             self._account(loss, eq, sh)
-            total = total + loss
         if sparse and prefetch and self.prefetch_at == "capture_bwd":
             # the next passes' VAE enqueued right behind the sparse capture backward (select()'s
             # backward calls it): the VAE then shares the GPU with the UNet backward's GEMMs and
@@ -326,13 +322,7 @@ class TokenOptimizer:
         rows = got.select(sel + sel)
         n = rows.shape[0] // 2
         A, At = rows[:n], rows[n:]
-        total, off, parts = 0.0, 0, []
-        for i, idx in enumerate(sel):
-            m = idx.numel()
-            loss, eq, sh = self._losses(A[off:off + m], At[off:off + m], i, th_inv[i])
-            off += m
-            parts.append((loss, eq, sh))
-            total = total + loss
+        total, parts = self._pass_losses(sel, A, At, th_inv)
         (total / self.accum).backward()
         return sel, parts
 
@@ -437,6 +427,30 @@ class TokenOptimizer:
         else:
             raise NotImplementedError
         return ptp_utils.furthest_point_sampling(attention_map_transformed, self.top_k, cand)
+
+    def _pass_losses(self, sel, A, At, th_inv):
+        """The losses of every image of a pass (optimize.py:425-437 per replica) on the stacked
+        selected rows A / At (image i's rows follow image i−1's).  Returns (the pass's total,
+        [(loss, eq, sh)] to account).  With equal row counts the sharpening and equivariance
+        losses of all images run as one launch each per direction (ops.*_loss_batch: each
+        image's loss and gradient are the per-image call's); the accounted statistics are then
+        the pass's sums."""
+        k = len(sel)
+        n = sel[0].numel() if k else 0
+        if SEL_BATCH and k > 1 and all(t.numel() == n for t in sel) and A.shape[0] == k * n:
+            sh = ops.sharpening_loss_batch(A, k, sigma=self.sigma, num_subjects=self.num_subjects)
+            eq = ops.equivariance_loss_batch(A, At, th_inv[:k], k)
+            loss = eq * self.w_eq + sh * self.w_sharp
+            total = loss.sum()
+            return total, [(total, eq.sum(), sh.sum())]
+        total, off, parts = 0.0, 0, []
+        for i, idx in enumerate(sel):
+            m = idx.numel()
+            loss, eq, sh = self._losses(A[off:off + m], At[off:off + m], i, th_inv[i])
+            off += m
+            parts.append((loss, eq, sh))
+            total = total + loss
+        return total, parts
 
     def _losses(self, A, At, index, theta_inv=None):
         """optimize.py:425-437 on the selected rows; ``index`` selects the warp's theta

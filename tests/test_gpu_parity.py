@@ -229,6 +229,34 @@ def test_selection_batched_equals_per_image(num_subjects):
         assert np.array_equal(N(sel[0]), g["fps10"])
 
 
+@pytest.mark.parametrize("num_subjects", [1, 2])
+def test_losses_batched_equal_per_image(num_subjects):
+    """ops.sharpening_loss_batch / equivariance_loss_batch (one launch per direction for the pass's
+    images) against the per-image losses: each image's loss and dA bit-identical, dAt (the
+    warp adjoint scatters with atomics) within 1e-6 of its largest magnitude."""
+    from stablekeypoints_amd import ops
+    k, n = 4, 10
+    A = T(np.stack([recipes.attention_like_maps(60 + i, n, 128) for i in range(k)]).reshape(k * n, 128, 128))
+    At = T(np.stack([recipes.attention_like_maps(70 + i, n, 128) for i in range(k)]).reshape(k * n, 128, 128))
+    th = torch.tensor([[[0.9, -0.1, 0.05], [0.12, 0.95, -0.2]], [[1.1, 0.0, 0.1], [0.0, 1.05, 0.0]],
+                       [[0.97, 0.2, -0.15], [-0.2, 0.97, 0.1]], [[1.0, 0.0, 0.0], [0.0, 1.0, 0.0]]],
+                      device=A.device)
+    w = torch.tensor([1.0, -2.0, 0.5, 3.0], device=A.device)
+    a1, at1 = A.clone().requires_grad_(), At.clone().requires_grad_()
+    sh = ops.sharpening_loss_batch(a1, k, sigma=2.0, num_subjects=num_subjects)
+    eq = ops.equivariance_loss_batch(a1, at1, th, k)
+    ((sh + 1000.0 * eq) * w).sum().backward()
+    for i in range(k):
+        a2, at2 = A[i * n:(i + 1) * n].clone().requires_grad_(), At[i * n:(i + 1) * n].clone().requires_grad_()
+        s2 = ops.sharpening_loss(a2, sigma=2.0, num_subjects=num_subjects)
+        e2 = ops.equivariance_loss_single(a2, at2, th[i])
+        ((s2 + 1000.0 * e2) * w[i]).backward()
+        assert torch.equal(sh[i], s2) and torch.equal(eq[i], e2)
+        assert torch.equal(a1.grad[i * n:(i + 1) * n], a2.grad)
+        err = float((at1.grad[i * n:(i + 1) * n] - at2.grad).abs().max() / at2.grad.abs().max())
+        assert err < 1e-6, err
+
+
 @pytest.mark.parametrize("hw", [(64, 64), (90, 90), (128, 128), (256, 256)])
 def test_topk_gaussian_register_kernel_vs_four_pass(hw):
     """The register-resident KL kernel (16-B aligned rows, h·w ≤ 16384) against the four-pass
