@@ -200,6 +200,15 @@ int skp_equiv_fwd_batch(const float* A, const float* At, int nb, int T, int h, i
 int skp_equiv_bwd_batch(const float* A, const float* At, int nb, int T, int h, int w, const float* theta_inv,
                         const float* gout, float* dA, float* dAt, void* stream);
 
+/* ---------------------------------------------------------------- Winograd as batched GEMMs
+ * The frozen UNet's small-image 3×3 convolutions (SD-1.5 ResnetBlock2D conv1/conv2 at 8²-32²):
+ * F(4×4, 3×3) with the fused kernels' points, as V = Bᵀ d B → M[p] = V[p]ᵀ U[p] (36 batched
+ * library GEMMs, host side) → y = Aᵀ M A (+ bias[k]) (+ residual).
+ * V (36, C, T) and M (36, T, K), T = B·(H/4)·(W/4) tiles, t = (b·H/4 + ty)·W/4 + tx.          */
+int skp_wino_in_transform(const float* x, int B, int C, int H, int W, float* V, void* stream);
+int skp_wino_out_transform(const float* M, int B, int K, int H, int W, const float* bias, const float* residual,
+                           float* y, void* stream);
+
 /* ---------------------------------------------------------------- Q·Kᵀ (fp32 MFMA)
  * C[b,m,n] = alpha · Σ_k A[b,m,k] · B[b,k,n] (+ C if accumulate), arbitrary element
  * strides; exact-f32 v_mfma_f32_32x32x2_f32.  Used for the capture logits

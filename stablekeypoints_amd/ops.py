@@ -1294,8 +1294,59 @@ def wino_eligible(B, C, K, H, W, min_workgroups=None):
     return wgs >= (WINO_MIN_WORKGROUPS if min_workgroups is None else min_workgroups)
 
 
+# Small-image, many-channel convolutions (the UNet's 8²-32² layers) as Winograd transforms + 36
+# batched library GEMMs (skp_wino_in_transform → torch.bmm → skp_wino_out_transform) instead of the
+# fused kernels: at these sizes the fused grids are a few hundred latency-bound workgroups.
+# SKP_WINO_GEMM_MAX_HW = the largest H·W that takes it (0 = off; A/B).
+WINO_GEMM_MAX_HW = int(os.environ.get("SKP_WINO_GEMM_MAX_HW", "1024"))
+WINO_GEMM_MIN_CH = 256
+# G of F(4×4, 3×3) at the points (0, 1, −1, 1/2, −2, ∞) (skp_conv.hip wino_weights_kernel's Gm)
+_WINO_G = ((1.0, 0.0, 0.0), (1 / 3, 1 / 3, 1 / 3), (-1 / 3, 1 / 3, -1 / 3), (-16 / 15, -8 / 15, -4 / 15),
+           (1 / 15, -2 / 15, 4 / 15), (0.0, 0.0, 1.0))
+
+
+def _wino_gemm_ok(B, C, K, H, W):
+    return (0 < H * W <= WINO_GEMM_MAX_HW and C >= WINO_GEMM_MIN_CH and K >= WINO_GEMM_MIN_CH
+            and H % 4 == 0 and W % 4 == 0 and B * (H // 4) * (W // 4) <= 65535)
+
+
+def _wino_u_gemm(weight, flip):
+    """U[p = 6i + j] (36, C, K) = (G g Gᵀ)[i][j] in fp64 → fp32, g = w[k][c] (flip 0) or
+    rot180(w[c][k]) (flip 1, the input-gradient convolution); cached per frozen weight like
+    _wino_u."""
+    ent = _WINO_U.get(id(weight))
+    if ent is None or ent[0]() is not weight:
+        key = id(weight)
+        ent = (_weakref.ref(weight, lambda _r, key=key: _WINO_U.pop(key, None)), {})
+        _WINO_U[key] = ent
+    hit = ent[1].get((flip, "gemm"))
+    if hit is not None and hit[0] == weight._version:
+        return hit[1]
+    w = weight.detach().double()
+    g = w.flip(2, 3).transpose(0, 1) if flip else w                 # (K, C, 3, 3) of this convolution
+    G = torch.tensor(_WINO_G, dtype=torch.float64, device=w.device)
+    U = torch.einsum("iu,kcuv,jv->ijck", G, g, G).reshape(36, g.shape[1], g.shape[0]).float().contiguous()
+    ent[1][(flip, "gemm")] = (weight._version, U)
+    return U
+
+
+def _wino_gemm_conv(x, weight, flip, bias, residual, K):
+    B, C, H, W = x.shape
+    T = B * (H // 4) * (W // 4)
+    U = _wino_u_gemm(weight, flip)
+    V = torch.empty(36, C, T, device=x.device, dtype=F32)
+    call("skp_wino_in_transform", ptr(x), B, C, H, W, ptr(V), stream(x.device))
+    M = torch.bmm(V.transpose(1, 2), U)                              # (36, T, K)
+    y = torch.empty(B, K, H, W, device=x.device, dtype=F32)
+    call("skp_wino_out_transform", ptr(M), B, K, H, W, ptr(bias) if bias is not None else None,
+         ptr(residual) if residual is not None else None, ptr(y), stream(x.device))
+    return y
+
+
 def _wino_conv(x, weight, flip, bias, residual, K):
     B, C, H, W = x.shape
+    if _wino_gemm_ok(B, C, K, H, W):
+        return _wino_gemm_conv(x, weight, flip, bias, residual, K)
     y = torch.empty(B, K, H, W, device=x.device, dtype=F32)
     # the kernels address x through 32-bit buffer offsets: batches above 2 GiB run in chunks
     per_img = C * H * W * 4

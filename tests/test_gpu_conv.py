@@ -24,6 +24,7 @@ def _need_gpu():
 def all_shapes(monkeypatch):
     from stablekeypoints_amd import ops
     monkeypatch.setattr(ops, "WINO_MIN_WORKGROUPS", 1)
+    monkeypatch.setattr(ops, "WINO_GEMM_MAX_HW", 0)   # these tests cover the fused kernels
     return ops
 
 
@@ -328,3 +329,47 @@ def test_resnet_block_shortcut_gemm_matches_miopen_form(monkeypatch):
     y2.square().sum().backward()
     assert ((y - y2).abs().max() / y2.abs().max()).item() < 3e-5
     assert ((gx - x.grad).abs().max() / x.grad.abs().max()).item() < 3e-5
+
+
+# ----------------------------------------------------------------------------- Winograd as batched GEMMs
+@pytest.mark.parametrize("B,C,K,H,W", [(8, 1280, 1280, 16, 16), (8, 2560, 1280, 8, 8), (8, 640, 640, 32, 32),
+                                       (3, 256, 320, 12, 20), (1, 320, 256, 4, 4)])
+@pytest.mark.parametrize("bias,res", [(False, False), (True, True)])
+def test_conv3x3_wino_gemm_vs_fp64(monkeypatch, B, C, K, H, W, bias, res):
+    """skp_wino_in_transform → 36 batched GEMMs → skp_wino_out_transform (the UNet's 8²-32²
+    layers) vs fp64 conv2d: forward with bias / residual, and the input gradient (the same path on
+    the rotated weights), at the fused kernels' 3e-5 bound."""
+    from stablekeypoints_amd import ops
+    monkeypatch.setattr(ops, "WINO_MIN_WORKGROUPS", 1)
+    monkeypatch.setattr(ops, "WINO_GEMM_MAX_HW", 1024)
+    assert ops._wino_gemm_ok(B, C, K, H, W) and ops._wino_gemm_ok(B, K, C, H, W)
+    g = torch.Generator().manual_seed(B + C + K + H + W)
+    x = torch.randn(B, C, H, W, generator=g)
+    w = torch.randn(K, C, 3, 3, generator=g) / (3 * C ** 0.5)
+    b = torch.randn(K, generator=g) if bias else None
+    r = torch.randn(B, K, H, W, generator=g) if res else None
+    dy = torch.randn(B, K, H, W, generator=g)
+    xd = x.to(DEV).requires_grad_(True)
+    y = ops.conv3x3(xd, w.to(DEV), None if b is None else b.to(DEV), None if r is None else r.to(DEV))
+    (y * dy.to(DEV)).sum().backward()
+    x64 = x.double().requires_grad_(True)
+    ref = F.conv2d(x64, w.double(), None if b is None else b.double(), 1, 1)
+    if r is not None:
+        ref = ref + r.double()
+    (ref * dy.double()).sum().backward()
+    assert _rel(y.detach().cpu(), ref.detach()) < 3e-5
+    assert _rel(xd.grad.cpu(), x64.grad) < 3e-5
+
+
+def test_conv3x3_wino_gemm_equals_fused_kernel_closely(monkeypatch):
+    """The GEMM form and the fused kernel compute the same F(4×4, 3×3) transform: at a UNet 16²
+    shape they agree far inside the fp64 bound."""
+    from stablekeypoints_amd import ops
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(8, 1280, 16, 16, generator=g).to(DEV)
+    w = (torch.randn(1280, 1280, 3, 3, generator=g) / (3 * 1280 ** 0.5)).to(DEV)
+    monkeypatch.setattr(ops, "WINO_GEMM_MAX_HW", 0)
+    y0 = ops.conv3x3(x, w)
+    monkeypatch.setattr(ops, "WINO_GEMM_MAX_HW", 1024)
+    y1 = ops.conv3x3(x, w)
+    assert ((y0 - y1).abs().max() / y0.abs().max()).item() < 2e-5
