@@ -4,7 +4,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 ROOT=$GRAFT_REPO_ROOT
-O=$ROOT/gpurun_out/r03au
+O=$ROOT/gpurun_out/${RUN_TAG:-r03au}
 mkdir -p $O
 cd $ROOT
 bash tools/tune_gemms.sh || { echo "tuning failed"; exit 1; }
