@@ -88,6 +88,25 @@ def _pmc_record(path, name, key, value):
 
 
 # ------------------------------------------------------------------------------ CPU baseline (port)
+def _cgroup_cpus():
+    """The job's CPU quota from cgroup v2 ``cpu.max`` ("quota period" or "max period"): raw text and
+    quota / period CPUs (None when unlimited or unreadable)."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            raw = open(path).read().strip()
+        except OSError:
+            continue
+        parts = raw.split()
+        cpus = None
+        if len(parts) == 2 and parts[0] != "max":
+            try:
+                cpus = float(parts[0]) / float(parts[1])
+            except ValueError:
+                cpus = None
+        return {"raw": raw, "cpus": cpus}
+    return {"raw": None, "cpus": None}
+
+
 def cpu_baseline(args):
     """One micro-iteration of the same workload on the host CPU: torch-CPU UNet/VAE
     (same architecture and seed) + the numpy oracle for every hot-path row (capture,
@@ -223,6 +242,16 @@ def cpu_baseline(args):
     # BASELINE.md's small figure: the same micro-iteration at N = 10 tokens (configs[0] scale)
     ctx10 = torch.randn(1, 10, 768).requires_grad_(True)
     rate10, dt10 = timed_rate(ctx10, 2)
+    # SURVEY §8(d)'s thread count, os.cpu_count(), as a second figure: one image (the model and
+    # allocator are warm from the legs above); more threads than the cgroup quota oversubscribe it
+    rate_np, dt_np = None, None
+    if nproc != threads:
+        torch.set_num_threads(nproc)
+        t0 = time.time()
+        micro_iteration(context)
+        dt_np = time.time() - t0
+        rate_np = 1.0 / dt_np
+        torch.set_num_threads(threads)
     cpu = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
@@ -231,7 +260,13 @@ def cpu_baseline(args):
                 break
     except OSError:
         pass
+    quota = _cgroup_cpus()
     return {"value": rate, "unit": "images/sec", "cores": threads, "kind": "port", "nproc": nproc,
+            "affinity_cpus": allowed, "cgroup_cpu_max": quota["raw"], "cgroup_cpus": quota["cpus"],
+            "threads_source": "OMP_NUM_THREADS" if os.environ.get("OMP_NUM_THREADS") else "sched_getaffinity",
+            "value_nproc_threads": rate_np, "nproc_threads_sample": (
+                f"1 image at N={args.tokens} with torch.set_num_threads(os.cpu_count() = {nproc}) after the legs "
+                f"above ({dt_np:.1f} s)" if dt_np else None),
             "cpu_model": cpu, "value_N10": rate10,
             "sample": f"2 timed images after 1 warm-up, 1 image = 1 token-opt micro-iteration (2 captures + select + "
                       f"losses + backward), N={args.tokens}, {args.res}²; torch-CPU SD-1.5 UNet/VAE + numpy oracle "
@@ -399,6 +434,8 @@ def main():
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
                     help="JSON with PMC-derived HBM bytes per launch of the roofline kernel")
     args = ap.parse_args()
+    if args.graph and args.prefetch < 1:
+        args.prefetch = 1   # only prefetched passes replay a graph (TokenOptimizer.micro_steps)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -448,7 +485,7 @@ def main():
     data = SyntheticDataset(n=16, size=args.res, seed=rank)
     imgs = [data[i]["img"][None].to(dev) for i in range(len(data))]
     timer = KernelTimer(["skp_aggregate", "skp_capture_fwd", "skp_capture_bwd", "skp_capture_maps_fwd",
-                         "skp_capture_maps_bwd", "skp_capture_maps_bwd_sel"])
+                         "skp_capture_maps_bwd", "skp_capture_maps_bwd_sel", "skp_topk_gaussian_batch"])
     ops.set_kernel_timer(timer)
 
     counter = [0]
@@ -568,6 +605,17 @@ def main():
             roof = rec_a
         else:
             extra["skp_aggregate"] = rec_a
+    sel = timer.summary("skp_topk_gaussian_batch")
+    if sel:
+        achieved = sel["bytes_per_launch"] / (sel["avg_ms"] * 1e-3)
+        traffic, traffic_src = _pmc_record(args.traffic, "skp_topk_gaussian_batch",
+                                           ("algorithmic_bytes_per_launch", sel["bytes_per_launch"]),
+                                           "hbm_bytes_per_launch")
+        extra["skp_topk_gaussian_batch"] = {
+            "bound": "hbm", "avg_ms": sel["avg_ms"], "launches": sel["launches"], "timing_source": timing_src,
+            "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,
+            "algorithmic_bytes_per_launch": sel["bytes_per_launch"], "traffic": traffic, "traffic_source": traffic_src,
+            "note": "the A8 KL ranking (kl_gauss_win_kernel) + the top-k sort of every image of a pass, one call"}
     for k in ("skp_capture_fwd", "skp_capture_bwd"):
         s_ = timer.summary(k)
         if s_:
@@ -600,7 +648,7 @@ def main():
                           "feature_upsample_res": args.upsample_res, "micro_batch": mb,
                           "parallelism": (f"dp{world} ({'RCCL' if backend == 'nccl' else backend} all-reduce of the "
                                           "token-embedding gradient)" if world > 1 else "dp1 (single process, no collective)"),
-                          "tuned_gemms": _tuned_gemms_in_use(), "hip_graph": bool(args.graph),
+                          "tuned_gemms": _tuned_gemms_in_use(), "hip_graph": opt._g is not None,
                           "vae_prefetch": args.prefetch, "prefetch_at": args.prefetch_at},
                "roofline": roof, "cpu_baseline": cpu, "kernels": extra,
                "last_loss": float(rec["loss"])}

@@ -389,10 +389,17 @@ def affine_params(rng_uniforms, degrees, scale, translate):
 
 
 def theta_inverse(theta):
-    """RandomAffineWithInverse.inverse (72-84): 2x3 part of the 3x3 inverse."""
+    """RandomAffineWithInverse.inverse (72-84): 2x3 part of the 3x3 inverse, in the reference's
+    arithmetic: fp32 ``torch.inverse`` (LU with partial pivoting through torch-CPU's LAPACK) of the
+    fp32 3x3 batch.  numpy's float32 ``linalg.inv`` rounds differently (1 ulp on ≈25% of entries
+    of tests/golden/theta_inv.npz), so this one call goes through torch-CPU, the reference's own
+    arithmetic dependency: bit-identical to the reference's recorded θ⁻¹ on the golden's host, and
+    to the reference on any other host (MKL's LU code path, and so the last bit, follows the CPU)."""
+    import torch
     B = theta.shape[0]
-    aug = np.concatenate([theta.astype(np.float64), np.tile(np.array([[[0, 0, 1.0]]]), (B, 1, 1))], axis=1)
-    return np.linalg.inv(aug)[:, :2, :].astype(np.float32)
+    aug = np.concatenate([np.asarray(theta, np.float32), np.tile(np.array([[[0, 0, 1.0]]], np.float32), (B, 1, 1))],
+                         axis=1)
+    return torch.inverse(torch.from_numpy(aug))[:, :2, :].numpy().astype(np.float32)
 
 
 def _fma32(a, b, c):

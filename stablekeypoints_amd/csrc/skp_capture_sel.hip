@@ -20,8 +20,9 @@
 //   sel_adj      per (bh, k): es[bh][k] = bicubicᵀ(E[bh][k])  (R² → s², separable through an LDS table
 //                of the adjoint weights, deterministic)
 //   sel_dense    per (bh, 128-token chunk): the dense part's adjoint, plus es at the selected tokens
-// sel_dense is the hot kernel.  One workgroup = R/16 waves; wave w owns output columns
-// [16w, 16w+16) of every row and lanes own token pairs (packed f32: v_pk_fma).  With R = S·RATIO
+// sel_dense is the hot kernel.  One workgroup = R/PW bands of 64 (or, at R/s = 4, 32) lanes; band
+// w owns output columns [PW·w, PW·w + PW) of every row and lanes own token pairs (packed f32:
+// v_pk_fma).  With R = S·RATIO
 // (RATIO a power of two, 4..16) the bicubic taps of a wave's pixels relative to its band are the
 // same for every wave and every row group, so the horizontal taps, the pixel loop and the register
 // indices are compile-time; the tap weights (RATIO distinct sets) sit in SGPRs, and so do the
@@ -207,45 +208,50 @@ struct SelLayers {   // up to 4 layers of the same s per launch
   float* dz[4];
 };
 
-// output columns per wave and row: 16 where R/s ≥ 8; 8 at R/s = 4 (the s = 32 layers), which keeps
-// the band at 6 low-res columns and the registers under 128 (4 waves per SIMD, 16-wave blocks)
+// output columns per band and row: 16 where R/s ≥ 8; 8 at R/s = 4 (the s = 32 layers), which keeps
+// the band at 6 low-res columns and the registers under 128 (4 waves per SIMD)
 template <int RATIO>
 constexpr int sel_pw() { return RATIO >= 8 ? 16 : 8; }
 template <int RATIO>
 constexpr int sel_nc() { return lo_rel(sel_pw<RATIO>() - 1, RATIO) + 6; }   // band columns: relative −2 … lo_rel(PW−1)+3
-
-// One block = (layer l, head bh, 128-token chunk); R/PW waves, wave w owns output columns
-// [PW·w, PW·w + PW) of every row, lanes own token pairs.  The 4 low-res z rows the current output
-// rows interpolate sit in an LDS ring Z[slot][column][lane] shared by all waves (bands overlap, so
-// each column is loaded once per block); the next row is fetched into registers at the start of a
-// phase and stored into the retired slot behind the emit's first barrier.  acc (the vertical adjoint
-// of the 4 rows) and the per-row V / Hs stay in registers.
+// lanes per band: a whole wave (128-token chunks) where R/s ≥ 8; a half-wave at R/s = 4, so a block
+// holds 2·R/PW bands in R/PW/2 waves (64-token chunks): the s = 32 block then needs 8 waves and
+// 57 KB of LDS like the s = 16 one, two share a CU, and one launch runs both (sel_dense_pair)
+template <int RATIO>
+constexpr int sel_lw() { return RATIO >= 8 ? 64 : 32; }
 template <int RATIO, int S>
-__global__ __launch_bounds__((S * RATIO / sel_pw<RATIO>()) * WAVE)
-void sel_dense_kernel(SelLayers sl, int BH, int H, int N, int K, const long long* __restrict__ tok, int nchunk,
-                      int njobs) {
+constexpr int sel_threads() { return (S * RATIO / sel_pw<RATIO>()) * sel_lw<RATIO>(); }
+template <int RATIO, int S>
+constexpr int sel_lds_m() { return (S * RATIO / sel_pw<RATIO>()) * sel_nc<RATIO>() * sel_lw<RATIO>(); }   // f2
+template <int RATIO, int S>
+constexpr int sel_lds_z() { return 4 * (S + 4) * sel_lw<RATIO>(); }                                       // f2
+
+// One job = (layer l, head bh, token chunk of 2·LW); NB = R/PW bands of LW lanes, band bw owns
+// output columns [PW·bw, PW·bw + PW) of every row, lanes own token pairs.  The 4 low-res z rows
+// the current output rows interpolate sit in an LDS ring Z[slot][column][lane] shared by all bands
+// (bands overlap, so each column is loaded once per block); the next row is fetched into registers
+// at the start of a phase and stored into the retired slot behind the emit's first barrier.  acc
+// (the vertical adjoint of the 4 rows) and the per-row V / Hs stay in registers.
+template <int RATIO, int S>
+__device__ __forceinline__ void sel_dense_body(const SelLayers& sl, int BH, int H, int N, int K,
+                                               const long long* __restrict__ tok, int nchunk, int job, f2* M, f2* Z) {
   constexpr int PW = sel_pw<RATIO>();
+  constexpr int LW = sel_lw<RATIO>();
   constexpr int R = S * RATIO;
-  constexpr int WAVES = R / PW;
+  constexpr int NB = R / PW;                      // bands
   constexpr int CS = PW / RATIO;                  // band step in low-res columns
   constexpr int NC = sel_nc<RATIO>();
-  constexpr int CPT = (S + WAVES - 1) / WAVES;    // ring columns each thread fetches per row
+  constexpr int CPT = (S + NB - 1) / NB;          // ring columns each thread fetches per row
+  constexpr int TPC = 2 * LW;                     // tokens per chunk
   static_assert(R % PW == 0 && PW % RATIO == 0, "band geometry");
-  __shared__ __attribute__((aligned(16))) f2 M[WAVES * NC * WAVE];   // band partials of one low-res row
-  __shared__ __attribute__((aligned(16))) f2 Z[4 * S * WAVE];        // ring of 4 low-res z rows
-
-  // XCD-major job order: XCD x walks a contiguous job range, so a head's 128-token chunks share
-  // one L2 (its z_low slab)
-  const int per = (njobs + 7) / 8;
-  const int job = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
-  if (job >= njobs) return;
   const int chunk = job % nchunk;
   const int bh = (job / nchunk) % BH;
   const int l = job / (nchunk * BH);
   const int b = bh / H;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int n0 = chunk * 128 + 2 * lane;
+  const int tid = threadIdx.x, lane = tid & (LW - 1);
+  // band of this thread: the wave (uniform) or, at LW = 32, the wave's half
+  const int bw = LW == WAVE ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid / LW;
+  const int n0 = chunk * TPC + 2 * lane;
   const int nl = min(n0, N - 2);                   // clamped load position (N even)
   const float* zl = sl.z[l] + (size_t)bh * S * S * N;
   const float2* pixl = sl.pix[l] + (size_t)bh * R * R;
@@ -263,30 +269,37 @@ void sel_dense_kernel(SelLayers sl, int BH, int H, int N, int K, const long long
   // phase u's taps exactly as the forward did, then every lane reads them as uniform values
   float wt[RATIO][4];
   {
-    const Taps4 t = bicubic_taps(lane < RATIO ? lane : 0, S, R);
+    const int wl = tid & 63;
+    const Taps4 t = bicubic_taps(wl < RATIO ? wl : 0, S, R);
 #pragma unroll
     for (int u = 0; u < RATIO; ++u)
 #pragma unroll
       for (int m = 0; m < 4; ++m)
         wt[u][m] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t.w[m]), u));
   }
-  auto col_abs = [&](int c) { return min(max(w * CS + c - 2, 0), S - 1); };
+  // ring rows carry two virtual columns each side (−2, −1 = column 0; S, S + 1 = column S − 1, as
+  // torch's clamped taps), so band slot c of band bw is ring column bw·CS + c: no clamp per read
+  constexpr int SP = S + 4;
   auto slot = [](int r) { return (r + 4) & 3; };   // virtual rows ≥ −2
   f2 pre[CPT];
   auto fetch = [&](int r) {   // z_low row r (clamped): this thread's ring columns, its lane's token pair
     const int rr = min(max(r, 0), S - 1);
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
-      const int col = w + k * WAVES;
+      const int col = bw + k * NB;
       if (col < S) pre[k] = *reinterpret_cast<const f2*>(zl + ((size_t)rr * S + col) * N + nl);
     }
   };
   auto stash = [&](int r) {
-    f2* zs = Z + slot(r) * S * WAVE;
+    f2* zs = Z + slot(r) * SP * LW;
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
-      const int col = w + k * WAVES;
-      if (col < S) zs[col * WAVE + lane] = pre[k];
+      const int col = bw + k * NB;
+      if (col < S) {
+        zs[(col + 2) * LW + lane] = pre[k];
+        if (col == 0) { zs[lane] = pre[k]; zs[LW + lane] = pre[k]; }
+        if (col == S - 1) { zs[(S + 2) * LW + lane] = pre[k]; zs[(S + 3) * LW + lane] = pre[k]; }
+      }
     }
   };
 #pragma unroll 1
@@ -304,21 +317,21 @@ void sel_dense_kernel(SelLayers sl, int BH, int H, int N, int K, const long long
   const f2 l2e = (f2)L2E;
 
   // low-res row r complete: merge the bands, add es at the selected tokens, store; then the
-  // fetched row `next` goes into the retired slot (every wave is past its reads of it)
+  // fetched row `next` goes into the retired slot (every band is past its reads of it)
   auto emit = [&](int r, const f2 (&v)[NC], int next) {
 #pragma unroll
-    for (int c = 0; c < NC; ++c) M[(w * NC + c) * WAVE + lane] = v[c];
+    for (int c = 0; c < NC; ++c) M[(bw * NC + c) * LW + lane] = v[c];
     __syncthreads();
-    const int n = chunk * 128 + 2 * lane;
-    for (int j = w; j < S; j += WAVES) {   // a wave per low-res column (uniform j)
+    const int n = chunk * TPC + 2 * lane;
+    for (int j = bw; j < S; j += NB) {   // a band per low-res column (uniform j per band)
       f2 s = (f2)0.0f;
       if (j == 0 || j == S - 1) {   // clamped edge columns: every (band, column) folding into j, band order
-        for (int w2 = 0; w2 < WAVES; ++w2)
+        for (int w2 = 0; w2 < NB; ++w2)
           for (int c = 0; c < NC; ++c)
-            if (min(max(w2 * CS + c - 2, 0), S - 1) == j) s += M[(w2 * NC + c) * WAVE + lane];
+            if (min(max(w2 * CS + c - 2, 0), S - 1) == j) s += M[(w2 * NC + c) * LW + lane];
       } else {                      // interior: one column per band, c = j + 2 − w2·CS (band order)
-        const int wlo = max(0, (j + 2 - NC + CS) / CS), whi = min(WAVES - 1, (j + 2) / CS);
-        for (int w2 = wlo; w2 <= whi; ++w2) s += M[(w2 * NC + j + 2 - w2 * CS) * WAVE + lane];
+        const int wlo = max(0, (j + 2 - NC + CS) / CS), whi = min(NB - 1, (j + 2) / CS);
+        for (int w2 = wlo; w2 <= whi; ++w2) s += M[(w2 * NC + j + 2 - w2 * CS) * LW + lane];
       }
       if (n < N) {
         for (unsigned m = mx; m; m &= m - 1) s.x += esl[((size_t)__builtin_ctz(m) * S + r) * S + j];   // k order
@@ -335,10 +348,10 @@ void sel_dense_kernel(SelLayers sl, int BH, int H, int N, int K, const long long
   for (int lo = -2; lo <= S - 2; ++lo) {
     const bool more = lo + 1 <= S - 2;             // the next phase needs row lo + 4
     if (more) fetch(lo + 4);
-    const f2* z0 = Z + slot(lo) * S * WAVE + lane;
-    const f2* z1 = Z + slot(lo + 1) * S * WAVE + lane;
-    const f2* z2 = Z + slot(lo + 2) * S * WAVE + lane;
-    const f2* z3 = Z + slot(lo + 3) * S * WAVE + lane;
+    const f2* z0 = Z + slot(lo) * SP * LW + bw * CS * LW + lane;
+    const f2* z1 = Z + slot(lo + 1) * SP * LW + bw * CS * LW + lane;
+    const f2* z2 = Z + slot(lo + 2) * SP * LW + bw * CS * LW + lane;
+    const f2* z3 = Z + slot(lo + 3) * SP * LW + bw * CS * LW + lane;
 #pragma unroll
     for (int v = 0; v < RATIO; ++v) {
       const int y = RATIO * (lo + 1) + RATIO / 2 + v;
@@ -347,7 +360,7 @@ void sel_dense_kernel(SelLayers sl, int BH, int H, int N, int K, const long long
       f2 V[NC], Hs[NC];
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
-        const int o = col_abs(c) * WAVE;
+        const int o = c * LW;
         f2 t = z0[o] * wt[u][0];
         t = __builtin_elementwise_fma(z1[o], (f2)wt[u][1], t);
         t = __builtin_elementwise_fma(z2[o], (f2)wt[u][2], t);
@@ -355,12 +368,12 @@ void sel_dense_kernel(SelLayers sl, int BH, int H, int N, int K, const long long
         V[c] = t;
         Hs[c] = (f2)0.0f;
       }
-      const float2* pp = pixl + (size_t)y * R + w * PW;
+      const float2* pp = pixl + (size_t)y * R + bw * PW;
 #pragma unroll
       for (int t = 0; t < PW; ++t) {
         const int ut = t % RATIO;
         const int c0 = lo_rel(t, RATIO) + 2;                             // band slot of the first tap
-        const float2 pd = pp[t];                                         // (mb, d), uniform
+        const float2 pd = pp[t];                                         // (mb, d), uniform per band
         f2 zv = V[c0] * wt[ut][0];
         zv = __builtin_elementwise_fma(V[c0 + 1], (f2)wt[ut][1], zv);
         zv = __builtin_elementwise_fma(V[c0 + 2], (f2)wt[ut][2], zv);
@@ -383,7 +396,7 @@ void sel_dense_kernel(SelLayers sl, int BH, int H, int N, int K, const long long
     if (lo < 0) {
 #pragma unroll
       for (int c = 0; c < NC; ++c) acc[1][c] += acc[0][c];   // rows −2, −1 clamp to row 0 (next slot)
-      __syncthreads();                                        // every wave past its reads of slot(lo)
+      __syncthreads();                                        // every band past its reads of slot(lo)
       if (more) stash(lo + 4);
       __syncthreads();
     } else {
@@ -400,14 +413,71 @@ void sel_dense_kernel(SelLayers sl, int BH, int H, int N, int K, const long long
   emit(S - 1, acc[0], S + 2);
 }
 
+// XCD-major job order: XCD x walks a contiguous job range, so a head's token chunks share one L2
+// (its z_low slab)
+__device__ __forceinline__ int xcd_job(int njobs) {
+  const int per = (njobs + 7) / 8;
+  return (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+}
+
+template <int RATIO, int S>
+__global__ __launch_bounds__((sel_threads<RATIO, S>()))
+void sel_dense_kernel(SelLayers sl, int BH, int H, int N, int K, const long long* __restrict__ tok, int nchunk,
+                      int njobs) {
+  __shared__ __attribute__((aligned(16))) f2 M[sel_lds_m<RATIO, S>()];   // band partials of one low-res row
+  __shared__ __attribute__((aligned(16))) f2 Z[sel_lds_z<RATIO, S>()];   // ring of 4 low-res z rows
+  const int job = xcd_job(njobs);
+  if (job >= njobs) return;
+  sel_dense_body<RATIO, S>(sl, BH, H, N, K, tok, nchunk, job, M, Z);
+}
+
+// Two layer classes (e.g. SD-1.5's s = 16 layers and its s = 32 layer at R = 128) in ONE grid of
+// equal-size blocks: per XCD, its share of class A's jobs first, then its share of class B's, so
+// the shorter class-B blocks fill the slots class A's last round leaves idle (two launches left
+// half of the CUs idle in the s = 16 launch's last round and ran the s = 32 launch alone).
+template <int RA, int SA, int RB, int SB>
+__global__ __launch_bounds__((sel_threads<RA, SA>()))
+void sel_dense_pair_kernel(SelLayers sa, int nca, int ja, SelLayers sb, int ncb, int jb, int BH, int H, int N, int K,
+                           const long long* __restrict__ tok) {
+  static_assert(sel_threads<RA, SA>() == sel_threads<RB, SB>(), "equal block sizes");
+  constexpr int MA = sel_lds_m<RA, SA>(), MB = sel_lds_m<RB, SB>();
+  constexpr int ZA = sel_lds_z<RA, SA>(), ZB = sel_lds_z<RB, SB>();
+  __shared__ __attribute__((aligned(16))) f2 M[MA > MB ? MA : MB];
+  __shared__ __attribute__((aligned(16))) f2 Z[ZA > ZB ? ZA : ZB];
+  const int pa = (ja + 7) / 8, pb = (jb + 7) / 8;   // per-XCD shares
+  const int xcd = blockIdx.x & 7, k = blockIdx.x >> 3;
+  if (k < pa) {
+    const int job = xcd * pa + k;
+    if (job < ja) sel_dense_body<RA, SA>(sa, BH, H, N, K, tok, nca, job, M, Z);
+  } else {
+    const int job = xcd * pb + (k - pa);
+    if (job < jb) sel_dense_body<RB, SB>(sb, BH, H, N, K, tok, ncb, job, M, Z);
+  }
+}
+
 template <int RATIO, int S>
 void launch_dense(const SelLayers& sl, int nl, int BH, int H, int N, int K, const long long* tok, hipStream_t st) {
-  const int nchunk = (N + 127) / 128;
+  const int nchunk = (N + 2 * sel_lw<RATIO>() - 1) / (2 * sel_lw<RATIO>());
   const int njobs = nl * BH * nchunk;
   const int grid = 8 * ((njobs + 7) / 8);
-  hipLaunchKernelGGL((sel_dense_kernel<RATIO, S>), dim3(grid), dim3((S * RATIO / sel_pw<RATIO>()) * WAVE), 0, st, sl,
-                     BH, H, N, K, tok, nchunk, njobs);
+  hipLaunchKernelGGL((sel_dense_kernel<RATIO, S>), dim3(grid), dim3(sel_threads<RATIO, S>()), 0, st, sl, BH, H, N, K,
+                     tok, nchunk, njobs);
 }
+
+template <int RA, int SA, int RB, int SB>
+void launch_dense_pair(const SelLayers& sa, int na, const SelLayers& sb, int nb, int BH, int H, int N, int K,
+                       const long long* tok, hipStream_t st) {
+  const int nca = (N + 2 * sel_lw<RA / SA>() - 1) / (2 * sel_lw<RA / SA>());
+  const int ncb = (N + 2 * sel_lw<RB / SB>() - 1) / (2 * sel_lw<RB / SB>());
+  const int ja = na * BH * nca, jb = nb * BH * ncb;
+  const int grid = 8 * ((ja + 7) / 8 + (jb + 7) / 8);
+  hipLaunchKernelGGL((sel_dense_pair_kernel<RA / SA, SA, RB / SB, SB>), dim3(grid), dim3(sel_threads<RA / SA, SA>()), 0,
+                     st, sa, nca, ja, sb, ncb, jb, BH, H, N, K, tok);
+}
+
+#ifndef SKP_SEL_PAIR
+#define SKP_SEL_PAIR 1   // 0: one sel_dense launch per layer size (A/B build)
+#endif
 
 // (R, S) pairs with a compiled sel_dense kernel
 bool dense_launch(int R, int S, const SelLayers& sl, int nl, int BH, int H, int N, int K, const long long* tok,
@@ -426,6 +496,21 @@ bool dense_launch(int R, int S, const SelLayers& sl, int nl, int BH, int H, int 
   SKP_SEL_CASE(32, 8)
   SKP_SEL_CASE(32, 4)
 #undef SKP_SEL_CASE
+  return false;
+}
+
+// the SD-1.5 capture layers at R = 128 (s = 16 ×3 and s = 32) as one sel_dense_pair launch
+bool dense_pair_launch(int R, int SA, const SelLayers& sa, int na, int SB, const SelLayers& sb, int nb, int BH, int H,
+                       int N, int K, const long long* tok, hipStream_t st) {
+  if (!SKP_SEL_PAIR) return false;
+  if (R == 128 && SA == 16 && SB == 32) {
+    launch_dense_pair<128, 16, 128, 32>(sa, na, sb, nb, BH, H, N, K, tok, st);
+    return true;
+  }
+  if (R == 128 && SA == 32 && SB == 16) {
+    launch_dense_pair<128, 16, 128, 32>(sb, nb, sa, na, BH, H, N, K, tok, st);
+    return true;
+  }
   return false;
 }
 
@@ -542,7 +627,10 @@ extern "C" int skp_capture_maps_bwd_sel(const float* const* z_low, const int* si
                      (size_t)(smax * (R + 1) + R * smax + SEL_ADJ_TILE * (R + 1)) * sizeof(float), st, t, E, BH * K,
                      smax, R, es);
   SKP_LAUNCH_CHECK();
-  // the dense part: layers of equal s share a launch (up to 4 per launch)
+  // the dense part: layers of equal s share a class (up to 4 per launch); two classes that have
+  // a paired kernel (SD-1.5: s = 16 and 32 at R = 128) run as one launch
+  SelLayers cls[SKP_MAX_LAYERS];
+  int cls_s[SKP_MAX_LAYERS], cls_n[SKP_MAX_LAYERS], ncls = 0;
   bool done[SKP_MAX_LAYERS] = {};
   for (int l = 0; l < L; ++l) {
     if (done[l]) continue;
@@ -557,7 +645,18 @@ extern "C" int skp_capture_maps_bwd_sel(const float* const* z_low, const int* si
       done[m] = true;
       ++nl;
     }
-    if (!dense_launch(R, sizes[l], sl, nl, BH, H, N, K, sel_tok, st)) {
+    cls[ncls] = sl;
+    cls_s[ncls] = sizes[l];
+    cls_n[ncls] = nl;
+    ++ncls;
+  }
+  if (ncls == 2 && dense_pair_launch(R, cls_s[0], cls[0], cls_n[0], cls_s[1], cls[1], cls_n[1], BH, H, N, K, sel_tok,
+                                     st)) {
+    SKP_LAUNCH_CHECK();
+    return SKP_OK;
+  }
+  for (int c = 0; c < ncls; ++c) {
+    if (!dense_launch(R, cls_s[c], cls[c], cls_n[c], BH, H, N, K, sel_tok, st)) {
       SKP_CHECK_ARG(false, "internal: no sel_dense kernel for this shape");
     }
     SKP_LAUNCH_CHECK();

@@ -327,6 +327,116 @@ __global__ __launch_bounds__(kRowThreads) void kl_gauss_reg_kernel(const float* 
   if (threadIdx.x == 0) kl[blockIdx.x] = acc;
 }
 
+// Block sum of N doubles at once (one pair of barriers for all N); sd holds N·(blockDim/64).
+template <int N>
+__device__ __forceinline__ void block_sum_n(double (&v)[N], double* sd) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    v[k] = wave_sum(v[k]);
+    if (lane == 0) sd[k * nw + wid] = v[k];
+  }
+  __syncthreads();
+  if (wid == 0) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      double x = lane < nw ? sd[k * nw + lane] : 0.0;
+      x = wave_sum(x);
+      if (lane == 0) sd[k * nw] = x;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < N; ++k) v[k] = sd[k * nw];
+}
+
+// KL(target ‖ softmax(map + eps)) per token for ONE subject (ptp_utils.py:97-108), one HBM read
+// of the row.  With u = fl(v + eps) − max (the softmax's shifted logit), t = g + eps the target
+// before normalisation and S_t = Σ t, S_e = Σ exp(u):
+//   KL = Σ (t/S_t)(log(t/S_t) − (u − log S_e)) = (Σ t·log t − Σ t·u)/S_t − log S_t + log S_e.
+// The Gaussian g (optimize_token.py:211-223, σ from the caller) is centred on the row's argmax;
+// outside a (2·wr + 1)² window around it g < ulp(eps)/2, so t == eps exactly in fp32 there (the
+// host picks wr from σ and eps) and those pixels enter only through Σ u and their count.  So per
+// pixel the row costs one exp (for S_e); the Gaussian, its logs and the t·u products run over the
+// window only (≈33² pixels at σ = 2, re-read from L2).  Agrees with the per-pixel kernel above to
+// fp32 rounding (≈3e-7 absolute on KL ≈ 5, tests/test_gpu_parity.py); rows of HW ≤ 4·NV·BT
+// floats, 16-B aligned, HW % 4 == 0 (the launcher checks); blockIdx.x = row of a (rows, HW) stack.
+template <int BT, int NV>
+__global__ __launch_bounds__(BT) void kl_gauss_win_kernel(const float* __restrict__ maps, int h, int w, float two_sig2,
+                                                         float eps, int wr, double* __restrict__ kl) {
+  __shared__ float sv[BT / 64];
+  __shared__ int si[BT / 64];
+  __shared__ double sd[6 * (BT / 64)];
+  const int HW = h * w, nq = HW >> 2;
+  const float* row = maps + (size_t)blockIdx.x * HW;
+  const float4* m4 = reinterpret_cast<const float4*>(row);
+  float4 v[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int q = threadIdx.x + j * BT;
+    v[j] = q < nq ? m4[q] : make_float4(0.f, 0.f, 0.f, 0.f);   // cached: the window re-reads hit L2
+  }
+  // torch.argmax of the row (find_k_max_pixels, num = 1): within a thread the indices increase,
+  // so a strict '>' (or the first NaN) keeps the first occurrence
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int q = threadIdx.x + j * BT;
+    if (q < nq) {
+      const float x[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (x[c] > best || (isnan(x[c]) && !isnan(best))) { best = x[c]; bi = 4 * q + c; }
+    }
+  }
+  block_argmax(best, bi, sv, si);
+  const float mx = best + eps;   // max of fl(v + eps): rounding is monotonic
+  double acc[2] = {0.0, 0.0};    // Σ exp(u), Σ u
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int q = threadIdx.x + j * BT;
+    if (q < nq) {
+      const float x[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+      double su = 0.0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float u = (x[c] + eps) - mx;
+        acc[0] += (double)expf(u);
+        su += (double)u;
+      }
+      acc[1] += su;
+    }
+  }
+  // the target window (find_k_max_pixels / image_h, times size = image_h, as gaussian_circles)
+  const float p0 = (((float)(bi / w) + 0.5f) / (float)h) * (float)h;
+  const float p1 = (((float)(bi % w) + 0.5f) / (float)h) * (float)h;
+  const int c0 = (int)floorf(p0), c1 = (int)floorf(p1);
+  const int i0 = max(0, c0 - wr), i1 = min(h - 1, c0 + wr);
+  const int j0 = max(0, c1 - wr), j1 = min(w - 1, c1 + wr);
+  const int ww = j1 - j0 + 1, nW = (i1 - i0 + 1) * ww;
+  double win[4] = {0.0, 0.0, 0.0, 0.0};   // Σ_W t, Σ_W t·log t, Σ_W t·u, Σ_W u
+  for (int k = threadIdx.x; k < nW; k += BT) {
+    const int i = i0 + k / ww, jj = j0 + k % ww;
+    const float di = ((float)i + 0.5f) - p0, dj = ((float)jj + 0.5f) - p1;
+    const float t = expf(-(dj * dj + di * di) / two_sig2) + eps;
+    const float u = (row[i * w + jj] + eps) - mx;
+    win[0] += (double)t;
+    win[1] += (double)t * (double)logf(t);
+    win[2] += (double)t * (double)u;
+    win[3] += (double)u;
+  }
+  double red[6] = {acc[0], acc[1], win[0], win[1], win[2], win[3]};
+  block_sum_n<6>(red, sd);
+  if (threadIdx.x == 0) {
+    const double e = (double)eps, nO = (double)(HW - nW);
+    const double St = red[2] + nO * e;
+    const double Stl = red[3] + (nO > 0.0 ? nO * e * (double)logf(eps) : 0.0);
+    const double Stu = red[4] + e * (red[1] - red[5]);
+    kl[blockIdx.x] = (Stl - Stu) / St - log(St) + log(red[0]);
+  }
+}
+
 // entropy of softmax(map) (ptp_utils.py:179-182; torch Categorical renormalises and clamps)
 __global__ __launch_bounds__(kRowThreads) void entropy_kernel(const float* __restrict__ maps, int h, int w,
                                                            double* __restrict__ ent) {
@@ -609,6 +719,9 @@ static int launch_sort(const double* keys, int T, int top_k, long long* out, hip
   return SKP_OK;
 }
 
+#ifndef SKP_KL_WIN
+#define SKP_KL_WIN 1   // 0: the per-pixel register kernel for one subject too (A/B build)
+#endif
 #ifndef SKP_KL_REG
 #define SKP_KL_REG 1   // 0: the four-pass kl_gauss_kernel for every shape (A/B build)
 #endif
@@ -627,7 +740,22 @@ extern "C" int skp_topk_gaussian_batch(const float* maps, int nb, int T, int h, 
   hipStream_t st = as_stream(stream);
   const int rows = nb * T, HW = h * w;
   const bool reg = SKP_KL_REG && (HW & 3) == 0 && (reinterpret_cast<uintptr_t>(maps) & 15) == 0;
-  if (reg && HW <= 4 * 1 * kRowThreads)
+  if (reg && SKP_KL_WIN && num_subjects == 1 && HW <= 4 * 16 * 1024) {
+    // window half-width: outside it exp(−d²/2σ²) < eps·2⁻²⁵ (< half an ulp of eps), i.e.
+    // d² ≥ 2σ²·(ln(1/eps) + 20); no usable bound (eps ≤ 0, σ ≤ 0, …): the whole row
+    int wr = h > w ? h : w;
+    const double kk = epsilon > 0.0f ? log(1.0 / (double)epsilon) + 20.0 : -1.0;
+    if (kk > 0.0 && sigma > 0.0f && isfinite(kk)) {
+      const double r = ceil(sqrt((double)two_sig2 * kk));
+      if (r < (double)wr) wr = (int)r;
+    }
+    if (HW <= 4 * 16 * 256)
+      hipLaunchKernelGGL((kl_gauss_win_kernel<256, 16>), dim3(rows), dim3(256), 0, st, maps, h, w, two_sig2, epsilon,
+                         wr, keys);
+    else
+      hipLaunchKernelGGL((kl_gauss_win_kernel<1024, 16>), dim3(rows), dim3(1024), 0, st, maps, h, w, two_sig2, epsilon,
+                         wr, keys);
+  } else if (reg && HW <= 4 * 1 * kRowThreads)
     hipLaunchKernelGGL(kl_gauss_reg_kernel<1>, dim3(rows), dim3(kRowThreads), 0, st, maps, h, w, num_subjects,
                        radius2, two_sig2, epsilon, keys);
   else if (reg && HW <= 4 * 2 * kRowThreads)

@@ -35,6 +35,11 @@ def pixel_from_weighted_avg(heatmaps, distance=5):
     return ops.pixel_from_weighted_avg(heatmaps, distance=distance)
 
 
+# default TTA batch bound: warped copies per capture pass × pixels per copy (10 copies at 512², the
+# measured TTA setting, profiles/r03ao_bench_tta.json)
+AUG_BATCH_PIXELS = 10 * 512 * 512
+
+
 @torch.no_grad()
 def run_image_with_context_augmented(ldm, image, context, indices, device="cuda",
                                      from_where=("down_cross", "mid_cross", "up_cross"), layers=(0, 1, 2, 3, 4, 5),
@@ -50,8 +55,10 @@ def run_image_with_context_augmented(ldm, image, context, indices, device="cuda"
     copy is captured (``indices`` gathered, bilinear to ``upscale_size``: collect_maps), then its
     map and a ones map are inverse-warped and summed.  Returns Σmaps / Σones with NaN → 0.
 
-    ``augmentation_batch`` (extra; None = all of this rank's iterations): how many iterations'
-    warped copies go through ONE batched VAE/UNet capture pass.  Every copy is captured on its
+    ``augmentation_batch`` (extra; None = as many iterations as ``AUG_BATCH_PIXELS`` allows: 10
+    at 512², 2 at SDXL's 1024²): how many iterations' warped copies go through ONE batched
+    VAE/UNet capture pass.  Peak activation memory grows linearly with it (the reference's loop
+    holds one copy at a time), so the default is bounded by image area.  Every copy is captured on its
     own (per-image maps, ``run_and_find_attn_per_image``), the thetas are drawn iteration by
     iteration exactly as the reference draws them, and the copies' contributions are summed in
     iteration order, so this is the reference's loop up to fp32 summation order and the GPU
@@ -80,7 +87,9 @@ def run_image_with_context_augmented(ldm, image, context, indices, device="cuda"
     sum_samples = torch.zeros(n, upscale_size, upscale_size, device=device)
     T = RandomAffineWithInverse(degrees=augment_degrees, scale=augment_scale, translate=augment_translate)
     iters = augmentation_iterations // num_gpus
-    chunk = iters if augmentation_batch is None else max(1, int(augmentation_batch))
+    if augmentation_batch is None:
+        augmentation_batch = max(1, AUG_BATCH_PIXELS // (img.shape[-1] * img.shape[-2] * max(1, num_gpus // world)))
+    chunk = max(1, int(augmentation_batch))
     done = 0
     while done < iters:
         c = min(chunk, iters - done)

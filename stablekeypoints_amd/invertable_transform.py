@@ -56,11 +56,15 @@ class RandomAffineWithInverse:
         return ops.affine_warp(img_tensor, _upload(theta.float(), img_tensor.device))
 
     def theta_inverse(self):
-        """2×3 part of the 3×3 inverse of each stored theta (invertable_transform.py:77-84)."""
-        theta = self.last_params["theta"].double()
-        aug = torch.cat([theta, torch.tensor([[[0.0, 0.0, 1.0]]], dtype=torch.float64).expand(theta.shape[0], -1, -1)],
+        """2×3 part of the 3×3 inverse of each stored theta (invertable_transform.py:77-84), with the
+        reference's arithmetic: ``torch.inverse`` of the fp32 batch on the host CPU (its θ lives on
+        the CPU: ``optimize.py:386``, ``eval.py:242``), so on any host it is bit-identical to the θ⁻¹
+        the reference would hand to affine_grid there (MKL's LU rounds the last bit per CPU code
+        path: tests/golden/theta_inv.npz was recorded on the build host)."""
+        theta = self.last_params["theta"].float()
+        aug = torch.cat([theta, torch.tensor([[[0.0, 0.0, 1.0]]], dtype=torch.float32).expand(theta.shape[0], -1, -1)],
                         dim=1)
-        return torch.inverse(aug)[:, :2, :].float()
+        return torch.inverse(aug)[:, :2, :].contiguous()
 
     def inverse(self, img_tensor):
         """invertable_transform.py:72-92: warp by the inverse of the stored thetas."""

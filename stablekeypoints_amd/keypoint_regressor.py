@@ -76,7 +76,16 @@ def find_best_indices(ldm, context, num_steps=100, device="cuda", noise_level=-1
         else:
             per = ptp_utils.run_and_find_attn_per_image(ldm, mine, context, noise_level=noise_level, device=device,
                                                         layers=layers, upsample_res=upsample_res,
-                                                        controllers=controllers)
+                                                        controllers=controllers, stacked=True)
+            if all(torch.is_tensor(p) for p in per) and _select_batched(top_k_strategy, top_k,
+                                                                         furthest_point_num_samples):
+                # image b's maps (in the reference's per-device order) in one (B', N, S, S) stack
+                stack = per[0] if len(per) == 1 else torch.stack(
+                    [p[b] for b in range(mine.shape[0]) for p in per])
+                indices_list.extend(_select_stack(stack, top_k, furthest_point_num_samples, top_k_strategy, sigma,
+                                                  num_subjects))
+                done += c
+                continue
             per_image = [[per[k][b] for k in range(len(per))] for b in range(mine.shape[0])]
         for attention_maps in per_image:
             for attention_map in attention_maps:
@@ -98,6 +107,29 @@ def find_best_indices(ldm, context, num_steps=100, device="cuda", noise_level=-1
     indices, counts = torch.unique(indices_list, return_counts=True)
     indices = indices[counts.argsort(descending=True)]
     return indices[:top_k]
+
+
+def _select_batched(strategy, top_k, n_cand):
+    """The one-launch-per-stage selection applies: a batched candidate ranking exists for the
+    strategy and the FPS kernel's bounds hold (top_k ≥ 2 picks from ≥ 2 candidates)."""
+    return strategy in ("gaussian", "consistent") and top_k >= 2 and n_cand >= 2
+
+
+def _select_stack(stack, top_k, n_cand, strategy, sigma, num_subjects):
+    """The reference's per-image candidates + furthest-point sampling (keypoint_regressor.py:95-112)
+    for every image of a (B, N, S, S) stack: one skp_topk_gaussian_batch (or the consistent
+    arange) and one skp_fps_batch launch, one device→host copy.  Returns the per-image index
+    tensors in stack order; an image whose FPS ran out of candidates keeps fewer, as the reference's
+    list does (ptp_utils.py:156-157)."""
+    from . import ops
+    B, N = stack.shape[:2]
+    if strategy == "gaussian":
+        cand = ops.find_top_k_gaussian_batch(stack, n_cand, sigma=sigma, num_subjects=num_subjects)
+    else:
+        cand = torch.arange(n_cand, device=stack.device).expand(B, n_cand)
+    sel, n = ops.furthest_point_sampling_batch(stack, top_k, cand)
+    sel, n = sel.cpu(), n.cpu()
+    return [sel[b, :int(n[b])] for b in range(B)]
 
 
 @torch.no_grad()

@@ -298,6 +298,9 @@ def capture_maps(zs, sizes, B, R):
 # A/B: 0 = the selected rows' gradient goes through the dense (B, N, R²) map gradient and
 # skp_capture_maps_bwd, as in r02
 SEL_BWD = os.environ.get("SKP_SEL_BWD", "1") != "0"
+# skp_capture_maps_bwd_sel's per-image row limit (32-bit lane masks in csrc/skp_capture_sel.hip);
+# more selected rows per image (a user --top_k > 32) take the dense backward
+SEL_MAXK = 32
 
 
 def capture_maps_sel_bwd_bytes(B, H, N, R, sizes, K):
@@ -416,7 +419,7 @@ class _SelectMaps(torch.autograd.Function):
         K = max(max(counts), 1)
         g = _c(g).view(-1, RR)
         scale = 1.0 / float(L * cm.H)
-        if SEL_BWD and N % 4 == 0:
+        if SEL_BWD and N % 4 == 0 and K <= SEL_MAXK:
             # (B, K) token table (−1 pads) and the (B, K, R²) gradient rows, in row order per image
             tt = torch.full((B, K), -1, dtype=torch.int64, device=g.device)
             gs = torch.zeros(B, K, RR, dtype=F32, device=g.device)
@@ -555,8 +558,10 @@ def find_top_k_gaussian_batch(maps, top_k, sigma=3, epsilon=1e-5, num_subjects=1
     top_k = min(int(top_k), T)
     out = torch.empty(nb, top_k, device=maps.device, dtype=torch.int64)
     kl = torch.empty(nb, T, device=maps.device, dtype=torch.float64)
-    call("skp_topk_gaussian_batch", ptr(maps), nb, T, h, w, int(top_k), float(sigma), float(epsilon),
-         int(num_subjects), ptr(out), ptr(kl), ptr(kl), stream(maps.device))
+    # algorithmic bytes: every map read once (the KL ranking; the sort's 8·T B per image are noise)
+    with _timed("skp_topk_gaussian_batch", maps.numel() * 4 + nb * T * 16):
+        call("skp_topk_gaussian_batch", ptr(maps), nb, T, h, w, int(top_k), float(sigma), float(epsilon),
+             int(num_subjects), ptr(out), ptr(kl), ptr(kl), stream(maps.device))
     return out
 
 

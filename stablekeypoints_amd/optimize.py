@@ -367,7 +367,7 @@ class TokenOptimizer:
             grad = eager_grad
         else:
             _, g, (s_in, s_th), (s_sel, s_parts, s_grad) = self._g
-            prev = self.context.grad if self._grad_acc is not None else None
+            prev = self.context.grad     # eager passes of this step too (zero_grad leaves None)
             s_in.copy_(inputs)
             s_th.copy_(th_inv)
             g.replay()

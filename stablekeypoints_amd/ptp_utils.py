@@ -335,7 +335,11 @@ def _collect_per_image(ldm, images, context, noise_level, device, layers, upsamp
                 ctl.reset()
                 continue
             maps = ctl.maps_per_image(B, ldm.feature_upsample_res, layers)
-            if stacked and indices is None and upsample_res in (-1, maps.shape[-1]):
+            if stacked and indices is None:
+                if upsample_res not in (-1, maps.shape[-1]):   # every image's maps in one resize launch
+                    Bm, Nm, R = maps.shape[:3]
+                    maps = ops.resize_bilinear(maps.view(Bm * Nm, R, R), upsample_res).view(
+                        Bm, Nm, upsample_res, upsample_res)
                 out.append(maps)
                 ctl.reset()
                 continue

@@ -34,9 +34,16 @@ def import_reference():
     ds = types.ModuleType("datasets")
     ds.__path__ = [os.path.join(REF, "datasets")]
     sys.modules["datasets"] = ds
+    # The reference's package has no __init__.py: this repo's own `unsupervised_keypoints` alias
+    # (a regular package) would shadow the namespace package, so pin the reference's path.
+    uk = types.ModuleType("unsupervised_keypoints")
+    uk.__path__ = [os.path.join(REF, "unsupervised_keypoints")]
+    sys.modules["unsupervised_keypoints"] = uk
     sys.path.insert(0, REF)
     from unsupervised_keypoints import ptp_utils, optimize, eval as ref_eval, optimize_token, invertable_transform
     from unsupervised_keypoints import keypoint_regressor
+    for m in (ptp_utils, optimize, ref_eval, invertable_transform, keypoint_regressor):
+        assert os.path.abspath(m.__file__).startswith(REF), m.__file__
     return types.SimpleNamespace(ptp_utils=ptp_utils, optimize=optimize, eval=ref_eval,
                                  optimize_token=optimize_token, invertable_transform=invertable_transform,
                                  keypoint_regressor=keypoint_regressor)
@@ -603,6 +610,62 @@ def gen_evaluate_tiny():
     np.savez_compressed(os.path.join(HERE, "evaluate_tiny.npz"), **out)
 
 
+def gen_theta_inv():
+    """The reference's own θ⁻¹ (invertable_transform.py:72-92): the 2×3 matrix its ``inverse``
+    hands to F.affine_grid, recorded by wrapping affine_grid, for seeded draws at the training
+    augmentation (main.py:160-180: 15°, scale [0.8, 1], translate 0.25) and the TTA one
+    (eval.py:224-228 defaults: 30°, [0.9, 1.1], 0.1), plus the inverse-warped image."""
+    it = REFM.invertable_transform
+    seen = []
+    orig = it.F.affine_grid
+
+    def rec(theta, size, align_corners=None):
+        seen.append(theta.detach().clone())
+        return orig(theta, size, align_corners=align_corners)
+    it.F.affine_grid = rec
+    out = {}
+    try:
+        for name, (deg, sc, tr) in (("train", (15, (0.8, 1.0), (0.25, 0.25))),
+                                     ("tta", (30, (0.9, 1.1), (0.1, 0.1)))):
+            T = it.RandomAffineWithInverse(degrees=deg, scale=sc, translate=tr)
+            torch.manual_seed(500 if name == "train" else 501)
+            img = torch.from_numpy(recipes.uniform(502, (64, 2, 24, 24)))
+            seen.clear()
+            T(img)
+            theta = T.last_params["theta"].clone()
+            inv_img = T.inverse(img)
+            out[f"{name}_theta"] = _np(theta)
+            out[f"{name}_theta_inv"] = _np(seen[1])
+            out[f"{name}_inv_img"] = _np(inv_img)
+        out["img"] = recipes.uniform(502, (64, 2, 24, 24))
+    finally:
+        it.F.affine_grid = orig
+    np.savez_compressed(os.path.join(HERE, "theta_inv.npz"), **out)
+
+
+def gen_entropy_ref():
+    """The reference's fp32 Categorical entropies behind entropy_sort (ptp_utils.py:179-185) on the
+    select golden's raw maps, recorded by wrapping the ``dist.Categorical`` it builds, plus the
+    ranking torch.argsort gives them: exact fp32 ties at the top-25 boundary are ordered by
+    torch's unspecified sort order."""
+    pu = REFM.ptp_utils
+    rec = []
+    orig = pu.dist.Categorical
+
+    class RecCat(orig):
+        def entropy(self):
+            e = super().entropy()
+            rec.append(e.detach().clone())
+            return e
+    pu.dist.Categorical = RecCat
+    try:
+        maps = torch.from_numpy(recipes.attention_like_maps(31, 500, 128))
+        order = pu.entropy_sort(maps, 25)
+    finally:
+        pu.dist.Categorical = orig
+    np.savez_compressed(os.path.join(HERE, "entropy_ref.npz"), entropy_f32=_np(rec[0]), entropy25=_np(order))
+
+
 def gen_interp():
     """Torch interpolation/warp numerics the kernels restate."""
     import torch.nn.functional as F
@@ -623,7 +686,7 @@ if __name__ == "__main__":
     torch.set_num_threads(8)
     which = sys.argv[1:] or ["capture_small", "capture_sd15", "argmax", "gaussian", "select", "losses",
                              "step_tiny", "interp", "eval_tiny", "best_indices_tiny", "regressor", "celeba_reader", "evaluate_tiny",
-                             "cub_reader"]
+                             "cub_reader", "theta_inv", "entropy_ref"]
     for w in which:
         print("generating", w, flush=True)
         globals()["gen_" + w]()

@@ -115,8 +115,12 @@ def test_tta_maps_tiny_vs_reference(monkeypatch):
 
 
 # "entropy" is not pinned end to end: see make_goldens.gen_best_indices_tiny
+@pytest.mark.parametrize("batched", [False, True])
 @pytest.mark.parametrize("strategy", ["gaussian", "consistent"])
-def test_find_best_indices_tiny_vs_reference(monkeypatch, strategy):
+def test_find_best_indices_tiny_vs_reference(monkeypatch, strategy, batched):
+    """batched=False: capture_batch=1, the reference's one capture + per-image selection per image.
+    batched=True: every image of the run in one capture pass and ONE batched top-k / FPS launch
+    (keypoint_regressor._select_stack); the stages are recorded from the stack it ranks."""
     from stablekeypoints_amd import keypoint_regressor as kr
     from stablekeypoints_amd.sd import TINY_IMAGE
     g = load_golden("best_indices_tiny")
@@ -144,10 +148,27 @@ def test_find_best_indices_tiny_vs_reference(monkeypatch, strategy):
         picks.append(N(fps(maps, top_k, cand)))
         return torch.as_tensor(picks[-1])
     monkeypatch.setattr(ptp_utils, "furthest_point_sampling", spy)
+    select_stack = kr._select_stack
+    n_batched = []
+
+    def spy_stack(stack, top_k, n_cand, strat, sigma, num_subjects):
+        from stablekeypoints_amd import ops
+        out = select_stack(stack, top_k, n_cand, strat, sigma, num_subjects)
+        c = ops.find_top_k_gaussian_batch(stack, n_cand, sigma=sigma) if strat == "gaussian" else \
+            torch.arange(n_cand, device=stack.device).expand(stack.shape[0], n_cand)
+        for b in range(stack.shape[0]):
+            maps_seen.append(stack[b].clone())
+            cands.append(N(c[b]))
+            picks.append(N(out[b]))
+        n_batched.append(stack.shape[0])
+        return out
+    monkeypatch.setattr(kr, "_select_stack", spy_stack)
     torch.manual_seed(300)   # the DataLoader shuffle draws its seed from the CPU generator
     idx = kr.find_best_indices(ldm, T(g["ctx"]), num_steps=5, device=DEV, upsample_res=S, layers=[0, 1, 2, 3],
                                top_k=4, furthest_point_num_samples=8, controllers=controllers, num_gpus=1,
-                               top_k_strategy=strategy, sigma=2.0, dataset=MemDS())
+                               top_k_strategy=strategy, sigma=2.0, dataset=MemDS(),
+                               capture_batch=8 if batched else 1)
+    assert n_batched == ([5] if batched else [])
     assert order == list(g[f"{strategy}_order"])
     ref_m, ref_c, ref_p = g[f"{strategy}_maps"], g[f"{strategy}_cands"], g[f"{strategy}_picks"]
     assert len(maps_seen) == len(ref_m)

@@ -258,10 +258,13 @@ def test_losses_batched_equal_per_image(num_subjects):
 
 
 @pytest.mark.parametrize("hw", [(64, 64), (90, 90), (128, 128), (256, 256)])
-def test_topk_gaussian_register_kernel_vs_four_pass(hw):
-    """The register-resident KL kernel (16-B aligned rows, h·w ≤ 16384) against the four-pass
-    kernel the launcher takes for a misaligned row: same ranking, KL within double rounding;
-    (256, 256) exercises the four-pass kernel on both sides and the batched launch."""
+def test_topk_gaussian_window_kernel_vs_per_pixel(hw):
+    """One subject on 16-B aligned rows takes the windowed KL kernel (skp_select.hip
+    kl_gauss_win_kernel: one exp per pixel, the Gaussian and its logs over the argmax's window
+    only); a misaligned copy of the same rows takes the per-pixel four-pass kernel.  Same
+    ranking, KL within 1e-6 relative (fp32 rounding of the closed form), both within 1e-6 of the
+    fp64 oracle.  Two subjects take the register-resident per-pixel kernel, bit-identical to the
+    four-pass one.  (256, 256) = find_best_indices' upsample_res: the 1024-thread window form."""
     from stablekeypoints_amd import ops
     h, w = hw
     rng = np.random.default_rng(h)
@@ -274,38 +277,66 @@ def test_topk_gaussian_register_kernel_vs_four_pass(hw):
         idx_r, kl_r = ops.find_top_k_gaussian(a[i], 12, sigma=2.0, return_kl=True)
         idx_m, kl_m = ops.find_top_k_gaussian(mis[i], 12, sigma=2.0, return_kl=True)
         assert torch.equal(idx_r, idx_m)
-        assert torch.allclose(kl_r, kl_m, rtol=1e-12, atol=0)
+        assert torch.allclose(kl_r, kl_m, rtol=1e-6, atol=0), float((kl_r - kl_m).abs().max())
+        if i == 0:
+            ko = O.kl_to_gaussian(maps[0], 2.0)
+            assert np.allclose(N(kl_r), ko, rtol=1e-6, atol=0)
+        idx2, kl2 = ops.find_top_k_gaussian(a[i], 12, sigma=2.0, num_subjects=2, return_kl=True)
+        idx2m, kl2m = ops.find_top_k_gaussian(mis[i], 12, sigma=2.0, num_subjects=2, return_kl=True)
+        assert torch.equal(idx2, idx2m) and torch.allclose(kl2, kl2m, rtol=1e-12, atol=0)
     batch = ops.find_top_k_gaussian_batch(a, 12, sigma=2.0)
     for i in range(3):
         assert torch.equal(batch[i], ops.find_top_k_gaussian(a[i], 12, sigma=2.0))
 
 
-def test_entropy_sort_raw_maps_pinned_expectation():
-    """entropy_sort on raw (near-uniform) maps (ptp_utils.py:165-187).  The reference ranks
-    fp32 Categorical entropies of softmax over 16384 pixels; on these maps those carry 2.25e-6 of
-    rounding noise (fp32 vs fp64, measured with torch-CPU on the golden's own inputs) while the 25
-    lowest entropies span only 3.4e-5 and the 25th/26th gap is 1e-7, so the reference's order is
-    partly its own rounding.  skp_entropy_sort ranks by fp64-accumulated entropy.  Pinned
-    expectation (measured): the candidate SET matches the reference's in >= 24 of 25 tokens, and
-    every position where the order differs swaps tokens whose fp64 entropies differ by less than
-    the reference's noise (2.5e-6); against the fp64 oracle the ranking differs only inside this
-    kernel's own fp32-exp noise (1e-7)."""
+def test_topk_gaussian_window_edges_and_sigma():
+    """The window clipped at every border (argmax in corners and on edges), σ large enough that
+    the window covers the whole row, and a non-default epsilon: KL within 1e-6 relative of the
+    fp64 oracle and the same ranking."""
     from stablekeypoints_amd import ops
-    g = load_golden("select")
+    rng = np.random.default_rng(9)
+    maps = rng.random((24, 64, 64), dtype=np.float32) * 0.5
+    spots = [(0, 0), (0, 63), (63, 0), (63, 63), (0, 30), (30, 0), (63, 30), (30, 63), (2, 2), (61, 5)]
+    for t, (r, c) in enumerate(spots):
+        maps[t, r, c] = 3.0
+    for sigma, eps in ((2.0, 1e-5), (3.0, 1e-5), (9.0, 1e-5), (2.0, 1e-3)):
+        idx, kl = ops.find_top_k_gaussian(T(maps), 24, sigma=sigma, epsilon=eps, return_kl=True)
+        ko = O.kl_to_gaussian(maps, sigma, epsilon=eps)
+        assert np.allclose(N(kl), ko, rtol=1e-6, atol=0), (sigma, eps, np.abs(N(kl) - ko).max())
+        assert np.array_equal(N(idx), np.argsort(ko, kind="stable")), (sigma, eps)
+
+
+def test_entropy_sort_raw_maps_vs_reference_ties():
+    """entropy_sort on raw (near-uniform) maps (ptp_utils.py:165-187) against the reference's OWN
+    fp32 entropies (recorded from the reference, tests/golden/entropy_ref.npz).  25/25 is
+    unreachable by construction: the reference's 25th and 26th smallest fp32 entropies are the
+    same float (asserted), and it keeps whichever torch.argsort's unspecified order among equal
+    keys puts first.  skp_entropy_sort ranks by fp64-accumulated entropy (ties by token id).
+    Recorded margin: at every position our token and the reference's have reference entropies
+    within the reference's own fp32 rounding noise (max |H32 − H64| over the 500 tokens,
+    2.25e-6), every token in only one of the two sets is tied with the reference's 25th value to
+    that noise, and against the fp64 oracle the order differs only inside the kernel's own exp
+    noise (1e-7)."""
+    from stablekeypoints_amd import ops
+    ge = load_golden("entropy_ref")
+    h32, ref = ge["entropy_f32"], ge["entropy25"]
     maps = recipes.attention_like_maps(31, 500, 128)
     ours = N(ops.entropy_sort(T(maps), 25))
-    ref = g["entropy25"]
     h64 = O.entropy_values(maps)
+    s = np.sort(h32)
+    assert s[24] == s[25]
+    noise = float(np.abs(h32 - h64).max())
     same_pos = int((ours == ref).sum())
-    overlap = len(set(ours.tolist()) & set(ref.tolist()))
-    d_ref = float(np.abs(h64[ours] - h64[ref]).max())
+    diff_set = set(ours.tolist()) ^ set(ref.tolist())
+    d_ref = float(np.abs(h32[ours] - h32[ref]).max())
     orc = O.entropy_sort(maps, 25)
     d_orc = float(np.abs(h64[ours] - h64[orc]).max())
-    print(f"\nentropy_sort on raw maps vs the reference: {same_pos}/25 same positions, {overlap}/25 same tokens, "
-          f"max fp64-entropy gap at differing positions {d_ref:.1e}; vs the fp64 oracle: "
-          f"{int((ours == orc).sum())}/25 same positions, gap {d_orc:.1e}")
-    assert overlap >= 24
-    assert d_ref <= 2.5e-6
+    print(f"\nentropy_sort on raw maps vs the reference: {same_pos}/25 same positions, "
+          f"{25 - len(diff_set) // 2}/25 same tokens, max reference-entropy gap at any position {d_ref:.1e} "
+          f"(noise {noise:.1e}); vs the fp64 oracle: {int((ours == orc).sum())}/25 positions, gap {d_orc:.1e}")
+    assert noise < 2.5e-6
+    assert d_ref <= noise
+    assert all(abs(h32[t] - s[24]) <= noise for t in diff_set)
     assert d_orc <= 1e-7
     assert np.all(np.diff(h64[ours]) >= -1e-7)   # ascending up to the kernel's noise
 
@@ -325,7 +356,7 @@ def test_kl_values_vs_oracle():
     from stablekeypoints_amd import ops
     maps = recipes.attention_like_maps(34, 64, 64)
     _, kl = ops.find_top_k_gaussian(T(maps), 10, sigma=2.0, return_kl=True)
-    assert np.allclose(N(kl), O.kl_to_gaussian(maps, 2.0), rtol=1e-5, atol=1e-7)
+    assert np.allclose(N(kl), O.kl_to_gaussian(maps, 2.0), rtol=1e-6, atol=1e-7)
 
 
 # ----------------------------------------------------------------------------- A11/A12
@@ -347,8 +378,39 @@ def test_losses_vs_golden():
     l.backward()
     print(f"\nwarp max|Δ| {dw:.1e}, equivariance loss rel {abs(float(l) / float(g['equiv']) - 1):.1e}")
     assert np.allclose(N(l), g["equiv"], rtol=1e-5)
-    assert np.allclose(N(A.grad), g["dA_equiv"], atol=1e-8, rtol=1e-4)
-    assert np.allclose(N(At.grad), g["dAt_equiv"], atol=1e-8, rtol=1e-4)
+    for ours, ref in ((N(A.grad), g["dA_equiv"]), (N(At.grad), g["dAt_equiv"])):
+        assert np.abs(ours - ref).max() <= 1e-4 * np.abs(ref).max()
+
+
+def test_random_affine_inverse_vs_reference():
+    """RandomAffineWithInverse.inverse (invertable_transform.py:72-92) on the reference's own θ:
+    θ⁻¹ is the reference's expression (fp32 torch.inverse of the augmented 3×3 on the host CPU),
+    bit for bit on this host; against the θ⁻¹ recorded from the reference on the golden's host
+    within 2 ulp (MKL's LU rounds per CPU code path); the inverse warp on the GPU within 1e-6 of
+    the reference's (losses.npz inv_At, theta_inv.npz at the training and TTA ranges)."""
+    from stablekeypoints_amd.invertable_transform import RandomAffineWithInverse
+    g = load_golden("losses")
+    tr = RandomAffineWithInverse(degrees=15, scale=(0.8, 1.0), translate=(0.25, 0.25))
+    tr.last_params = {"theta": torch.from_numpy(g["theta"])}
+    inv = N(tr.inverse(T(np.repeat(g["At"][None], 2, 0))))
+    d = float(np.abs(inv - g["inv_At"]).max())
+    gi = load_golden("theta_inv")
+    ulp = 0.0
+    for name in ("train", "tta"):
+        th = torch.from_numpy(gi[f"{name}_theta"])
+        tr.last_params = {"theta": th}
+        ti = N(tr.theta_inverse())
+        # the reference's own expression on THIS host (its θ lives on the CPU) — bit for bit
+        aug = torch.cat([th, torch.Tensor([[0, 0, 1]]).expand(th.shape[0], -1, -1)], dim=1)
+        assert np.array_equal(ti, N(torch.inverse(aug)[:, :2, :])), name
+        # vs the bits recorded on the golden's host: torch.inverse is MKL's LU, whose code path
+        # (and last-bit rounding) depends on the CPU; bit-identical there, ≤ 2 ulp on other CPUs
+        ref = gi[f"{name}_theta_inv"]
+        ulp = max(ulp, float((np.abs(ti - ref) / np.spacing(np.abs(ref).astype(np.float32))).max()))
+        d = max(d, float(np.abs(N(tr.inverse(T(gi["img"]))) - gi[f"{name}_inv_img"]).max()))
+    print(f"\nθ⁻¹ vs the golden host's: max {ulp:.0f} ulp; inverse warp vs the reference: max|Δ| {d:.1e}")
+    assert ulp <= 2
+    assert d <= 1e-6
 
 
 def test_affine_warp_adjoint():

@@ -140,3 +140,27 @@ def test_select_autograd_equals_dense_gather():
     for a, b in zip(za, zb):
         err = (a.grad - b.grad).abs().max().item() / b.grad.abs().max().item()
         assert err < 2e-5, err
+
+
+def test_select_more_rows_than_the_sparse_kernel_takes():
+    """top_k = 40 selected rows per image (the reference exposes --top_k, main.py:194) exceed the
+    sparse kernel's 32-row limit (ops.SEL_MAXK): CapturedMaps.select's backward takes the dense
+    skp_capture_maps_bwd and gives the dense gather's dz_low."""
+    from stablekeypoints_amd import ops
+    B, H, R, Nn, sizes = 2, 4, 64, 64, (8, 16)
+    zs = [recipes.random_logits(720 + i, (B * H, s * s, Nn), scale=2.0) for i, s in enumerate(sizes)]
+    g = torch.Generator().manual_seed(3)
+    rows = [torch.randperm(Nn, generator=g)[:40].to(DEV) for _ in range(B)]
+    assert rows[0].numel() > ops.SEL_MAXK
+    w = torch.from_numpy(recipes.random_logits(73, (80, R, R))).to(DEV)
+    za = [T(z).requires_grad_(True) for z in zs]
+    cm = ops.CapturedMaps(za, sizes, B, R)
+    (cm.select(rows) * w).sum().backward()
+    zb = [T(z).requires_grad_(True) for z in zs]
+    maps = ops.capture_maps(zb, sizes, B, R)
+    img = torch.cat([torch.full((40,), b, device=DEV) for b in range(B)])
+    (maps[img, torch.cat(rows)] * w).sum().backward()
+    for a, b in zip(za, zb):
+        assert torch.isfinite(a.grad).all()
+        err = (a.grad - b.grad).abs().max().item() / b.grad.abs().max().item()
+        assert err < 2e-5, err

@@ -133,6 +133,13 @@ def main():
                   "sharp": lambda: ops.sharpening_loss(A10, 2.0),
                   "equiv": lambda: ops.equivariance_loss_single(A10, At10, th)}[name]
             res[name] = timed(fn, args.iters)
+        elif name in ("kl4", "kl4_s2", "kl8_256"):   # the A8 KL ranking of a pass's images, one launch
+            nb, rr = (8, 256) if name == "kl8_256" else (4, R)
+            m4 = torch.rand(nb, N, rr, rr, device=dev, generator=g) ** 8
+            ns = 2 if name == "kl4_s2" else 1
+            res[name] = timed(lambda: ops.find_top_k_gaussian_batch(m4, 25, sigma=2.0, num_subjects=ns), args.iters)
+            res[name + "_GBs"] = m4.numel() * 4 / (res[name] * 1e-3) / 1e9 / 1e3
+            del m4
         elif name == "bwd16_dense":
             res[name] = timed(lambda: ops.capture_bwd(zs[16], 16, R, attn[16]), args.iters)
     agg_bytes = (4 * H * R * R * N + N * R * R) * 4
