@@ -392,20 +392,22 @@ __global__ __launch_bounds__(BT) void kl_gauss_win_kernel(const float* __restric
   }
   block_argmax(best, bi, sv, si);
   const float mx = best + eps;   // max of fl(v + eps): rounding is monotonic
-  double acc[2] = {0.0, 0.0};    // Σ exp(u), Σ u
+  // Σ exp(u) and Σ u: each float4's four terms summed in fp32 (pairwise), the float4 partials in
+  // fp64.  exp(u) = exp2(u·log2e) on v_exp_f32: u ≤ 0 and, for attention maps (values in [0, 1]),
+  // u ≥ −1 − eps, where the product's rounding and v_exp_f32's ≤ 1-ulp error keep each term within
+  // ≈2e-7 relative; the KL ranking's gaps are ≥ 1e-5 on the goldens (tests/test_gpu_parity.py)
+  double acc[2] = {0.0, 0.0};
+  constexpr float L2E = 1.4426950408889634f;
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
     const int q = threadIdx.x + j * BT;
     if (q < nq) {
-      const float x[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
-      double su = 0.0;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const float u = (x[c] + eps) - mx;
-        acc[0] += (double)expf(u);
-        su += (double)u;
-      }
-      acc[1] += su;
+      const float u0 = (v[j].x + eps) - mx, u1 = (v[j].y + eps) - mx;
+      const float u2 = (v[j].z + eps) - mx, u3 = (v[j].w + eps) - mx;
+      const float e0 = __builtin_amdgcn_exp2f(u0 * L2E), e1 = __builtin_amdgcn_exp2f(u1 * L2E);
+      const float e2 = __builtin_amdgcn_exp2f(u2 * L2E), e3 = __builtin_amdgcn_exp2f(u3 * L2E);
+      acc[0] += (double)((e0 + e1) + (e2 + e3));
+      acc[1] += (double)((u0 + u1) + (u2 + u3));
     }
   }
   // the target window (find_k_max_pixels / image_h, times size = image_h, as gaussian_circles)
