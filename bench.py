@@ -107,7 +107,30 @@ def _cgroup_cpus():
     return {"raw": None, "cpus": None}
 
 
-def cpu_baseline(args):
+def _cpu_leg_child(threads, tokens, limit_s):
+    """bench.py --cpu-leg THREADS in a child process (CPU only: it never initialises HIP), its
+    progress on our stderr; returns its JSON result, or {"error": ...} past ``limit_s``."""
+    import subprocess
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-leg", str(threads), "--tokens", str(tokens)]
+    try:
+        out = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, timeout=limit_s, text=True)
+    except subprocess.TimeoutExpired:
+        return {"error": f"timed out after {limit_s} s"}
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    return json.loads(lines[-1]) if out.returncode == 0 and lines else {"error": f"rc {out.returncode}"}
+
+
+def cpu_leg_main(args):
+    """--cpu-leg THREADS: one warm-up + one timed micro-iteration of the CPU port at --tokens with
+    THREADS torch threads; prints {"value": images/s, "seconds": s}.  Touches no GPU."""
+    threads = int(args.cpu_leg)
+    torch.set_num_threads(threads)
+    rate, dt = cpu_baseline(args, legs_only=True)
+    print(json.dumps({"value": rate, "seconds": dt, "threads": threads, "tokens": args.tokens}), flush=True)
+
+
+def cpu_baseline(args, legs_only=False):
     """One micro-iteration of the same workload on the host CPU: torch-CPU UNet/VAE
     (same architecture and seed) + the numpy oracle for every hot-path row (capture,
     aggregate, selection, losses and their backward).  kind = "port"."""
@@ -124,7 +147,8 @@ def cpu_baseline(args):
     # OMP_NUM_THREADS, when the host sets it, is the CPU share this job owns (a cgroup quota that
     # neither nproc nor the affinity mask shows); oversubscribing a quota only slows the baseline
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or allowed
-    torch.set_num_threads(threads)
+    if not legs_only:
+        torch.set_num_threads(threads)
     ldm = build_sd15(seed=0, device="cpu")
     R = args.res // 4
 
@@ -238,20 +262,18 @@ def cpu_baseline(args):
                   flush=True)
         return reps / (time.time() - t0), time.time() - t0
 
+    if legs_only:
+        return timed_rate(context, 1)
     rate, dt = timed_rate(context, 2)
     # BASELINE.md's small figure: the same micro-iteration at N = 10 tokens (configs[0] scale)
     ctx10 = torch.randn(1, 10, 768).requires_grad_(True)
     rate10, dt10 = timed_rate(ctx10, 2)
-    # SURVEY §8(d)'s thread count, os.cpu_count(), as a second figure: one image (the model and
-    # allocator are warm from the legs above); more threads than the cgroup quota oversubscribe it
-    rate_np, dt_np = None, None
+    # SURVEY §8(d)'s thread count, os.cpu_count(), as a second figure, in a child process (a fresh
+    # OpenMP pool of that size) under a time limit: more threads than the cgroup quota oversubscribe
+    # it, and the spinning pool can run many times slower than the quota's thread count
+    np_leg = None
     if nproc != threads:
-        torch.set_num_threads(nproc)
-        t0 = time.time()
-        micro_iteration(context)
-        dt_np = time.time() - t0
-        rate_np = 1.0 / dt_np
-        torch.set_num_threads(threads)
+        np_leg = _cpu_leg_child(nproc, 10, limit_s=150)
     cpu = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
@@ -264,9 +286,11 @@ def cpu_baseline(args):
     return {"value": rate, "unit": "images/sec", "cores": threads, "kind": "port", "nproc": nproc,
             "affinity_cpus": allowed, "cgroup_cpu_max": quota["raw"], "cgroup_cpus": quota["cpus"],
             "threads_source": "OMP_NUM_THREADS" if os.environ.get("OMP_NUM_THREADS") else "sched_getaffinity",
-            "value_nproc_threads": rate_np, "nproc_threads_sample": (
-                f"1 image at N={args.tokens} with torch.set_num_threads(os.cpu_count() = {nproc}) after the legs "
-                f"above ({dt_np:.1f} s)" if dt_np else None),
+            "value_nproc_threads_N10": np_leg and np_leg.get("value"), "nproc_threads_sample": (
+                f"os.cpu_count() = {nproc} threads (child process, OMP_NUM_THREADS={nproc}): "
+                + (f"1 image at N=10 after 1 warm-up, {np_leg['seconds']:.1f} s; compare value_N10" if np_leg and
+                   np_leg.get("value") else f"did not finish 1 warm-up + 1 image at N=10 within {150} s "
+                   f"({np_leg.get('error') if np_leg else 'no result'})")),
             "cpu_model": cpu, "value_N10": rate10,
             "sample": f"2 timed images after 1 warm-up, 1 image = 1 token-opt micro-iteration (2 captures + select + "
                       f"losses + backward), N={args.tokens}, {args.res}²; torch-CPU SD-1.5 UNet/VAE + numpy oracle "
@@ -433,7 +457,10 @@ def main():
     ap.add_argument("--stage-images", type=int, default=8, help="images per rank per step of a --stage bench")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
                     help="JSON with PMC-derived HBM bytes per launch of the roofline kernel")
+    ap.add_argument("--cpu-leg", type=int, default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.cpu_leg:
+        return cpu_leg_main(args)
     if args.graph and args.prefetch < 1:
         args.prefetch = 1   # only prefetched passes replay a graph (TokenOptimizer.micro_steps)
 

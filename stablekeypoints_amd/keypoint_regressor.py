@@ -63,12 +63,21 @@ def find_best_indices(ldm, context, num_steps=100, device="cuda", noise_level=-1
     indices_list = []
     steps = num_steps // num_gpus
     chunk = max(1, int(capture_batch))
+
+    def load(c):
+        """The next c loader batches, this rank's replica of each (the reference's per-device
+        image), on the device via pinned memory without waiting for the queued GPU work."""
+        groups = [_next(state)["img"] for _ in range(c)]
+        mine = torch.cat([g[rank:rank + 1] if world > 1 else g for g in groups])
+        if torch.device(device).type == "cuda":
+            return mine.pin_memory().to(device, non_blocking=True)
+        return mine.to(device)
+
     done = 0
+    nxt = load(min(chunk, steps)) if steps > 0 else None
     while done < steps:
         c = min(chunk, steps - done)
-        groups = [_next(state)["img"] for _ in range(c)]
-        # one replica = one image (the reference's per-device maps)
-        mine = torch.cat([g[rank:rank + 1] if world > 1 else g for g in groups]).to(device)
+        mine = nxt
         if mine.shape[0] == 1:
             per_image = [ptp_utils.run_and_find_attn(ldm, mine, context, layers=layers, noise_level=noise_level,
                                                      from_where=from_where, upsample_res=upsample_res,
@@ -82,8 +91,13 @@ def find_best_indices(ldm, context, num_steps=100, device="cuda", noise_level=-1
                 # image b's maps (in the reference's per-device order) in one (B', N, S, S) stack
                 stack = per[0] if len(per) == 1 else torch.stack(
                     [p[b] for b in range(mine.shape[0]) for p in per])
-                indices_list.extend(_select_stack(stack, top_k, furthest_point_num_samples, top_k_strategy, sigma,
-                                                  num_subjects))
+                sel, n = _select_stack(stack, top_k, furthest_point_num_samples, top_k_strategy, sigma,
+                                       num_subjects)
+                # the next batch is drawn and uploaded while this one's kernels run; then the picks
+                # come back (the loader's draws keep the reference's order)
+                nxt = load(min(chunk, steps - done - c)) if done + c < steps else None
+                sel, n = sel.cpu(), n.cpu()
+                indices_list.extend(sel[b, :int(n[b])] for b in range(sel.shape[0]))
                 done += c
                 continue
             per_image = [[per[k][b] for k in range(len(per))] for b in range(mine.shape[0])]
@@ -98,6 +112,8 @@ def find_best_indices(ldm, context, num_steps=100, device="cuda", noise_level=-1
                     cand = torch.arange(furthest_point_num_samples, device=attention_map.device)
                 indices_list.append(ptp_utils.furthest_point_sampling(attention_map, top_k, cand).cpu())
         done += c
+        if done < steps:
+            nxt = load(min(chunk, steps - done))
     indices_list = torch.cat(indices_list)
     if world > 1:
         import torch.distributed as dist
@@ -118,18 +134,16 @@ def _select_batched(strategy, top_k, n_cand):
 def _select_stack(stack, top_k, n_cand, strategy, sigma, num_subjects):
     """The reference's per-image candidates + furthest-point sampling (keypoint_regressor.py:95-112)
     for every image of a (B, N, S, S) stack: one skp_topk_gaussian_batch (or the consistent
-    arange) and one skp_fps_batch launch, one device→host copy.  Returns the per-image index
-    tensors in stack order; an image whose FPS ran out of candidates keeps fewer, as the reference's
-    list does (ptp_utils.py:156-157)."""
+    arange) and one skp_fps_batch launch.  Returns the device tensors ((B, top_k) picks, (B,)
+    counts): image b's picks are the first counts[b] (fewer when its FPS ran out of candidates, as
+    the reference's list, ptp_utils.py:156-157)."""
     from . import ops
     B, N = stack.shape[:2]
     if strategy == "gaussian":
         cand = ops.find_top_k_gaussian_batch(stack, n_cand, sigma=sigma, num_subjects=num_subjects)
     else:
         cand = torch.arange(n_cand, device=stack.device).expand(B, n_cand)
-    sel, n = ops.furthest_point_sampling_batch(stack, top_k, cand)
-    sel, n = sel.cpu(), n.cpu()
-    return [sel[b, :int(n[b])] for b in range(B)]
+    return ops.furthest_point_sampling_batch(stack, top_k, cand)
 
 
 @torch.no_grad()

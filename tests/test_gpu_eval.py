@@ -156,10 +156,11 @@ def test_find_best_indices_tiny_vs_reference(monkeypatch, strategy, batched):
         out = select_stack(stack, top_k, n_cand, strat, sigma, num_subjects)
         c = ops.find_top_k_gaussian_batch(stack, n_cand, sigma=sigma) if strat == "gaussian" else \
             torch.arange(n_cand, device=stack.device).expand(stack.shape[0], n_cand)
+        sel, n = out
         for b in range(stack.shape[0]):
             maps_seen.append(stack[b].clone())
             cands.append(N(c[b]))
-            picks.append(N(out[b]))
+            picks.append(N(sel[b, :int(n[b])]))
         n_batched.append(stack.shape[0])
         return out
     monkeypatch.setattr(kr, "_select_stack", spy_stack)

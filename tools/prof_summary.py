@@ -8,6 +8,8 @@ token-opt micro-iterations at the one-per-micro-step `sort_topk_kernel`, keeps t
 
 usage: python tools/prof_summary.py TRACE.csv --micro 8 [--out summary.csv]
        python tools/prof_summary.py TRACE.csv --steps 2 --accum 4   # split at the Adam kernels
+       python tools/prof_summary.py TRACE.csv --tail-ms 250 --images 24   # the last 250 ms of dispatches
+       (the --stage benches: their timed region is the end of the run; --images per region)
 (with batched micro-steps the per-image marker no longer bounds the timed region; the
 optimiser step's multi_tensor_apply kernels do)
 """
@@ -23,12 +25,18 @@ def main():
     ap.add_argument("--steps", type=int, default=0, help="optimiser steps in the timed region (Adam marker)")
     ap.add_argument("--accum", type=int, default=4, help="images per optimiser step (with --steps)")
     ap.add_argument("--marker", default="sort_topk_kernel")
+    ap.add_argument("--tail-ms", type=float, default=0.0, help="keep the dispatches of the trace's last TAIL_MS")
+    ap.add_argument("--images", type=int, default=0, help="images in the --tail-ms region (per-image figure)")
     ap.add_argument("--out", default=None)
     ap.add_argument("--top", type=int, default=30)
     args = ap.parse_args()
     rows = list(csv.DictReader(open(args.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    if args.steps:
+    if args.tail_ms:
+        t_end = max(int(r["End_Timestamp"]) for r in rows)
+        start = next(i for i, r in enumerate(rows) if int(r["Start_Timestamp"]) >= t_end - args.tail_ms * 1e6)
+        args.micro = args.images or 1
+    elif args.steps:
         adam = [i for i, r in enumerate(rows) if "multi_tensor_apply" in r["Kernel_Name"]]
         groups = []   # consecutive Adam kernels of one optimiser step
         for i in adam:
