@@ -40,9 +40,10 @@ class KernelTimer:
         self.events = {n: [] for n in names}
         self.nbytes = {n: [] for n in names}
         self.flops = {n: [] for n in names}
+        self.cycles = {n: [] for n in names}
         self.enabled = False
 
-    def record(self, name, nbytes, flops=0):
+    def record(self, name, nbytes, flops=0, cycles=0):
         timer = self
 
         class _Ctx:
@@ -60,6 +61,7 @@ class KernelTimer:
                     timer.events[name].append(self_.ev)
                     timer.nbytes[name].append(nbytes)
                     timer.flops[name].append(flops)
+                    timer.cycles[name].append(cycles)
                 return False
         return _Ctx()
 
@@ -69,7 +71,25 @@ class KernelTimer:
             return None
         ms = [a.elapsed_time(b) for a, b in ev]
         return {"launches": len(ms), "avg_ms": float(np.mean(ms)), "bytes_per_launch": float(np.mean(self.nbytes[name])),
-                "flop_per_launch": float(np.mean(self.flops[name]))}
+                "flop_per_launch": float(np.mean(self.flops[name])),
+                "issue_cycles_per_launch": float(np.mean(self.cycles[name]))}
+
+
+# gfx950 VALU issue capacity: 256 CUs × 4 SIMDs at the 2.4 GHz peak engine clock (MI355X_MICROARCH.md)
+SIMD_CYCLES_PER_S = 1024 * 2.4e9
+
+
+def issue_roofline(summary, model):
+    """The launch's minimal VALU issue time (its instruction-mix floor: ops.*_issue_cycles over
+    1024 SIMDs at 2.4 GHz) against its measured average: the roofline of a kernel whose binding
+    resource is VALU ISSUE with 8-cycle transcendentals in the mix, which the packed-FMA FLOP
+    peak does not see."""
+    cyc = summary.get("issue_cycles_per_launch") or 0.0
+    if not cyc:
+        return None
+    floor_ms = cyc / SIMD_CYCLES_PER_S * 1e3
+    return {"floor_ms": floor_ms, "avg_launch_ms": summary["avg_ms"], "frac": floor_ms / summary["avg_ms"],
+            "issue_cycles_per_launch": cyc, "model": model}
 
 
 def _pmc_record(path, name, key, value):
@@ -382,7 +402,8 @@ def stage_main(args, ldm, controllers, context, dev, world, rank, backend):
                 "algorithmic_flop_per_launch": flops, "algorithmic_bytes_per_launch": fw["bytes_per_launch"],
                 "hbm_achieved_GBps": fw["bytes_per_launch"] / t / 1e9,
                 "flop_model": "15 FLOP per (image, head, layer, pixel, token) + 8 per (row, low-res column, token); "
-                              "ops.capture_maps_flops"}
+                              "ops.capture_maps_flops",
+                "issue_roofline": issue_roofline(fw, "ops.capture_maps_issue_cycles")}
     if rank == 0:
         if args.stage == "find_indices":
             metric = f"it/s (find_best_indices, {args.res}², N={args.tokens} tokens, 1 image per it)"
@@ -600,7 +621,10 @@ def main():
                 "hbm_frac": fw["bytes_per_launch"] / t / HBM_PEAK,
                 "valu_busy_pmc": vb, "valu_busy_source": vb_src,
                 "flop_model": "15 FLOP per (image, head, layer, pixel, token) + 8 per (row, low-res column, token); "
-                              "ops.capture_maps_flops"}
+                              "ops.capture_maps_flops",
+                "issue_roofline": issue_roofline(fw, "ops.capture_maps_issue_cycles: per (image, head, layer, pixel, "
+                                                     "token) 4 packed tap FMAs, ½ v_max3, 1 packed FMA, 1 v_exp_f32 "
+                                                     "(8 cycles), 1 packed add, 1 packed FMA")}
     for name, model in (("skp_capture_maps_bwd_sel", "20 FLOP per (image, head, layer, pixel, token) + 16 per (row, "
                          "low-res column, token): the dense part; ops.capture_maps_sel_bwd_flops"),
                         ("skp_capture_maps_bwd", "24 FLOP per (image, head, layer, pixel, token) + 16 per (row, "
@@ -616,7 +640,8 @@ def main():
                            "algorithmic_flop_per_call": bw["flop_per_launch"], "flop_model": model,
                            "GB/s_algorithmic": bw["bytes_per_launch"] / t / 1e9,
                            "algorithmic_bytes_per_call": bw["bytes_per_launch"],
-                           "valu_busy_pmc": vb, "valu_busy_source": vb_src}
+                           "valu_busy_pmc": vb, "valu_busy_source": vb_src,
+                           "issue_roofline": issue_roofline(bw, "ops.capture_maps_sel_bwd_issue_cycles (the dense part)")}
     agg = timer.summary("skp_aggregate")
     if agg:
         achieved = agg["bytes_per_launch"] / (agg["avg_ms"] * 1e-3)

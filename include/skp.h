@@ -216,6 +216,15 @@ int skp_wino_out_transform(const float* M, int B, int K, int H, int W, const flo
 int skp_bgemm_f32(const float* A, long long sAb, long long sAm, long long sAk, const float* B, long long sBb,
                   long long sBk, long long sBn, float* C, long long sCb, long long sCm, long long sCn, int batch,
                   int M, int N, int K, float alpha, int accumulate, void* stream);
+/* skp_bgemm_f32 with a two-level batch: batch index z = o·hb + i, operand X's base X + o·sXo + i·sXb.
+ * Reads attention heads in place from the (B, S, H·d) projections (sXo = S·H·d, sXb = d, row stride
+ * H·d) and an operand shared by the B images with sXo = 0 — the captured layers' q·kᵀ and P·v with
+ * the batch-shared token embedding (ptp_utils.py:481-536) without head-permute or batch-expand copies.
+ * skp_bgemm_f32 is the hb = batch, sXo = 0 case. */
+int skp_bgemm_f32_2b(const float* A, long long sAo, long long sAb, long long sAm, long long sAk, const float* B,
+                     long long sBo, long long sBb, long long sBk, long long sBn, float* C, long long sCo, long long sCb,
+                     long long sCm, long long sCn, int batch, int hb, int M, int N, int K, float alpha, int accumulate,
+                     void* stream);
 
 /* ---------------------------------------------------------------- UNet-side: GroupNorm (+SiLU)
  * The token-opt backward runs through the frozen SD-1.5 UNet; its
@@ -233,6 +242,12 @@ int skp_groupnorm_fwd(const float* x, const float* gamma, const float* beta, con
 int skp_groupnorm_bwd(const float* x, const float* dy, const float* gamma, const float* beta, const float* shift,
                       const float* stats, int B, int C, long long HW, int G, int act, float* dx, double* partial,
                       void* stream);
+/* skp_groupnorm_bwd plus dres (may be null): dx = GroupNorm-backward(dy) + dres, the gradient of x's
+ * other consumer (the ResNet block's residual or shortcut, the spatial transformer's residual) added
+ * in the same pass instead of by the autograd engine (diffusers resnet.py / attention.py residuals). */
+int skp_groupnorm_bwd_add(const float* x, const float* dy, const float* gamma, const float* beta, const float* shift,
+                          const float* stats, int B, int C, long long HW, int G, int act, const float* dres, float* dx,
+                          double* partial, void* stream);
 /* Softmax backward of the UNet's math attention (diffusers-0.8.0 CrossAttention,
  * softmax(q kᵀ·scale) v): per row of P (rows × cols), dS = alpha·P ⊙ (dP − Σ P ⊙ dP),
  * written over dP (alpha = the logits' scale, baddbmm's backward folded in).  cols ≤ 16384. */
@@ -291,6 +306,10 @@ int skp_layernorm_fwd(const float* x, const float* gamma, const float* beta, lon
                       float* stats, void* stream);
 int skp_layernorm_bwd(const float* x, const float* dy, const float* gamma, const float* stats, long long rows, int C,
                       float* dx, void* stream);
+/* skp_layernorm_bwd plus dres (may be null): dx = LayerNorm-backward(dy) + dres, the transformer
+ * block's residual gradient (h = attn(norm(h)) + h, diffusers attention.py) added in the same pass. */
+int skp_layernorm_bwd_add(const float* x, const float* dy, const float* gamma, const float* stats, long long rows,
+                          int C, const float* dres, float* dx, void* stream);
 /* diffusers GEGLU (the UNet FeedForward's proj → chunk(2) → x·gelu(gate), exact-erf GELU):
  * h (rows, 2I) → out (rows, I), and its backward dh (rows, 2I) from dout (rows, I).
  * I % 4 == 0, 16-byte aligned.                                                 */

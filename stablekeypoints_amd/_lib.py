@@ -54,9 +54,12 @@ _SIGS = {
     "skp_equiv_bwd_batch": [_p, _p, _c_int, _c_int, _c_int, _c_int, _p, _p, _p, _p, _p],
     "skp_bgemm_f32": [_p, _c_ll, _c_ll, _c_ll, _p, _c_ll, _c_ll, _c_ll, _p, _c_ll, _c_ll, _c_ll, _c_int, _c_int,
                       _c_int, _c_int, _c_float, _c_int, _p],
+    "skp_bgemm_f32_2b": [_p, _c_ll, _c_ll, _c_ll, _c_ll, _p, _c_ll, _c_ll, _c_ll, _c_ll, _p, _c_ll, _c_ll, _c_ll,
+                         _c_ll, _c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _c_int, _p],
     "skp_groupnorm_workspace": [_c_int, _c_int, _c_ll, _c_int],
     "skp_groupnorm_fwd": [_p, _p, _p, _p, _c_int, _c_int, _c_ll, _c_int, _c_float, _c_int, _p, _p, _p, _p],
     "skp_groupnorm_bwd": [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_ll, _c_int, _c_int, _p, _p, _p],
+    "skp_groupnorm_bwd_add": [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_ll, _c_int, _c_int, _p, _p, _p, _p],
     "skp_residual_bias_add": [_p, _p, _p, _c_int, _c_int, _c_ll, _p, _p],
     "skp_softmax_bwd": [_p, _p, _c_ll, _c_int, _c_float, _p],
     "skp_softmax_fwd": [_p, _c_ll, _c_int, _p],
@@ -71,6 +74,7 @@ _SIGS = {
                                 _p],
     "skp_layernorm_fwd": [_p, _p, _p, _c_ll, _c_int, _c_float, _p, _p, _p],
     "skp_layernorm_bwd": [_p, _p, _p, _p, _c_ll, _c_int, _p, _p],
+    "skp_layernorm_bwd_add": [_p, _p, _p, _p, _c_ll, _c_int, _p, _p, _p],
     "skp_geglu_fwd": [_p, _c_ll, _c_int, _p, _p],
     "skp_geglu_bwd": [_p, _p, _c_ll, _c_int, _p, _p],
     "skp_wino_weights": [_p, _c_int, _c_int, _c_int, _p, _p],

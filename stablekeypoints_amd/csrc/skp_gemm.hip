@@ -108,12 +108,17 @@ struct Loader {
 };
 
 // BM×BN tile per workgroup as WM×WN waves of (BM/WM)×(BN/WN), each a grid of MI×NI 32×32 MFMA blocks
+// Batch index bz = o·hb + i (o < batch / hb): operand X's base is X + o·sXo + i·sXb, so a (B, S, H·d)
+// projection is a batch of B·H (S, d) heads in place (sXo = S·H·d, sXb = d, rows H·d apart) and an
+// operand shared by the B images is sXo = 0 — no head-permute or batch-expand copies (hb = batch,
+// sXo = 0: the plain one-stride batch).
 template <int MA, int MB, bool ACC, int BM, int BN, int WM, int WN>
 __global__ __launch_bounds__(WM * WN * WAVE) void bgemm_kernel(const float* __restrict__ A, long long sAb, long long sAm,
                                                          long long sAk, const float* __restrict__ B, long long sBb,
                                                          long long sBk, long long sBn, float* __restrict__ C,
                                                          long long sCb, long long sCm, long long sCn, int M, int N,
-                                                         int K, float alpha, int tiles_m, int tiles_n, int tiles) {
+                                                         int K, float alpha, int tiles_m, int tiles_n, int tiles,
+                                                         int hb, long long sAo, long long sBo, long long sCo) {
   constexpr int NT = WM * WN * WAVE;
   using LA = Loader<MA, BM, NT>;
   using LB = Loader<MB, BN, NT>;
@@ -149,8 +154,9 @@ __global__ __launch_bounds__(WM * WN * WAVE) void bgemm_kernel(const float* __re
     c.p = 0;
     c.m0 = tm * BM;
     c.n0 = tn * BN;
-    c.a = A + bz * sAb;
-    c.b = B + bz * sBb;
+    const int bo = bz / hb, bi = bz - bo * hb;
+    c.a = A + bo * sAo + bi * sAb;
+    c.b = B + bo * sBo + bi * sBb;
   };
   Cursor ld;
   decode(0, ld);
@@ -209,7 +215,8 @@ __global__ __launch_bounds__(WM * WN * WAVE) void bgemm_kernel(const float* __re
       if (p == npanel - 1) {
         const int t = t0 + ti * G;
         const int tn = t % tiles_n, tm = (t / tiles_n) % tiles_m, bz = t / (tiles_n * tiles_m);
-        float* Cb = C + bz * sCb;
+        const int bo = bz / hb, bi = bz - bo * hb;
+        float* Cb = C + bo * sCo + bi * sCb;
         // materialise the tile's row/column bases here: otherwise LICM hoists all MI·NI·16 store
         // addresses out of the panel loop and keeps them live across the MFMAs (register blow-up)
         int rb = tm * BM + wm + 4 * h, cb = tn * BN + wn + r;
@@ -245,17 +252,18 @@ int mode_of(const void* P, long long sk, long long smn, int k, int mn) {
 
 }  // namespace
 
-extern "C" int skp_bgemm_f32(const float* A, long long sAb, long long sAm, long long sAk, const float* B,
-                             long long sBb, long long sBk, long long sBn, float* C, long long sCb, long long sCm,
-                             long long sCn, int batch, int M, int N, int K, float alpha, int accumulate,
-                             void* stream) {
+extern "C" int skp_bgemm_f32_2b(const float* A, long long sAo, long long sAb, long long sAm, long long sAk,
+                                const float* B, long long sBo, long long sBb, long long sBk, long long sBn, float* C,
+                                long long sCo, long long sCb, long long sCm, long long sCn, int batch, int hb, int M,
+                                int N, int K, float alpha, int accumulate, void* stream) {
   SKP_CHECK_ARG(A && B && C, "null pointer");
   SKP_CHECK_ARG(batch > 0 && M > 0 && N > 0 && K > 0, "non-positive shape");
   SKP_CHECK_ARG(batch <= 65535, "batch > 65535");
+  SKP_CHECK_ARG(hb > 0 && batch % hb == 0, "hb must divide batch");
   const int ma = mode_of(A, sAk, sAm, K, M), mb = mode_of(B, sBk, sBn, K, N);
   // batch strides must keep each batch's base aligned for the vector paths
-  const int fa = (ma < 2 && sAb % 4 != 0) ? 2 : ma;
-  const int fb = (mb < 2 && sBb % 4 != 0) ? 2 : mb;
+  const int fa = (ma < 2 && (sAb % 4 != 0 || sAo % 4 != 0)) ? 2 : ma;
+  const int fb = (mb < 2 && (sBb % 4 != 0 || sBo % 4 != 0)) ? 2 : mb;
   // tile edge per dimension: 128 (twice the flops per loaded byte) unless its padding wastes more
   // than 64's; 128×128 runs 2 workgroups per CU (73.7 KB LDS), the others 4 (or 3)
   auto pick = [](int n) {
@@ -285,11 +293,11 @@ extern "C" int skp_bgemm_f32(const float* A, long long sAb, long long sAm, long 
   if (accumulate)                                                                                               \
     hipLaunchKernelGGL((bgemm_kernel<X, Y, true, TM, TN, WM, WN>), dim3(grid), dim3(WM * WN * WAVE), 0, st, A,  \
                        sAb, sAm, sAk, B, sBb, sBk, sBn, C, sCb, sCm, sCn, M, N, K, alpha, tiles_m, tiles_n,     \
-                       (int)tiles);                                                                             \
+                       (int)tiles, hb, sAo, sBo, sCo);                                                          \
   else                                                                                                          \
     hipLaunchKernelGGL((bgemm_kernel<X, Y, false, TM, TN, WM, WN>), dim3(grid), dim3(WM * WN * WAVE), 0, st, A, \
                        sAb, sAm, sAk, B, sBb, sBk, sBn, C, sCb, sCm, sCn, M, N, K, alpha, tiles_m, tiles_n,     \
-                       (int)tiles)
+                       (int)tiles, hb, sAo, sBo, sCo)
   // 128-edge tiles run 8 waves (4 per SIMD at two workgroups per CU) unless SKP_BGEMM_WAVES=4
   static const bool four_waves = [] {
     const char* e = getenv("SKP_BGEMM_WAVES");
@@ -321,4 +329,12 @@ extern "C" int skp_bgemm_f32(const float* A, long long sAb, long long sAm, long 
 #undef SKP_BG3
   SKP_LAUNCH_CHECK();
   return SKP_OK;
+}
+
+extern "C" int skp_bgemm_f32(const float* A, long long sAb, long long sAm, long long sAk, const float* B,
+                             long long sBb, long long sBk, long long sBn, float* C, long long sCb, long long sCm,
+                             long long sCn, int batch, int M, int N, int K, float alpha, int accumulate,
+                             void* stream) {
+  return skp_bgemm_f32_2b(A, 0, sAb, sAm, sAk, B, 0, sBb, sBk, sBn, C, 0, sCb, sCm, sCn, batch, batch, M, N, K, alpha,
+                          accumulate, stream);
 }

@@ -200,6 +200,7 @@ __global__ __launch_bounds__(kThreads) void gn_bwd_apply_kernel(const float* __r
                                                                 const float* __restrict__ shift, GNShape sh,
                                                                 const float* __restrict__ stats,
                                                                 const double* __restrict__ partial,
+                                                                const float* __restrict__ dres,
                                                                 float* __restrict__ dx) {
   __shared__ float sm[2];
   const int grp = blockIdx.x / sh.nsplit, sp = blockIdx.x % sh.nsplit;
@@ -219,12 +220,13 @@ __global__ __launch_bounds__(kThreads) void gn_bwd_apply_kernel(const float* __r
   const float* xb = x + (size_t)grp * sh.len;
   const float* db = dy + (size_t)grp * sh.len;
   float* ob = dx + (size_t)grp * sh.len;
+  const float* rb = dres ? dres + (size_t)grp * sh.len : nullptr;
   const long long lo = (long long)sp * kChunk, hi = min(sh.len, lo + kChunk);
   const long long step = VEC ? 4 : 1;
   for (long long e0 = lo + step * threadIdx.x; e0 < hi; e0 += step * kThreads) {
     const int c = g * sh.cpg + (int)(e0 / sh.HW);
     const float ga = gamma[c], be = beta[c], t = shift_of(shift, sh, grp, c);
-    float xv[4], dv[4], r[4];
+    float xv[4], dv[4], r[4], av[4] = {0.f, 0.f, 0.f, 0.f};
     if (VEC) {
       const float4 a = *reinterpret_cast<const float4*>(xb + e0), b = *reinterpret_cast<const float4*>(db + e0);
       xv[0] = a.x; xv[1] = a.y; xv[2] = a.z; xv[3] = a.w;
@@ -239,6 +241,16 @@ __global__ __launch_bounds__(kThreads) void gn_bwd_apply_kernel(const float* __r
       float gz = dv[k];
       if (ACT) gz *= silu_grad(xh * ga + be);
       r[k] = rstd * (gz * ga - ma - xh * mb);
+    }
+    if (rb) {   // + the gradient of x's other consumer (the residual / shortcut), in one pass
+      if (VEC) {
+        const float4 a = *reinterpret_cast<const float4*>(rb + e0);
+        av[0] = a.x; av[1] = a.y; av[2] = a.z; av[3] = a.w;
+      } else {
+        av[0] = rb[e0];
+      }
+#pragma unroll
+      for (int k = 0; k < (VEC ? 4 : 1); ++k) r[k] += av[k];
     }
     if (VEC) *reinterpret_cast<float4*>(ob + e0) = make_float4(r[0], r[1], r[2], r[3]);
     else ob[e0] = r[0];
@@ -304,14 +316,15 @@ extern "C" int skp_groupnorm_fwd(const float* x, const float* gamma, const float
   return SKP_OK;
 }
 
-extern "C" int skp_groupnorm_bwd(const float* x, const float* dy, const float* gamma, const float* beta,
-                                 const float* shift, const float* stats, int B, int C, long long HW, int G, int act,
-                                 float* dx, double* partial, void* stream) {
+extern "C" int skp_groupnorm_bwd_add(const float* x, const float* dy, const float* gamma, const float* beta,
+                                     const float* shift, const float* stats, int B, int C, long long HW, int G, int act,
+                                     const float* dres, float* dx, double* partial, void* stream) {
   SKP_CHECK_ARG(x && dy && gamma && beta && stats && dx && partial, "null pointer");
   GNShape sh;
   SKP_CHECK_ARG(make_shape(B, C, HW, G, sh), "bad shape (C must be divisible by G)");
   const bool vec = (HW % 4 == 0) && ((reinterpret_cast<uintptr_t>(x) & 15) == 0) &&
-                   ((reinterpret_cast<uintptr_t>(dy) & 15) == 0) && ((reinterpret_cast<uintptr_t>(dx) & 15) == 0);
+                   ((reinterpret_cast<uintptr_t>(dy) & 15) == 0) && ((reinterpret_cast<uintptr_t>(dx) & 15) == 0) &&
+                   ((reinterpret_cast<uintptr_t>(dres) & 15) == 0);
   hipStream_t st = as_stream(stream);
   const dim3 grid(B * G * sh.nsplit);
 #define SKP_GN_B(K, V, A, ...) hipLaunchKernelGGL((K<V, A>), grid, dim3(kThreads), 0, st, __VA_ARGS__)
@@ -324,15 +337,21 @@ extern "C" int skp_groupnorm_bwd(const float* x, const float* dy, const float* g
   }
   SKP_LAUNCH_CHECK();
   if (vec) {
-    if (act) SKP_GN_B(gn_bwd_apply_kernel, true, true, x, dy, gamma, beta, shift, sh, stats, partial, dx);
-    else SKP_GN_B(gn_bwd_apply_kernel, true, false, x, dy, gamma, beta, shift, sh, stats, partial, dx);
+    if (act) SKP_GN_B(gn_bwd_apply_kernel, true, true, x, dy, gamma, beta, shift, sh, stats, partial, dres, dx);
+    else SKP_GN_B(gn_bwd_apply_kernel, true, false, x, dy, gamma, beta, shift, sh, stats, partial, dres, dx);
   } else {
-    if (act) SKP_GN_B(gn_bwd_apply_kernel, false, true, x, dy, gamma, beta, shift, sh, stats, partial, dx);
-    else SKP_GN_B(gn_bwd_apply_kernel, false, false, x, dy, gamma, beta, shift, sh, stats, partial, dx);
+    if (act) SKP_GN_B(gn_bwd_apply_kernel, false, true, x, dy, gamma, beta, shift, sh, stats, partial, dres, dx);
+    else SKP_GN_B(gn_bwd_apply_kernel, false, false, x, dy, gamma, beta, shift, sh, stats, partial, dres, dx);
   }
 #undef SKP_GN_B
   SKP_LAUNCH_CHECK();
   return SKP_OK;
+}
+
+extern "C" int skp_groupnorm_bwd(const float* x, const float* dy, const float* gamma, const float* beta,
+                                 const float* shift, const float* stats, int B, int C, long long HW, int G, int act,
+                                 float* dx, double* partial, void* stream) {
+  return skp_groupnorm_bwd_add(x, dy, gamma, beta, shift, stats, B, C, HW, G, act, nullptr, dx, partial, stream);
 }
 
 extern "C" int skp_residual_bias_add(const float* a, const float* h, const float* bias, int B, int C, long long HW,

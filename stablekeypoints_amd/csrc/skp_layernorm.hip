@@ -5,7 +5,8 @@
 // ATen's kernel runs at ≈1.7 TB/s on these shapes.
 //   forward:  mean, rstd = 1/sqrt(var + eps) (biased variance, two-pass), y = x̂·γ + β;
 //             (mean, rstd) per row saved for the backward
-//   backward: g = dy·γ, dx = rstd·(g − mean(g) − x̂·mean(g·x̂))
+//   backward: g = dy·γ, dx = rstd·(g − mean(g) − x̂·mean(g·x̂)) [+ dres: the gradient of the other
+//             consumer of x — the transformer block's residual — added in the same pass]
 #include "skp_common.h"
 
 using namespace skp;
@@ -62,7 +63,8 @@ __global__ __launch_bounds__(64 * kRowsPerBlock) void ln_bwd_kernel(const float*
                                                                     const float* __restrict__ dy,
                                                                     const float* __restrict__ gamma,
                                                                     const float2* __restrict__ stats, long long rows,
-                                                                    int C, float* __restrict__ dx) {
+                                                                    int C, const float* __restrict__ dres,
+                                                                    float* __restrict__ dx) {
   const long long row = (long long)blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
   if (row >= rows) return;
   const int lane = threadIdx.x & 63, C4 = C >> 2;
@@ -89,12 +91,19 @@ __global__ __launch_bounds__(64 * kRowsPerBlock) void ln_bwd_kernel(const float*
   }
   const float mg = wave_sum(sg) / (float)C, mgx = wave_sum(sgx) / (float)C;
   float4* o = reinterpret_cast<float4*>(dx + row * C);
+  const float4* rr = reinterpret_cast<const float4*>(dres + row * C);
 #pragma unroll
   for (int i = 0; i < NQ; ++i) {
     const int q = lane + 64 * i;
-    if (q < C4)
-      o[q] = make_float4(rstd * (g[i].x - mg - xh[i].x * mgx), rstd * (g[i].y - mg - xh[i].y * mgx),
-                         rstd * (g[i].z - mg - xh[i].z * mgx), rstd * (g[i].w - mg - xh[i].w * mgx));
+    if (q < C4) {
+      float4 v = make_float4(rstd * (g[i].x - mg - xh[i].x * mgx), rstd * (g[i].y - mg - xh[i].y * mgx),
+                             rstd * (g[i].z - mg - xh[i].z * mgx), rstd * (g[i].w - mg - xh[i].w * mgx));
+      if (dres) {   // the autograd engine's sum of the two gradients, in one pass
+        const float4 a = rr[q];
+        v = make_float4(v.x + a.x, v.y + a.y, v.z + a.z, v.w + a.w);
+      }
+      o[q] = v;
+    }
   }
 }
 
@@ -126,9 +135,10 @@ extern "C" int skp_layernorm_fwd(const float* x, const float* gamma, const float
   return SKP_OK;
 }
 
-extern "C" int skp_layernorm_bwd(const float* x, const float* dy, const float* gamma, const float* stats, long long rows,
-                                 int C, float* dx, void* stream) {
+extern "C" int skp_layernorm_bwd_add(const float* x, const float* dy, const float* gamma, const float* stats,
+                                     long long rows, int C, const float* dres, float* dx, void* stream) {
   SKP_CHECK_ARG(x && dy && gamma && stats && dx, "null pointer");
+  SKP_CHECK_ARG(!dres || aligned16(dres), "dres must be 16-byte aligned");
   SKP_CHECK_ARG(rows > 0 && C > 0, "non-positive shape");
   SKP_CHECK_ARG(C % 4 == 0 && C <= 2048, "C must be a multiple of 4, at most 2048");
   SKP_CHECK_ARG((rows + kRowsPerBlock - 1) / kRowsPerBlock <= 0x7fffffffLL, "too many rows");
@@ -140,7 +150,7 @@ extern "C" int skp_layernorm_bwd(const float* x, const float* dy, const float* g
   const float2* S = reinterpret_cast<const float2*>(stats);
   const int nq = (C / 4 + 63) / 64;
 #define SKP_LNB(Q) \
-  hipLaunchKernelGGL((ln_bwd_kernel<Q>), grid, dim3(64 * kRowsPerBlock), 0, st, x, dy, gamma, S, rows, C, dx)
+  hipLaunchKernelGGL((ln_bwd_kernel<Q>), grid, dim3(64 * kRowsPerBlock), 0, st, x, dy, gamma, S, rows, C, dres, dx)
   if (nq <= 1) SKP_LNB(1);
   else if (nq <= 2) SKP_LNB(2);
   else if (nq <= 4) SKP_LNB(4);
@@ -148,4 +158,9 @@ extern "C" int skp_layernorm_bwd(const float* x, const float* dy, const float* g
 #undef SKP_LNB
   SKP_LAUNCH_CHECK();
   return SKP_OK;
+}
+
+extern "C" int skp_layernorm_bwd(const float* x, const float* dy, const float* gamma, const float* stats, long long rows,
+                                 int C, float* dx, void* stream) {
+  return skp_layernorm_bwd_add(x, dy, gamma, stats, rows, C, nullptr, dx, stream);
 }

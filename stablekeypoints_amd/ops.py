@@ -31,8 +31,8 @@ class _NoTimer:
         return False
 
 
-def _timed(name, nbytes=0, flops=0):
-    return _TIMER.record(name, nbytes, flops) if _TIMER is not None else _NoTimer()
+def _timed(name, nbytes=0, flops=0, cycles=0):
+    return _TIMER.record(name, nbytes, flops, cycles) if _TIMER is not None else _NoTimer()
 
 
 def _c(t, dtype=F32):
@@ -59,6 +59,112 @@ def bgemm(a, b, alpha=1.0, out=None, accumulate=False):
          b.stride(2), ptr(out), out.stride(0), out.stride(1), out.stride(2), Z, M, N, K, float(alpha),
          int(accumulate), stream(a.device))
     return out
+
+
+def bgemm_2b(a, sa, b, sb, out, so, batch, hb, M, N, K, alpha=1.0, accumulate=False):
+    """skp_bgemm_f32_2b: for z = o·hb + i, out_z = alpha · a_z @ b_z with operand X_z at
+    X + o·sX[0] + i·sX[1], row / column strides sX[2], sX[3] (elements; a: (M, K), b: (K, N),
+    out: (M, N))."""
+    call("skp_bgemm_f32_2b", ptr(a), *sa, ptr(b), *sb, ptr(out), *so, int(batch), int(hb), int(M), int(N), int(K),
+         float(alpha), int(accumulate), stream(a.device))
+    return out
+
+
+class CaptureLogitsHeads(torch.autograd.Function):
+    """z = q kᵀ · scale for the B·H heads of a captured layer read in place: q the layer's (B, S, H·d)
+    to_q projection, k the ONE (1, N, H·d) to_k projection of the token embedding the batch shares
+    (ptp_utils.py:493 / 534) — no head-permute copy of q and no batch-expanded copy of k.  Output
+    (B·H, S, N), the head-major layout the capture consumes.  Backward: dq straight into the (B, S,
+    H·d) layout; dk per image into a (B, N, H·d) scratch summed over the images (the expand's
+    reduction)."""
+
+    @staticmethod
+    def forward(ctx, qf, k1, H, scale):
+        qf, k1 = _c16(qf), _c16(k1)
+        B, S, C = qf.shape
+        N, d = k1.shape[1], C // H
+        z = torch.empty(B * H, S, N, device=qf.device, dtype=F32)
+        bgemm_2b(qf, (S * C, d, C, 1), k1, (0, d, 1, C), z, (H * S * N, S * N, N, 1), B * H, H, S, N, d, scale)
+        ctx.save_for_backward(qf, k1)
+        ctx.meta = (H, float(scale))
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        qf, k1 = ctx.saved_tensors
+        H, scale = ctx.meta
+        B, S, C = qf.shape
+        N, d = k1.shape[1], C // H
+        dz = _c16(dz)
+        dq = dk1 = None
+        if ctx.needs_input_grad[0]:
+            dq = torch.empty_like(qf)
+            bgemm_2b(dz, (H * S * N, S * N, N, 1), k1, (0, d, C, 1), dq, (S * C, d, C, 1), B * H, H, S, d, N, scale)
+        if ctx.needs_input_grad[1]:
+            dkb = torch.empty(B, N, C, device=qf.device, dtype=F32)
+            bgemm_2b(dz, (H * S * N, S * N, 1, N), qf, (S * C, d, C, 1), dkb, (N * C, d, C, 1), B * H, H, N, d, S,
+                     scale)
+            dk1 = dkb.sum(dim=0, keepdim=True) if B > 1 else dkb
+        return dq, dk1, None, None
+
+
+class AttnPVHeads(torch.autograd.Function):
+    """out = P v per head into the (B, S, H·d) layout to_out reads: P (B·H, S, N) the captured layer's
+    softmax, v the ONE (1, N, H·d) to_v projection of the shared token embedding (ptp_utils.py:
+    500-502 / 540-541, the normal-path output of a captured layer) — no batch-expanded copy of v and
+    no heads-to-batch permute of the output.  Backward: dP = dout vᵀ; dv per image summed over the
+    images."""
+
+    @staticmethod
+    def forward(ctx, P, v1, H):
+        P, v1 = _c16(P), _c16(v1)
+        BH, S, N = P.shape
+        B, C = BH // H, v1.shape[2]
+        d = C // H
+        out = torch.empty(B, S, C, device=P.device, dtype=F32)
+        bgemm_2b(P, (H * S * N, S * N, N, 1), v1, (0, d, C, 1), out, (S * C, d, C, 1), BH, H, S, d, N)
+        ctx.save_for_backward(P, v1)
+        ctx.H = H
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        P, v1 = ctx.saved_tensors
+        H = ctx.H
+        BH, S, N = P.shape
+        B, C = BH // H, v1.shape[2]
+        d = C // H
+        dout = _c16(dout)
+        dP = dv1 = None
+        if ctx.needs_input_grad[0]:
+            dP = torch.empty_like(P)
+            bgemm_2b(dout, (S * C, d, C, 1), v1, (0, d, 1, C), dP, (H * S * N, S * N, N, 1), BH, H, S, N, d)
+        if ctx.needs_input_grad[1]:
+            dvb = torch.empty(B, N, C, device=P.device, dtype=F32)
+            bgemm_2b(P, (H * S * N, S * N, 1, N), dout, (S * C, d, C, 1), dvb, (N * C, d, C, 1), BH, H, N, d, S)
+            dv1 = dvb.sum(dim=0, keepdim=True) if B > 1 else dvb
+        return dP, dv1, None
+
+
+def capture_logits_heads(qf, k1, heads, scale):
+    """(B·H, S, N) logits of a captured layer from its (B, S, H·d) query projection and the shared
+    (1, N, H·d) key projection (CaptureLogitsHeads)."""
+    _lib.require_device(qf, k1)
+    return CaptureLogitsHeads.apply(qf, k1, int(heads), float(scale))
+
+
+def attn_pv_heads(P, v1, heads):
+    """(B, S, H·d) = per-head P v with the shared (1, N, H·d) value projection (AttnPVHeads)."""
+    _lib.require_device(P, v1)
+    return AttnPVHeads.apply(P, v1, int(heads))
+
+
+def heads_eligible(qf, k1, heads):
+    """The in-place head GEMMs take fp32 (B, S, H·d) / (1, N, H·d) projections with d, S·H·d and N
+    multiples of 4 (16-B aligned heads for the vector loads)."""
+    C = qf.shape[-1]
+    return (qf.dtype == F32 and k1.dtype == F32 and qf.dim() == 3 and k1.dim() == 3 and k1.shape[0] == 1
+            and C % heads == 0 and (C // heads) % 4 == 0 and k1.shape[1] % 4 == 0 and k1.shape[2] == C)
 
 
 class CaptureLogits(torch.autograd.Function):
@@ -199,6 +305,31 @@ def capture_maps_flops(B, H, N, R, sizes):
     max 1 + (z − m)·log2e as an FMA 2 + exp 1 + Σ 1, normalise-and-accumulate FMA 2 — and per
     (image, head, layer, output row, low-res column, token) 8 for the vertical bicubic pass."""
     return sum(B * H * N * (15 * R * R + 8 * R * s) for s in sizes)
+
+
+# VALU issue cost on gfx950 (MI355X_MICROARCH.md, "vector-instruction ISSUE cost"): a wave64
+# instruction occupies its SIMD 4 cycles (v_fma_f32 / v_pk_fma_f32 / v_max3_f32 …), 8 for the
+# transcendentals (v_exp_f32); a packed f32 instruction does 2 elements per lane.  SIMD-cycles per
+# element of one f32 op: packed 4/128, transcendental 8/64.
+_PK, _TR = 4.0 / 128, 8.0 / 64
+
+
+def capture_maps_issue_cycles(B, H, N, R, sizes):
+    """Minimal VALU issue cycles (summed over SIMDs) of one skp_capture_maps_fwd launch: per (image,
+    head, layer, pixel, token) the 4 horizontal taps (4 packed FMA), the max (½ v_max3), the exp
+    argument (1 packed FMA), v_exp_f32 (transcendental), Σ (1 packed add) and the normalised
+    accumulate (1 packed FMA); per (row, low-res column, token) the 4 vertical taps."""
+    per_px = 4 * _PK + 0.5 * 4.0 / 64 + _PK + _TR + _PK + _PK
+    return sum(B * H * N * (per_px * R * R + 4 * _PK * R * s) for s in sizes)
+
+
+def capture_maps_sel_bwd_issue_cycles(B, H, N, R, sizes):
+    """Minimal VALU issue cycles of the dense part of skp_capture_maps_bwd_sel: per (image, head,
+    layer, pixel, token) 4 horizontal taps, the exp argument, v_exp_f32, ×(−dot) and the 4-tap
+    horizontal adjoint (packed f32 except the exp); per (row, low-res column, token) the vertical
+    pass and the vertical adjoint (4 + 4 packed FMA)."""
+    per_px = 4 * _PK + _PK + _TR + _PK + 4 * _PK
+    return sum(B * H * N * (per_px * R * R + 8 * _PK * R * s) for s in sizes)
 
 
 def capture_maps_bwd_flops(B, H, N, R, sizes):
@@ -365,7 +496,8 @@ def _capture_maps_run(zs, sizes, B, R):
     zp = (ctypes.c_void_p * L)(*[z.data_ptr() for z in zs])
     sp = (ctypes.c_int * L)(*[int(s) for s in sizes])
     stp = (ctypes.c_void_p * L)(*[st.data_ptr() for st in stats])
-    with _timed("skp_capture_maps_fwd", capture_maps_bytes(B, H, N, R, sizes), capture_maps_flops(B, H, N, R, sizes)):
+    with _timed("skp_capture_maps_fwd", capture_maps_bytes(B, H, N, R, sizes), capture_maps_flops(B, H, N, R, sizes),
+                capture_maps_issue_cycles(B, H, N, R, sizes)):
         call("skp_capture_maps_fwd", ctypes.cast(zp, ctypes.POINTER(ctypes.c_void_p)), sp, L, B, H, N, R,
              ptr(out), ctypes.cast(stp, ctypes.POINTER(ctypes.c_void_p)), stream(dev))
     return out, stats
@@ -391,7 +523,7 @@ def capture_maps_bwd_sel(zs, sizes, B, R, tok_table, gsel, gscale, stats):
     tok_table = tok_table.to(device=dev, dtype=torch.int64).contiguous()
     gsel = _c(gsel)
     with _timed("skp_capture_maps_bwd_sel", capture_maps_sel_bwd_bytes(B, H, N, R, sizes, K),
-                capture_maps_sel_bwd_flops(B, H, N, R, sizes)):
+                capture_maps_sel_bwd_flops(B, H, N, R, sizes), capture_maps_sel_bwd_issue_cycles(B, H, N, R, sizes)):
         call("skp_capture_maps_bwd_sel", arr(zs), sp, L, B, H, N, R, ptr(tok_table), K, ptr(gsel), float(gscale),
              arr(stats), arr(dzs), ptr(ws), stream(dev))
     return dzs
@@ -804,6 +936,52 @@ class GroupNormAct(torch.autograd.Function):
         return dx, None, None, None, None, None, None
 
 
+class GroupNormActRes(torch.autograd.Function):
+    """GroupNormAct that also hands x on (``x_pass``, the same values) to its other consumer — the
+    residual or shortcut of a ResNet block / spatial transformer — so that consumer's gradient
+    comes back to THIS node and is added inside the backward kernel (skp_groupnorm_bwd_add) instead
+    of by a separate autograd accumulation pass over the activation."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, groups, eps, act, shift):
+        xc = _c(x)
+        B, C = xc.shape[:2]
+        HW = xc[0, 0].numel()
+        nws = _lib.lib().skp_groupnorm_workspace(B, C, HW, groups)
+        if nws < 0:
+            raise ValueError(f"groupnorm: bad shape {tuple(xc.shape)} groups={groups}")
+        if shift is not None:
+            shift = _c(shift.detach().expand(B, C))
+        part = torch.empty(nws, device=xc.device, dtype=torch.float64)
+        stats = torch.empty(B * groups * 2, device=xc.device, dtype=F32)
+        y = torch.empty_like(xc)
+        g, b = _c(gamma.detach()), _c(beta.detach())
+        call("skp_groupnorm_fwd", ptr(xc), ptr(g), ptr(b), ptr(shift), B, C, HW, int(groups), float(eps), int(act),
+             ptr(y), ptr(stats), ptr(part), stream(xc.device))
+        ctx.save_for_backward(xc, g, b, stats, shift)
+        ctx.meta = (B, C, HW, int(groups), int(act), nws)
+        return y, x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy, dpass):
+        x, g, b, stats, shift = ctx.saved_tensors
+        B, C, HW, G, act, nws = ctx.meta
+        dy = _c(dy)
+        dres = None if dpass is None else _c16(dpass)
+        dx = torch.empty_like(x)
+        part = torch.empty(nws, device=x.device, dtype=torch.float64)
+        call("skp_groupnorm_bwd_add", ptr(x), ptr(dy), ptr(g), ptr(b), ptr(shift), ptr(stats), B, C, HW, G, act,
+             ptr(dres), ptr(dx), ptr(part), stream(x.device))
+        return dx, None, None, None, None, None, None
+
+
+def group_norm_act_res(x, gamma, beta, groups, eps, act):
+    """(act(GroupNorm(x)), x) where the second output is x for the node's other consumer: its
+    gradient is added by the GroupNorm backward kernel (GroupNormActRes)."""
+    _lib.require_device(x)
+    return GroupNormActRes.apply(x, gamma, beta, int(groups), float(eps), bool(act), None)
+
+
 def group_norm_act(x, gamma, beta, groups, eps, act, shift=None):
     """Fused GroupNorm(x + shift) (+SiLU when act) on the HIP device; frozen gamma/beta.
     ``shift``: None or a (B, C) / (1, C) / (C,) per-channel input offset without gradient."""
@@ -948,6 +1126,47 @@ class LayerNormFn(torch.autograd.Function):
         dx = torch.empty_like(x)
         call("skp_layernorm_bwd", ptr(x), ptr(dy), ptr(w), ptr(stats), x.numel() // C, C, ptr(dx), stream(x.device))
         return dx, None, None, None
+
+
+class LayerNormRes(torch.autograd.Function):
+    """LayerNormFn that also hands x on (``x_pass``) to the transformer block's residual add, so the
+    residual's gradient is added inside the backward kernel (skp_layernorm_bwd_add) rather than by
+    a separate autograd accumulation pass (h = attn(norm(h)) + h, diffusers attention.py)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps):
+        xc = _c(x)
+        C = xc.shape[-1]
+        rows = xc.numel() // C
+        y = torch.empty_like(xc)
+        stats = torch.empty(rows, 2, device=xc.device, dtype=F32)
+        w, b = _c(weight.detach()), _c(bias.detach())
+        call("skp_layernorm_fwd", ptr(xc), ptr(w), ptr(b), rows, C, float(eps), ptr(y), ptr(stats), stream(xc.device))
+        ctx.save_for_backward(xc, w, stats)
+        return y, x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy, dpass):
+        x, w, stats = ctx.saved_tensors
+        dy = _c(dy)
+        dres = None if dpass is None else _c16(dpass)
+        C = x.shape[-1]
+        dx = torch.empty_like(x)
+        call("skp_layernorm_bwd_add", ptr(x), ptr(dy), ptr(w), ptr(stats), x.numel() // C, C, ptr(dres), ptr(dx),
+             stream(x.device))
+        return dx, None, None, None
+
+
+def layer_norm_res(x, weight, bias, eps):
+    """(F.layer_norm(x, …), x) with the second output for the residual add: its gradient joins the
+    LayerNorm backward kernel (LayerNormRes).  Shapes the kernel does not take: torch's LayerNorm
+    and x itself."""
+    _lib.require_device(x)
+    C = x.shape[-1]
+    if (x.dtype != F32 or C % 4 or C > 2048 or weight is None or bias is None or weight.requires_grad
+            or bias.requires_grad or x.numel() == 0 or x.numel() // C < LN_MIN_ROWS):
+        return torch.nn.functional.layer_norm(x, (C,), weight, bias, eps), x
+    return LayerNormRes.apply(x, weight, bias, float(eps))
 
 
 # kernel time at batch 8 (tools/ln_time.py): 32768 rows × 320: 15.4 µs = 5.4 TB/s (ATen 40.8);

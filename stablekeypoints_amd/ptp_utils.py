@@ -22,7 +22,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
-from .sd.unet import CaptureComplete, attention_core, kv_projection
+from .sd.unet import CaptureComplete, _shared_context, attention_core, kv_projection
 
 
 # --------------------------------------------------------------------------- A2 controller / store
@@ -167,15 +167,37 @@ def register_attention_control(model, controller, feature_upsample_res=256):
         def forward(x, context=None, mask=None):
             batch_size, sequence_length, dim = x.shape
             h = self.heads
-            q = self.to_q(x)
             is_cross = context is not None
+            capture = (is_cross and sequence_length <= 32 ** 2
+                       and len(controller.step_store["attn"]) < AttentionStore.max_captures)
+            if not capture:
+                # ptp_utils.py:481-506: un-captured layers are the normal attention (the class's own
+                # forward: projections read in place, fused attention)
+                return type(self).forward(self, x, context, mask)
+            q = self.to_q(x)
+            one = _shared_context(context) if (is_cross and mask is None and x.is_cuda) else None
+            if capture and one is not None and ops.heads_eligible(q, one, h):
+                # the capture on the layer's own (B, S, H·d) projection and the ONE projection of the
+                # token embedding the batch shares: no head permutes, no batch-expanded keys / values
+                s = int(sequence_length ** 0.5)
+                if s * s != sequence_length:
+                    raise ValueError(f"capture needs a square token grid, got {sequence_length}")
+                k1, v1 = self.to_k(one), self.to_v(one)
+                sim = ops.capture_logits_heads(q, k1, h, self.scale)      # (B·H, s², N), MFMA
+                if getattr(controller, "stores_logits", False):
+                    controller({"attn": sim, "size": s, "heads": h}, is_cross, place_in_unet)
+                else:
+                    attn = ops.capture_attn(sim, s, feature_upsample_res)  # (B·H, R², N), HIP
+                    controller({"attn": attn}, is_cross, place_in_unet)
+                if getattr(controller, "early_exit", False) and \
+                        len(controller.step_store["attn"]) >= AttentionStore.max_captures:
+                    raise CaptureComplete()   # the UNet output is discarded: skip this layer's output too
+                return to_out(ops.attn_pv_heads(sim.softmax(dim=-1), v1, h))
             context = context if is_cross else x
             k, v = kv_projection(self, context)
             q = self.reshape_heads_to_batch_dim(q)
             k = self.reshape_heads_to_batch_dim(k)
             v = self.reshape_heads_to_batch_dim(v)
-            capture = (is_cross and sequence_length <= 32 ** 2
-                       and len(controller.step_store["attn"]) < AttentionStore.max_captures)
             if capture:
                 s = int(sequence_length ** 0.5)
                 if s * s != sequence_length:

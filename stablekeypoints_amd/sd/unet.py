@@ -64,6 +64,28 @@ def _ln(norm, x):
     return norm(x)
 
 
+# A/B switch: 0 = the residual consumers of a norm's input get their gradient summed by autograd
+NORM_RES = os.environ.get("SKP_NORM_RES", "1") != "0"
+
+
+def _ln_res(norm, x):
+    """(norm(x), x): on the fused path the second output hands x to the residual add, whose
+    gradient the LayerNorm backward kernel then adds in its own pass (ops.layer_norm_res)."""
+    if NORM_RES and USE_SKP_LAYERNORM and _fused(x, norm) and torch.is_grad_enabled() and x.requires_grad:
+        from .. import ops
+        return ops.layer_norm_res(x, norm.weight, norm.bias, norm.eps)
+    return _ln(norm, x), x
+
+
+def gn_act_res(norm, x, act):
+    """(act(norm(x)), x) with the second output for x's other consumer (residual / shortcut): its
+    gradient joins the GroupNorm backward kernel (ops.group_norm_act_res) on the fused path."""
+    if NORM_RES and _fused(x, norm) and torch.is_grad_enabled() and x.requires_grad:
+        from .. import ops
+        return ops.group_norm_act_res(x, norm.weight, norm.bias, norm.num_groups, norm.eps, act)
+    return gn_act(norm, x, act), x
+
+
 def gn_act(norm, x, act, shift=None):
     """act(norm(x + shift)) for an nn.GroupNorm ``norm`` (``shift``: None or a per-(sample,
     channel) offset (B or 1, C)): on the HIP device the fused libskp kernel (frozen affine
@@ -141,8 +163,15 @@ SHARED_HEAD_MAJOR = os.environ.get("SKP_SHARED_HEAD_MAJOR", "1") != "0"
 
 def _shared_context(context):
     """The one (1, L, C) sequence of a context whose batch is a stride-0 expansion (the token
-    embedding every image of a batched pass shares), else None."""
+    embedding every image of a batched pass shares), else None.  When the expansion is a view of
+    that sequence (``ctx.expand(B, -1, -1)``, ptp_utils.find_pred_noise) the sequence itself is
+    returned, so every layer's gradient lands on it directly: slicing the expansion (``[:1]``)
+    makes autograd build a zero-filled (B, L, C) gradient per layer and sum those across layers."""
     if SHARED_KV and context.dim() == 3 and context.shape[0] > 1 and context.stride(0) == 0:
+        base = context._base
+        if (base is not None and base.dim() == 3 and base.shape[0] == 1 and base.shape[1:] == context.shape[1:]
+                and base.stride()[1:] == context.stride()[1:] and base.data_ptr() == context.data_ptr()):
+            return base
         return context[:1]
     return None
 
@@ -167,8 +196,8 @@ def kv_projection(attn, context):
     """to_k(context), to_v(context).  A context whose batch is a stride-0 expansion of one
     sequence (the token embedding shared by every image of a batched pass) is projected once
     and the result expanded: the same values, 1/B of the GEMM work forward and backward."""
-    if SHARED_KV and context.dim() == 3 and context.shape[0] > 1 and context.stride(0) == 0:
-        one = context[:1]
+    one = _shared_context(context)
+    if one is not None:
         B = context.shape[0]
         return attn.to_k(one).expand(B, -1, -1), attn.to_v(one).expand(B, -1, -1)
     return attn.to_k(context), attn.to_v(context)
@@ -231,10 +260,12 @@ class BasicTransformerBlock(nn.Module):
         self.norm3 = nn.LayerNorm(dim)
 
     def forward(self, h, context=None):
-        h = self.attn1(_ln(self.norm1, h)) + h
-        h = self.attn2(_ln(self.norm2, h), context=context) + h
-        h = self.ff(_ln(self.norm3, h)) + h
-        return h
+        y, h = _ln_res(self.norm1, h)
+        h = self.attn1(y) + h
+        y, h = _ln_res(self.norm2, h)
+        h = self.attn2(y, context=context) + h
+        y, h = _ln_res(self.norm3, h)
+        return self.ff(y) + h
 
 
 class Transformer2DModel(nn.Module):
@@ -256,8 +287,7 @@ class Transformer2DModel(nn.Module):
 
     def forward(self, x, encoder_hidden_states=None):
         b, c, hh, ww = x.shape
-        res = x
-        x = gn_act(self.norm, x, False)
+        x, res = gn_act_res(self.norm, x, False)
         if not self.linear_proj and _fused(x, self.proj_in, self.proj_out):
             # 1×1 projections as strided batched GEMMs straight between NCHW and (B, HW, C')
             from .. import ops
@@ -298,7 +328,8 @@ class ResnetBlock2D(nn.Module):
             # the residual add: neither is a separate pass over the activations
             # (3×3 convolutions: Winograd F(4×4, 3×3) where the shape fills the chip, else MIOpen)
             from .. import ops
-            h = ops.conv3x3(gn_act(self.norm1, x, True), self.conv1.weight)
+            y, x = gn_act_res(self.norm1, x, True)   # x goes on to the residual / shortcut
+            h = ops.conv3x3(y, self.conv1.weight)
             shift = self.conv1.bias[None]
             if temb is not None and self.time_emb_proj is not None:
                 shift = shift + self.time_emb_proj(F.silu(temb))
