@@ -242,6 +242,12 @@ int skp_groupnorm_fwd(const float* x, const float* gamma, const float* beta, con
 int skp_groupnorm_bwd(const float* x, const float* dy, const float* gamma, const float* beta, const float* shift,
                       const float* stats, int B, int C, long long HW, int G, int act, float* dx, double* partial,
                       void* stream);
+/* skp_groupnorm_fwd with the statistics pass replaced by the producing convolution's per-segment
+ * sums: part (B, C, nseg) float2 (Σx, Σx²) as skp_conv3x3_wino2_gn writes them (nseg = H/8 · W/32);
+ * the shift is folded into the sums per channel.  Same output and saved (mean, rstd) layout. */
+int skp_groupnorm_fwd_part(const float* x, const float* gamma, const float* beta, const float* shift, const float* part,
+                           int nseg, int B, int C, long long HW, int G, float eps, int act, float* y, float* stats,
+                           double* partial, void* stream);
 /* skp_groupnorm_bwd plus dres (may be null): dx = GroupNorm-backward(dy) + dres, the gradient of x's
  * other consumer (the ResNet block's residual or shortcut, the spatial transformer's residual) added
  * in the same pass instead of by the autograd engine (diffusers resnet.py / attention.py residuals). */
@@ -342,6 +348,13 @@ int skp_conv3x3_wino(const float* x, const float* U, const float* bias, const fl
 int skp_wino2_weights(const float* w, int K, int C, int flip, float* U, void* stream);
 int skp_conv3x3_wino2(const float* x, const float* U, const float* bias, const float* residual, float* y, int B,
                       int C, int K, int H, int W, int nsplit, float* ws, void* stream);
+/* skp_conv3x3_wino2 that also writes the next GroupNorm's statistics from its epilogue: gn_part
+ * (B, K, H/8 · W/32) float2 = (Σy, Σy²) of the final output (bias and residual included) per channel
+ * over each 8-row × 32-pixel segment (nsplit = 1, H and W multiples of 32; may be null).  The
+ * consumer is skp_groupnorm_fwd_part: the frozen UNet / VAE's GroupNorm(+SiLU) after a 3×3 convolution
+ * (diffusers resnet.py) then reads its input once instead of twice. */
+int skp_conv3x3_wino2_gn(const float* x, const float* U, const float* bias, const float* residual, float* y, int B,
+                         int C, int K, int H, int W, int nsplit, float* ws, float* gn_part, void* stream);
 /* diffusers' Downsample2D(padding=0) of the VAE encoder (F.pad(x, (0, 1, 0, 1)) then a 3×3 stride-2
  * convolution; the encoder behind ptp_utils.image2latent, reference ptp_utils.py:289-304):
  * y (B, K, H/2, W/2) = the stride-1 pad-1 convolution of x sampled at (2oy + 1, 2ox + 1), + bias,

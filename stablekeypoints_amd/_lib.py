@@ -81,6 +81,9 @@ _SIGS = {
     "skp_conv3x3_wino": [_p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _p, _p],
     "skp_wino2_weights": [_p, _c_int, _c_int, _c_int, _p, _p],
     "skp_conv3x3_wino2": [_p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _p, _p],
+    "skp_conv3x3_wino2_gn": [_p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _p, _p, _p],
+    "skp_groupnorm_fwd_part": [_p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_ll, _c_int, _c_float, _c_int, _p, _p, _p,
+                               _p],
     "skp_conv3x3s2_wino2": [_p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _p, _p],
     "skp_version": [],
 }

@@ -730,7 +730,8 @@ template <int EPI, int HH, int TXB, int NW>
 __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __restrict__ x, const float* __restrict__ U,
                                            const float* __restrict__ bias, const float* __restrict__ res,
                                            float* __restrict__ y, int C, int K, int H, int W, int img, int x0,
-                                           int y0, int kb, int c0, int csplit, int wv, int dbg) {
+                                           int y0, int kb, int c0, int csplit, int wv, int dbg,
+                                           float2* __restrict__ gnp) {
   using Geo = w2::GeoT<TXB, NW>;
   constexpr int kChF = Geo::CHF, kRowF = Geo::RF, kRawInstr = Geo::RAW_INSTR, NI = Geo::NI, RR = Geo::RR,
                 RC = Geo::RC;
@@ -993,6 +994,19 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
       }
       if (dbg & 128) __builtin_nontemporal_store(f32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<f32x4*>(y + o));
       else if (!(dbg & 64)) *reinterpret_cast<float4*>(y + o) = v;
+      if (TXB == 8 && gnp) {
+        // the next GroupNorm's statistics: the wave's 1 KB is 8 rows × 32 pixels of channel k, one
+        // "segment" of the (H/8) × (W/32) segment grid; (Σv, Σv²) of it in fp32, wave-reduced
+        float s1 = (v.x + v.y) + (v.z + v.w);
+        float s2 = (v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w);
+        s1 = wave_sum(s1);
+        s2 = wave_sum(s2);
+        if ((tid & 63) == 0) {
+          const int row0 = q >> 3;   // lane 0's row in the block: the segment's first row
+          const int seg = ((y0 + row0) >> 3) * (W >> 5) + (x0 >> 5);
+          gnp[((size_t)img * K + k) * (size_t)((H >> 3) * (W >> 5)) + seg] = make_float2(s1, s2);
+        }
+      }
     }
     if (blk == 0) __syncthreads();
   }
@@ -1002,7 +1016,7 @@ template <int EPI, int TXB, int NW = 8>
 __global__ __launch_bounds__(NW * WAVE) __attribute__((amdgpu_waves_per_eu(2, 2))) void wino2_kernel(
     const float* __restrict__ x, const float* __restrict__ U, const float* __restrict__ bias,
     const float* __restrict__ res, float* __restrict__ y, int nimg, int C, int K, int H, int W, int bw, int bpi,
-    int nblk, int nkb, int kb_major, int csplit, int dbg) {
+    int nblk, int nkb, int kb_major, int csplit, int dbg, float2* __restrict__ gnp) {
   // separate LDS objects per ring slot: the compiler tells a DMA into one slot from a ds_read of
   // another and does not wait for outstanding DMAs before every LDS read
   __shared__ __attribute__((aligned(16))) float R0[w2::GeoT<TXB, NW>::RAWF], R1[w2::GeoT<TXB, NW>::RAWF],
@@ -1039,8 +1053,9 @@ __global__ __launch_bounds__(NW * WAVE) __attribute__((amdgpu_waves_per_eu(2, 2)
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const W2Smem sm{R0, R1, R2, R3, U0, U1, U2};
   const int c0 = sp * csplit;
-  if (wv < NW / 2) wino2_body<EPI, 0, TXB, NW>(sm, x, U, bias, res, y, C, K, H, W, img, x0, y0, kb, c0, csplit, wv, dbg);
-  else wino2_body<EPI, 1, TXB, NW>(sm, x, U, bias, res, y, C, K, H, W, img, x0, y0, kb, c0, csplit, wv, dbg);
+  if (wv < NW / 2)
+    wino2_body<EPI, 0, TXB, NW>(sm, x, U, bias, res, y, C, K, H, W, img, x0, y0, kb, c0, csplit, wv, dbg, gnp);
+  else wino2_body<EPI, 1, TXB, NW>(sm, x, U, bias, res, y, C, K, H, W, img, x0, y0, kb, c0, csplit, wv, dbg, gnp);
 }
 
 // U2[kb][c][k%32][40]: positions 0..17 at 0..17, 18..35 at 20..37, the rest zero
@@ -1128,24 +1143,27 @@ extern "C" int skp_conv3x3s2_wino2(const float* x, const float* U, const float* 
   const int fl = dbg | wino_nt_flag((long long)B * K * (H / 2) * (W / 2) * 4, nsplit);
   if (half && nsplit == 1 && bias)
     hipLaunchKernelGGL((wino2_kernel<5, 8, 4>), grid, dim3(4 * WAVE), 0, st, x, U, bias, nullptr, out, B, C, K, H, W,
-                       bw, bpi, (int)nblk, nkb, 0, C / nsplit, fl);
+                       bw, bpi, (int)nblk, nkb, 0, C / nsplit, fl, nullptr);
   else if (half)
     hipLaunchKernelGGL((wino2_kernel<4, 8, 4>), grid, dim3(4 * WAVE), 0, st, x, U, nullptr, nullptr, out, B, C, K, H,
-                       W, bw, bpi, (int)nblk, nkb, 0, C / nsplit, fl);
+                       W, bw, bpi, (int)nblk, nkb, 0, C / nsplit, fl, nullptr);
   else if (nsplit == 1 && bias)
     hipLaunchKernelGGL((wino2_kernel<5, 8>), grid, dim3(w2::kThreads), 0, st, x, U, bias, nullptr, out, B, C, K, H, W,
-                       bw, bpi, (int)nblk, nkb, 0, C / nsplit, fl);
+                       bw, bpi, (int)nblk, nkb, 0, C / nsplit, fl, nullptr);
   else
     hipLaunchKernelGGL((wino2_kernel<4, 8>), grid, dim3(w2::kThreads), 0, st, x, U, nullptr, nullptr, out, B, C, K, H,
-                       W, bw, bpi, (int)nblk, nkb, 0, C / nsplit, fl);
+                       W, bw, bpi, (int)nblk, nkb, 0, C / nsplit, fl, nullptr);
   SKP_LAUNCH_CHECK();
   if (nsplit > 1) return splitk_reduce(ws, nsplit, B, K, (H / 2) * (W / 2), bias, nullptr, y, st);
   return SKP_OK;
 }
 
-extern "C" int skp_conv3x3_wino2(const float* x, const float* U, const float* bias, const float* residual, float* y,
-                                 int B, int C, int K, int H, int W, int nsplit, float* ws, void* stream) {
+extern "C" int skp_conv3x3_wino2_gn(const float* x, const float* U, const float* bias, const float* residual, float* y,
+                                    int B, int C, int K, int H, int W, int nsplit, float* ws, float* gn_part,
+                                    void* stream) {
   SKP_CHECK_ARG(x && U && y, "null pointer");
+  SKP_CHECK_ARG(!gn_part || (nsplit == 1 && H % 32 == 0 && W % 32 == 0 && (reinterpret_cast<uintptr_t>(gn_part) & 7) == 0),
+                "gn_part: one split, H and W multiples of 32, 8-byte aligned");
   SKP_CHECK_ARG(B > 0 && C > 0 && K > 0 && H > 0 && W > 0, "non-positive shape");
   SKP_CHECK_ARG(C % w2::kCK == 0, "input channels must be a multiple of 4");
   SKP_CHECK_ARG(K % w2::kNC == 0, "output channels must be a multiple of 32");
@@ -1184,19 +1202,20 @@ extern "C" int skp_conv3x3_wino2(const float* x, const float* U, const float* bi
   hipStream_t st = as_stream(stream);
   const dim3 grid((unsigned)(nblk * nkb * nsplit));
   const int fl = dbg | wino_nt_flag((long long)B * K * H * W * 4, nsplit);
+  float2* gnp = reinterpret_cast<float2*>(gn_part);
 #define SKP_WG2(E)                                                                                            \
   if (half16)                                                                                                 \
     hipLaunchKernelGGL((wino2_kernel<E, 4, 4>), grid, dim3(4 * WAVE), 0, st, x, U, bias, residual, out, B, C, K,  \
-                       H, W, bw, bpi, (int)nblk, nkb, kb_major, C / nsplit, fl);                              \
+                       H, W, bw, bpi, (int)nblk, nkb, kb_major, C / nsplit, fl, nullptr);                              \
   else if (g16)                                                                                               \
     hipLaunchKernelGGL((wino2_kernel<E, 4>), grid, dim3(w2::kThreads), 0, st, x, U, bias, residual, out, B, C, K, \
-                       H, W, bw, bpi, (int)nblk, nkb, kb_major, C / nsplit, fl);                              \
+                       H, W, bw, bpi, (int)nblk, nkb, kb_major, C / nsplit, fl, nullptr);                              \
   else if (half)                                                                                              \
     hipLaunchKernelGGL((wino2_kernel<E, 8, 4>), grid, dim3(4 * WAVE), 0, st, x, U, bias, residual, out, B, C, K,  \
-                       H, W, bw, bpi, (int)nblk, nkb, kb_major, C / nsplit, fl);                              \
+                       H, W, bw, bpi, (int)nblk, nkb, kb_major, C / nsplit, fl, gnp);                              \
   else                                                                                                        \
     hipLaunchKernelGGL((wino2_kernel<E, 8>), grid, dim3(w2::kThreads), 0, st, x, U, bias, residual, out, B, C, K, \
-                       H, W, bw, bpi, (int)nblk, nkb, kb_major, C / nsplit, fl)
+                       H, W, bw, bpi, (int)nblk, nkb, kb_major, C / nsplit, fl, gnp)
   switch (epi) {
     case 0: SKP_WG2(0); break;
     case 1: SKP_WG2(1); break;
@@ -1207,4 +1226,9 @@ extern "C" int skp_conv3x3_wino2(const float* x, const float* U, const float* bi
   SKP_LAUNCH_CHECK();
   if (nsplit > 1) return splitk_reduce(ws, nsplit, B, K, H * W, bias, residual, y, st);
   return SKP_OK;
+}
+
+extern "C" int skp_conv3x3_wino2(const float* x, const float* U, const float* bias, const float* residual, float* y,
+                                 int B, int C, int K, int H, int W, int nsplit, float* ws, void* stream) {
+  return skp_conv3x3_wino2_gn(x, U, bias, residual, y, B, C, K, H, W, nsplit, ws, nullptr, stream);
 }

@@ -900,6 +900,43 @@ def equivariance_loss_batch(A, At, theta_inv, nb):
 
 
 # --------------------------------------------------------------------------- UNet-side GroupNorm(+SiLU)
+# A/B switch (SKP_GN_EPI=0 off): the Winograd convolution's epilogue writes per-segment (Σ, Σ²) of
+# its output (skp_conv3x3_wino2_gn) and a GroupNorm reading that output takes its statistics from
+# them (skp_groupnorm_fwd_part) instead of a pass over the activation.
+GN_EPI = os.environ.get("SKP_GN_EPI", "1") != "0"
+
+
+def _gn_parts_of(x):
+    """The (Σ, Σ²) segment partials the producing convolution left on ``x`` (None: none, or x was
+    modified in place since)."""
+    ent = getattr(x, "_skp_gn", None)
+    if ent is None or ent[0] != x._version:
+        return None
+    return ent[1], ent[2]
+
+
+def _gn_fwd(x, gamma, beta, shift, groups, eps, act):
+    """act(GroupNorm(x + shift)) forward: (y, stats, g, b, nws) — skp_groupnorm_fwd, or
+    skp_groupnorm_fwd_part when x carries its producer's statistics partials."""
+    B, C = x.shape[:2]
+    HW = x[0, 0].numel()
+    nws = _lib.lib().skp_groupnorm_workspace(B, C, HW, groups)
+    if nws < 0:
+        raise ValueError(f"groupnorm: bad shape {tuple(x.shape)} groups={groups}")
+    part = torch.empty(nws, device=x.device, dtype=torch.float64)
+    stats = torch.empty(B * groups * 2, device=x.device, dtype=F32)
+    y = torch.empty_like(x)
+    g, b = _c(gamma.detach()), _c(beta.detach())
+    pre = _gn_parts_of(x) if GN_EPI else None
+    if pre is not None:
+        call("skp_groupnorm_fwd_part", ptr(x), ptr(g), ptr(b), ptr(shift), ptr(pre[0]), pre[1], B, C, HW,
+             int(groups), float(eps), int(act), ptr(y), ptr(stats), ptr(part), stream(x.device))
+    else:
+        call("skp_groupnorm_fwd", ptr(x), ptr(g), ptr(b), ptr(shift), B, C, HW, int(groups), float(eps), int(act),
+             ptr(y), ptr(stats), ptr(part), stream(x.device))
+    return y, stats, g, b, nws
+
+
 class GroupNormAct(torch.autograd.Function):
     """y = act(GroupNorm(x + shift)) with frozen affine parameters (dx only) — skp_groupnorm_fwd/bwd.
     ``shift`` (B, C) or None: a per-(sample, channel) input offset (conv bias + time embedding)."""
@@ -909,17 +946,9 @@ class GroupNormAct(torch.autograd.Function):
         x = _c(x)
         B, C = x.shape[:2]
         HW = x[0, 0].numel()
-        nws = _lib.lib().skp_groupnorm_workspace(B, C, HW, groups)
-        if nws < 0:
-            raise ValueError(f"groupnorm: bad shape {tuple(x.shape)} groups={groups}")
         if shift is not None:
             shift = _c(shift.detach().expand(B, C))
-        part = torch.empty(nws, device=x.device, dtype=torch.float64)
-        stats = torch.empty(B * groups * 2, device=x.device, dtype=F32)
-        y = torch.empty_like(x)
-        g, b = _c(gamma.detach()), _c(beta.detach())
-        call("skp_groupnorm_fwd", ptr(x), ptr(g), ptr(b), ptr(shift), B, C, HW, int(groups), float(eps), int(act),
-             ptr(y), ptr(stats), ptr(part), stream(x.device))
+        y, stats, g, b, nws = _gn_fwd(x, gamma, beta, shift, groups, eps, act)
         ctx.save_for_backward(x, g, b, stats, shift)
         ctx.meta = (B, C, HW, int(groups), int(act), nws)
         return y
@@ -947,17 +976,9 @@ class GroupNormActRes(torch.autograd.Function):
         xc = _c(x)
         B, C = xc.shape[:2]
         HW = xc[0, 0].numel()
-        nws = _lib.lib().skp_groupnorm_workspace(B, C, HW, groups)
-        if nws < 0:
-            raise ValueError(f"groupnorm: bad shape {tuple(xc.shape)} groups={groups}")
         if shift is not None:
             shift = _c(shift.detach().expand(B, C))
-        part = torch.empty(nws, device=xc.device, dtype=torch.float64)
-        stats = torch.empty(B * groups * 2, device=xc.device, dtype=F32)
-        y = torch.empty_like(xc)
-        g, b = _c(gamma.detach()), _c(beta.detach())
-        call("skp_groupnorm_fwd", ptr(xc), ptr(g), ptr(b), ptr(shift), B, C, HW, int(groups), float(eps), int(act),
-             ptr(y), ptr(stats), ptr(part), stream(xc.device))
+        y, stats, g, b, nws = _gn_fwd(xc, gamma, beta, shift, groups, eps, act)
         ctx.save_for_backward(xc, g, b, stats, shift)
         ctx.meta = (B, C, HW, int(groups), int(act), nws)
         return y, x.view_as(x)
@@ -1567,7 +1588,9 @@ def _wino_gemm_conv(x, weight, flip, bias, residual, K):
     return y
 
 
-def _wino_conv(x, weight, flip, bias, residual, K):
+def _wino_conv(x, weight, flip, bias, residual, K, gn=False):
+    """``gn``: also leave the output's GroupNorm statistics partials on it (``y._skp_gn``) where the
+    kernel can write them (skp_conv3x3_wino2_gn: one split, H and W multiples of 32)."""
     B, C, H, W = x.shape
     if _wino_gemm_ok(B, C, K, H, W):
         return _wino_gemm_conv(x, weight, flip, bias, residual, K)
@@ -1575,22 +1598,34 @@ def _wino_conv(x, weight, flip, bias, residual, K):
     # the kernels address x through 32-bit buffer offsets: batches above 2 GiB run in chunks
     per_img = C * H * W * 4
     bmax = max(1, (2 ** 31 - 1) // per_img)
+    gnp = None
+    if gn and GN_EPI and H % 32 == 0 and W % 32 == 0 and all(
+            _wino_plan(min(B, b0 + bmax) - b0, C, K, H, W)[:2] == (True, 1) for b0 in range(0, B, bmax)):
+        nseg = (H // 8) * (W // 32)
+        gnp = torch.empty(B, K, nseg, 2, device=x.device, dtype=F32)
     for b0 in range(0, B, bmax):
         b1 = min(B, b0 + bmax)
-        _wino_launch(x[b0:b1], weight, flip, bias, None if residual is None else residual[b0:b1], y[b0:b1], K)
+        _wino_launch(x[b0:b1], weight, flip, bias, None if residual is None else residual[b0:b1], y[b0:b1], K,
+                     None if gnp is None else gnp[b0:b1])
+    if gnp is not None:
+        y._skp_gn = (y._version, gnp, gnp.shape[2])
     return y
 
 
-def _wino_launch(x, weight, flip, bias, residual, y, K):
+def _wino_launch(x, weight, flip, bias, residual, y, K, gnp=None):
     B, C, H, W = x.shape
     v2, nsplit, _ = _wino_plan(B, C, K, H, W)
     U = _wino_u(weight, flip, v2)
     ws = torch.empty(nsplit, B, K, H, W, device=x.device, dtype=F32) if nsplit > 1 else None
     name = "skp_conv3x3_wino2" if v2 else "skp_conv3x3_wino"
+    args = (ptr(x), ptr(U), ptr(bias) if bias is not None else None,
+            ptr(residual) if residual is not None else None, ptr(y), B, C, K, H, W, nsplit,
+            ptr(ws) if ws is not None else None)
     with _timed(name, 0):
-        call(name, ptr(x), ptr(U), ptr(bias) if bias is not None else None,
-             ptr(residual) if residual is not None else None, ptr(y), B, C, K, H, W, nsplit,
-             ptr(ws) if ws is not None else None, stream(x.device))
+        if gnp is not None:
+            call("skp_conv3x3_wino2_gn", *args, ptr(gnp), stream(x.device))
+        else:
+            call(name, *args, stream(x.device))
 
 
 class Conv3x3(torch.autograd.Function):
@@ -1603,7 +1638,7 @@ class Conv3x3(torch.autograd.Function):
         x = _c(x)
         K = weight.shape[0]
         y = _wino_conv(x, weight, False, None if bias is None else _c(bias.detach()),
-                       None if residual is None else _c(residual), K)
+                       None if residual is None else _c(residual), K, gn=True)
         ctx.weight = weight
         ctx.xshape = x.shape
         ctx.has_res = residual is not None
