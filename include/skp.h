@@ -208,6 +208,13 @@ int skp_equiv_bwd_batch(const float* A, const float* At, int nb, int T, int h, i
 int skp_wino_in_transform(const float* x, int B, int C, int H, int W, float* V, void* stream);
 int skp_wino_out_transform(const float* M, int B, int K, int H, int W, const float* bias, const float* residual,
                            float* y, void* stream);
+/* skp_wino_out_transform with the GEMM product laid out M[p][k][t] (the operands swapped: M[p] =
+ * U[p]ᵀ · V[p]), so the tiles leave as coalesced image-row runs; gn_part (optional): the next
+ * GroupNorm's (Σ, Σ²) per (image, channel, segment of min(P, 64) tiles), P = (H/4)·(W/4) tiles per
+ * plane (16, 32 or a multiple of 64), nseg = P / min(P, 64) — the layout skp_groupnorm_fwd_part
+ * reads. */
+int skp_wino_out_transform_kt(const float* M, int B, int K, int H, int W, const float* bias, const float* residual,
+                              float* y, float* gn_part, void* stream);
 
 /* ---------------------------------------------------------------- Q·Kᵀ (fp32 MFMA)
  * C[b,m,n] = alpha · Σ_k A[b,m,k] · B[b,k,n] (+ C if accumulate), arbitrary element
@@ -243,7 +250,7 @@ int skp_groupnorm_bwd(const float* x, const float* dy, const float* gamma, const
                       const float* stats, int B, int C, long long HW, int G, int act, float* dx, double* partial,
                       void* stream);
 /* skp_groupnorm_fwd with the statistics pass replaced by the producing convolution's per-segment
- * sums: part (B, C, nseg) float2 (Σx, Σx²) as skp_conv3x3_wino2_gn writes them (nseg = H/8 · W/32);
+ * sums: part (B, C, nseg) float2 (Σx, Σx²) as skp_conv3x3_wino2_gn writes them (nseg = H/16 · W/32);
  * the shift is folded into the sums per channel.  Same output and saved (mean, rstd) layout. */
 int skp_groupnorm_fwd_part(const float* x, const float* gamma, const float* beta, const float* shift, const float* part,
                            int nseg, int B, int C, long long HW, int G, float eps, int act, float* y, float* stats,
@@ -349,8 +356,8 @@ int skp_wino2_weights(const float* w, int K, int C, int flip, float* U, void* st
 int skp_conv3x3_wino2(const float* x, const float* U, const float* bias, const float* residual, float* y, int B,
                       int C, int K, int H, int W, int nsplit, float* ws, void* stream);
 /* skp_conv3x3_wino2 that also writes the next GroupNorm's statistics from its epilogue: gn_part
- * (B, K, H/8 · W/32) float2 = (Σy, Σy²) of the final output (bias and residual included) per channel
- * over each 8-row × 32-pixel segment (nsplit = 1, H and W multiples of 32; may be null).  The
+ * (B, K, H/16 · W/32) float2 = (Σy, Σy²) of the final output (bias and residual included) per channel
+ * over each 16-row × 32-pixel segment (nsplit = 1, H and W multiples of 32; may be null).  The
  * consumer is skp_groupnorm_fwd_part: the frozen UNet / VAE's GroupNorm(+SiLU) after a 3×3 convolution
  * (diffusers resnet.py) then reads its input once instead of twice. */
 int skp_conv3x3_wino2_gn(const float* x, const float* U, const float* bias, const float* residual, float* y, int B,

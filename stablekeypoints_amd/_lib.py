@@ -44,6 +44,7 @@ _SIGS = {
     "skp_sharpen_bwd": [_p, _c_int, _c_int, _c_int, _c_float, _c_int, _p, _p, _p, _p],
     "skp_wino_in_transform": [_p, _c_int, _c_int, _c_int, _c_int, _p, _p],
     "skp_wino_out_transform": [_p, _c_int, _c_int, _c_int, _c_int, _p, _p, _p, _p],
+    "skp_wino_out_transform_kt": [_p, _c_int, _c_int, _c_int, _c_int, _p, _p, _p, _p, _p],
     "skp_sharpen_fwd_batch": [_p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_int, _p, _p, _p, _p],
     "skp_sharpen_bwd_batch": [_p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_int, _p, _p, _p, _p],
     "skp_affine_warp": [_p, _c_int, _c_int, _c_int, _c_int, _p, _p, _p],

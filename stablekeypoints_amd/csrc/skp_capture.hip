@@ -716,28 +716,41 @@ void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nc
         float m = kPadLogit;
   #pragma unroll
         for (int c = 0; c < QPL; ++c) {
+#ifdef SKP_MAPS_PROBE_LDS2   // timing probe only (wrong maps): half the tap reads
+          const f4 a0 = V4[ti.x + 16 * c], a1 = V4[ti.y + 16 * c];
+          const f4 a2 = a1 * 0.5f, a3 = a0 * 0.25f;
+#else
           const f4 a0 = V4[ti.x + 16 * c], a1 = V4[ti.y + 16 * c];
           const f4 a2 = V4[ti.z + 16 * c], a3 = V4[ti.w + 16 * c];
+#endif
           // token pairs on the packed f32 VALU: z = ((w0·a0 + w1·a1) + w2·a2) + w3·a3
           f4 v = a0 * w.x;
           v = __builtin_elementwise_fma(a1, (f4)w.y, v);
           v = __builtin_elementwise_fma(a2, (f4)w.z, v);
           v = __builtin_elementwise_fma(a3, (f4)w.w, v);
           zc[c] = v;
+#ifndef SKP_MAPS_PROBE_NOMAX   // timing probe only: no max
           m = __builtin_fmaxf(__builtin_fmaxf(m, v.x), v.y);
           m = __builtin_fmaxf(__builtin_fmaxf(m, v.z), v.w);
+#endif
           if (QPL > 4 || (c & 1)) __builtin_amdgcn_sched_barrier(0);   // bound the LDS reads in flight (registers)
         }
+#ifdef SKP_MAPS_PROBE_NOMAX
+        m = 0.0f;
+#else
         m = row16_max(m);
+#endif
         const f4 mb = (f4)(-m * L2E);
         f4 sv = (f4)0.0f;
   #pragma unroll
         for (int c = 0; c < QPL; ++c) {
           f4 t = __builtin_elementwise_fma(zc[c], (f4)L2E, mb);
+#ifndef SKP_MAPS_PROBE_NOEXP   // timing probe only: no exp
           t.x = __builtin_amdgcn_exp2f(t.x);
           t.y = __builtin_amdgcn_exp2f(t.y);
           t.z = __builtin_amdgcn_exp2f(t.z);
           t.w = __builtin_amdgcn_exp2f(t.w);
+#endif
           zc[c] = t;
           sv += t;
         }

@@ -148,18 +148,34 @@ __global__ __launch_bounds__(256) void sel_dot_kernel(SelSmall t, const float* _
 // take consecutive rows of the tile, so one wave reads 32 different banks), then
 // es[i][j] = Σ_y A[i][y]·Hs[y][j].  Fixed summation order (x, then y ascending).
 constexpr int SEL_ADJ_TILE = 32;
+constexpr int SEL_ADJ_PF = 8;   // float4 of the next tile each thread holds in registers
+// rows per E tile: 32, fewer where R > 256 so a tile fits the register prefetch (256 threads)
+inline int sel_adj_tile(int R) { return std::min(SEL_ADJ_TILE, std::max(1, SEL_ADJ_PF * 256 * 4 / R)); }
 __global__ __launch_bounds__(256) void sel_adj_kernel(SelSmall t, const float* __restrict__ E, int BHK, int smax,
-                                                      int R, float* __restrict__ es) {
+                                                      int R, int TR, float* __restrict__ es) {
   extern __shared__ float sh[];
   const int RP = R + 1;
   const int l = blockIdx.x / BHK;
   const int S = t.s[l];
   float* A = sh;                 // S × (R + 1)
   float* Hs = A + S * RP;        // R × S
-  float* Et = Hs + R * S;        // SEL_ADJ_TILE × (R + 1)
+  float* Et = Hs + R * S;        // TR × (R + 1)
   const size_t bk = blockIdx.x - (size_t)l * BHK;  // bh·K + k
   const float* Eb = E + ((size_t)l * BHK + bk) * (size_t)R * R;
   es += (size_t)l * BHK * smax * smax;
+  // the next tile of E in flight in registers while the current one is reduced (the map is read
+  // exactly once, 16 B per lane, coalesced)
+  float4 pf[SEL_ADJ_PF];
+  auto fetch = [&](int y0) {
+    const int n4 = min(TR, R - y0) * R / 4;
+    const float4* src = reinterpret_cast<const float4*>(Eb + (size_t)y0 * R);
+#pragma unroll
+    for (int m = 0; m < SEL_ADJ_PF; ++m) {
+      const int e = m * 256 + (int)threadIdx.x;
+      if (e < n4) pf[m] = src[e];
+    }
+  };
+  fetch(0);
   for (int e = threadIdx.x; e < S * RP; e += blockDim.x) A[e] = 0.0f;
   __syncthreads();
   for (int x = threadIdx.x; x < R; x += blockDim.x) {
@@ -167,15 +183,18 @@ __global__ __launch_bounds__(256) void sel_adj_kernel(SelSmall t, const float* _
 #pragma unroll
     for (int m = 0; m < 4; ++m) A[t.i[m] * RP + x] += t.w[m];
   }
-  for (int y0 = 0; y0 < R; y0 += SEL_ADJ_TILE) {
-    const int ny = min(SEL_ADJ_TILE, R - y0);
-    const float4* src = reinterpret_cast<const float4*>(Eb + (size_t)y0 * R);
-    for (int e = threadIdx.x; e < ny * R / 4; e += blockDim.x) {
-      const float4 v = src[e];
-      const int yy = (4 * e) / R, x = 4 * e - yy * R;
-      float* d = Et + yy * RP + x;
-      d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+  for (int y0 = 0; y0 < R; y0 += TR) {
+    const int ny = min(TR, R - y0);
+#pragma unroll
+    for (int m = 0; m < SEL_ADJ_PF; ++m) {
+      const int e = m * 256 + (int)threadIdx.x;
+      if (e < ny * R / 4) {
+        const int yy = (4 * e) / R, x = 4 * e - yy * R;
+        float* d = Et + yy * RP + x;
+        d[0] = pf[m].x; d[1] = pf[m].y; d[2] = pf[m].z; d[3] = pf[m].w;
+      }
     }
+    if (y0 + TR < R) fetch(y0 + TR);
     __syncthreads();   // (the first pass also publishes A)
     for (int e = threadIdx.x; e < ny * S; e += blockDim.x) {
       const int yy = e % ny, j = e / ny;   // lanes over rows: distinct banks
@@ -579,6 +598,7 @@ extern "C" int skp_capture_maps_bwd_sel(const float* const* z_low, const int* si
   SKP_CHECK_ARG(z_low && sizes && sel_tok && gsel && stats && dz_low && workspace, "null pointer");
   SKP_CHECK_ARG(L > 0 && L <= SKP_MAX_LAYERS, "L out of range");
   SKP_CHECK_ARG(B > 0 && H > 0 && N > 0 && R > 0, "non-positive shape");
+  SKP_CHECK_ARG(R % 4 == 0, "R must be a multiple of 4");
   SKP_CHECK_ARG(K > 0 && K <= SEL_MAXK, "K must be in [1, 32]");
   SKP_CHECK_ARG(N % 4 == 0 && N <= 1024, "N must be a multiple of 4, at most 1024");
   SKP_CHECK_ARG((long long)B * H <= 65535 && (long long)B * H * R * R < (1LL << 31), "shape too large");
@@ -623,9 +643,10 @@ extern "C" int skp_capture_maps_bwd_sel(const float* const* z_low, const int* si
   hipLaunchKernelGGL(sel_dot_kernel, dim3((unsigned)(L * BH * R)), dim3(std::min(R, 256)),
                      (size_t)smax * K * sizeof(float), st, t, zsel, BH, R, H, K, sel_tok, gsel, gscale, E, pix);
   SKP_LAUNCH_CHECK();
+  const int tr = sel_adj_tile(R);
   hipLaunchKernelGGL(sel_adj_kernel, dim3((unsigned)(L * BH * K)), dim3(256),
-                     (size_t)(smax * (R + 1) + R * smax + SEL_ADJ_TILE * (R + 1)) * sizeof(float), st, t, E, BH * K,
-                     smax, R, es);
+                     (size_t)(smax * (R + 1) + R * smax + tr * (R + 1)) * sizeof(float), st, t, E, BH * K, smax, R, tr,
+                     es);
   SKP_LAUNCH_CHECK();
   // the dense part: layers of equal s share a class (up to 4 per launch); two classes that have
   // a paired kernel (SD-1.5: s = 16 and 32 at R = 128) run as one launch

@@ -90,36 +90,27 @@ __global__ __launch_bounds__(kThreads) void gn_stats_kernel(const float* __restr
 }
 
 // Statistics from the producing convolution's epilogue (skp_conv3x3_wino2_gn): part[b][c][seg] =
-// (Σx, Σx²) over pixel segment seg of channel c.  One block per (sample, group): per channel the
-// segments in order (fp64), the channel's shift folded in (Σ(x+t) = Σx + n·t, Σ(x+t)² = Σx² + 2tΣx +
-// n·t²), the channels in order; the group totals go to chunk 0 of the layout gn_apply_kernel reads
-// (the other chunks zero), so the apply pass is the one skp_groupnorm_fwd uses.
+// (Σx, Σx²) over pixel segment seg (HW / nseg pixels) of channel c.  One block per (sample, group),
+// one pass over the group's cpg·nseg segments in fp64 with the channel's shift folded in per
+// segment (Σ(x+t) = Σx + n·t, Σ(x+t)² = Σx² + 2tΣx + n·t², n = the segment's pixels) and one block
+// reduction; the group totals go to chunk 0 of the layout gn_apply_kernel reads (the other chunks
+// zero), so the apply pass is the one skp_groupnorm_fwd uses.
 __global__ __launch_bounds__(kThreads) void gn_part_combine_kernel(const float2* __restrict__ part, int nseg,
                                                                    const float* __restrict__ shift, GNShape sh,
                                                                    double* __restrict__ partial) {
   __shared__ double sd[2 * kThreads / 64];
   const int grp = blockIdx.x;   // b·G + g
   const int b = grp / sh.G, g = grp - b * sh.G;
+  const float2* pg = part + ((size_t)b * sh.C + (size_t)g * sh.cpg) * nseg;
+  const double n = (double)(sh.HW / nseg);
   double s1 = 0.0, s2 = 0.0;
-  for (int cc = 0; cc < sh.cpg; ++cc) {
-    const int c = g * sh.cpg + cc;
-    const float2* pc = part + ((size_t)b * sh.C + c) * nseg;
-    double a1 = 0.0, a2 = 0.0;
-    for (int e = threadIdx.x; e < nseg; e += kThreads) {
-      const float2 v = pc[e];
-      a1 += (double)v.x;
-      a2 += (double)v.y;
-    }
-    block_sum2(a1, a2, sd);
-    if (shift) {
-      const double t = (double)shift[(size_t)b * sh.C + c], n = (double)sh.HW;
-      a2 += 2.0 * t * a1 + n * t * t;
-      a1 += n * t;
-    }
-    s1 += a1;
-    s2 += a2;
-    __syncthreads();   // block_sum2's result slots are the next channel's wave slots
+  for (int e = threadIdx.x; e < sh.cpg * nseg; e += kThreads) {
+    const float2 v = pg[e];
+    const double t = shift ? (double)shift[(size_t)b * sh.C + g * sh.cpg + e / nseg] : 0.0;
+    s1 += (double)v.x + n * t;
+    s2 += (double)v.y + t * (2.0 * (double)v.x + n * t);
   }
+  block_sum2(s1, s2, sd);
   if (threadIdx.x < sh.nsplit) {
     partial[2 * ((size_t)grp * sh.nsplit + threadIdx.x)] = threadIdx.x == 0 ? s1 : 0.0;
     partial[2 * ((size_t)grp * sh.nsplit + threadIdx.x) + 1] = threadIdx.x == 0 ? s2 : 0.0;
@@ -361,7 +352,7 @@ extern "C" int skp_groupnorm_fwd_part(const float* x, const float* gamma, const 
                                       const float* part, int nseg, int B, int C, long long HW, int G, float eps,
                                       int act, float* y, float* stats, double* partial, void* stream) {
   SKP_CHECK_ARG(x && gamma && beta && y && partial && part, "null pointer");
-  SKP_CHECK_ARG(nseg > 0, "nseg must be positive");
+  SKP_CHECK_ARG(nseg > 0 && HW % nseg == 0, "nseg must divide H·W");
   GNShape sh;
   SKP_CHECK_ARG(make_shape(B, C, HW, G, sh), "bad shape (C must be divisible by G)");
   SKP_CHECK_ARG((reinterpret_cast<uintptr_t>(part) & 7) == 0, "part must be 8-byte aligned");

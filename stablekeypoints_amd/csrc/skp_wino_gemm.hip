@@ -129,6 +129,86 @@ __global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__
   }
 }
 
+// The same inverse transform with the GEMM's product laid out [p][k][t] (M[p] = U[p]ᵀ · V[p], the
+// operands swapped): one thread per (output channel, tile), a block's threads over consecutive
+// tiles of one channel, so the 36 loads per thread are coalesced over t AND the 4×4 tiles leave as
+// contiguous image-row runs (the [p][t][k] form above stores one 16-B piece per lane into 64
+// different channel planes).  gnp (optional): the next GroupNorm's (Σ, Σ²) of the output per
+// segment of min(P, 64) tiles of one channel plane (P = tiles per plane, 16, 32 or a multiple of
+// 64), nseg = P / min(P, 64) per plane, reduced over the segment's lanes.
+__global__ __launch_bounds__(256) void wino_out_kt_kernel(const float* __restrict__ M, int B, int K, int H, int W,
+                                                          const float* __restrict__ bias,
+                                                          const float* __restrict__ res, float* __restrict__ y,
+                                                          float2* __restrict__ gnp) {
+  const int tw = W >> 2, th = H >> 2, P = th * tw, T = B * P;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int k = blockIdx.y;
+  const bool live = t < T;
+  const int tt = live ? t : T - 1;
+  const int b = tt / P, r = tt - b * P;
+  const int ty = r / tw, tx = r - ty * tw;
+  const size_t ps = (size_t)K * T;
+  const float* m = M + (size_t)k * T + tt;
+  float mv[6][6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) mv[i][j] = m[(size_t)(6 * i + j) * ps];
+  float tmp[4][6];   // Aᵀ M
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      float s = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+        if (kAt[q][i] != 0.0f) s = fmaf(kAt[q][i], mv[i][j], s);
+      tmp[q][j] = s;
+    }
+  const float bk = bias ? bias[k] : 0.0f;
+  const size_t base = ((size_t)b * K + k) * H * W + (size_t)(4 * ty) * W + 4 * tx;
+  float s1 = 0.0f, s2 = 0.0f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float o[4];
+#pragma unroll
+    for (int s2i = 0; s2i < 4; ++s2i) {
+      float s = 0.0f;
+#pragma unroll
+      for (int j = 0; j < 6; ++j)
+        if (kAt[s2i][j] != 0.0f) s = fmaf(tmp[q][j], kAt[s2i][j], s);
+      o[s2i] = s;
+    }
+    const size_t off = base + (size_t)q * W;
+    float4 v = make_float4(o[0], o[1], o[2], o[3]);
+    if (bias) {
+      v.x += bk; v.y += bk; v.z += bk; v.w += bk;
+    }
+    if (res) {
+      const float4 rv = *reinterpret_cast<const float4*>(res + off);
+      v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
+    }
+    if (live) *reinterpret_cast<float4*>(y + off) = v;
+    s1 += (v.x + v.y) + (v.z + v.w);
+    s2 += (v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w);
+  }
+  if (gnp) {   // uniform: the segment's lanes all take part (dead lanes of a ragged tail add 0)
+    if (!live) s1 = s2 = 0.0f;
+    const int seg = P < 64 ? P : 64;
+    // reduce over aligned groups of `seg` lanes (16, 32 or 64; lanes of a segment are one plane)
+    s1 += dpp_read<0xB1>(s1); s2 += dpp_read<0xB1>(s2);
+    s1 += dpp_read<0x4E>(s1); s2 += dpp_read<0x4E>(s2);
+    s1 += dpp_read<0x141>(s1); s2 += dpp_read<0x141>(s2);
+    s1 += dpp_read<0x140>(s1); s2 += dpp_read<0x140>(s2);
+    if (seg >= 32) { s1 += __shfl_xor(s1, 16, 64); s2 += __shfl_xor(s2, 16, 64); }
+    if (seg >= 64) { s1 += __shfl_xor(s1, 32, 64); s2 += __shfl_xor(s2, 32, 64); }
+    if (live && (threadIdx.x & (seg - 1)) == 0) {
+      const int nseg = P / seg;
+      gnp[((size_t)b * K + k) * nseg + r / seg] = make_float2(s1, s2);
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int skp_wino_in_transform(const float* x, int B, int C, int H, int W, float* V, void* stream) {
@@ -156,6 +236,25 @@ extern "C" int skp_wino_out_transform(const float* M, int B, int K, int H, int W
   SKP_CHECK_ARG(T <= 65535, "more than 65535 tiles (grid y)");
   hipLaunchKernelGGL(wino_out_kernel, dim3((K + 255) / 256, (unsigned)T), dim3(256), 0, as_stream(stream), M, B, K, H,
                      W, bias, residual, y);
+  SKP_LAUNCH_CHECK();
+  return SKP_OK;
+}
+
+extern "C" int skp_wino_out_transform_kt(const float* M, int B, int K, int H, int W, const float* bias,
+                                         const float* residual, float* y, float* gn_part, void* stream) {
+  SKP_CHECK_ARG(M && y, "null pointer");
+  SKP_CHECK_ARG(B > 0 && K > 0 && H > 0 && W > 0, "non-positive shape");
+  SKP_CHECK_ARG(H % 4 == 0 && W % 4 == 0, "H and W must be multiples of 4");
+  SKP_CHECK_ARG(K <= 65535, "more than 65535 output channels (grid y)");
+  SKP_CHECK_ARG((reinterpret_cast<uintptr_t>(y) & 15) == 0 &&
+                    (!residual || (reinterpret_cast<uintptr_t>(residual) & 15) == 0),
+                "y and residual must be 16-B aligned");
+  const long long P = (long long)(H / 4) * (W / 4), T = B * P;
+  SKP_CHECK_ARG(T < (1LL << 31), "too many tiles");
+  SKP_CHECK_ARG(!gn_part || ((P == 16 || P == 32 || P % 64 == 0) && (reinterpret_cast<uintptr_t>(gn_part) & 7) == 0),
+                "gn_part: tiles per plane must be 16, 32 or a multiple of 64; 8-B aligned");
+  hipLaunchKernelGGL(wino_out_kt_kernel, dim3((unsigned)((T + 255) / 256), K), dim3(256), 0, as_stream(stream), M, B,
+                     K, H, W, bias, residual, y, reinterpret_cast<float2*>(gn_part));
   SKP_LAUNCH_CHECK();
   return SKP_OK;
 }

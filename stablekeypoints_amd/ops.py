@@ -1575,16 +1575,33 @@ def _wino_u_gemm(weight, flip):
     return U
 
 
-def _wino_gemm_conv(x, weight, flip, bias, residual, K):
+# A/B (SKP_WINO_KT=0: the (36, T, K) product and its per-lane scattered tile stores): the product
+# as (36, K, T), so the output transform reads it and writes the tiles coalesced (and leaves the
+# next GroupNorm's statistics partials, as the fused kernel does)
+WINO_KT = os.environ.get("SKP_WINO_KT", "1") != "0"
+
+
+def _wino_gemm_conv(x, weight, flip, bias, residual, K, gn=False):
     B, C, H, W = x.shape
     T = B * (H // 4) * (W // 4)
     U = _wino_u_gemm(weight, flip)
     V = torch.empty(36, C, T, device=x.device, dtype=F32)
     call("skp_wino_in_transform", ptr(x), B, C, H, W, ptr(V), stream(x.device))
-    M = torch.bmm(V.transpose(1, 2), U)                              # (36, T, K)
     y = torch.empty(B, K, H, W, device=x.device, dtype=F32)
-    call("skp_wino_out_transform", ptr(M), B, K, H, W, ptr(bias) if bias is not None else None,
-         ptr(residual) if residual is not None else None, ptr(y), stream(x.device))
+    bp, rp = ptr(bias) if bias is not None else None, ptr(residual) if residual is not None else None
+    if not WINO_KT:
+        M = torch.bmm(V.transpose(1, 2), U)                          # (36, T, K)
+        call("skp_wino_out_transform", ptr(M), B, K, H, W, bp, rp, ptr(y), stream(x.device))
+        return y
+    M = torch.bmm(U.transpose(1, 2), V)                              # (36, K, T)
+    P = (H // 4) * (W // 4)
+    gnp = None
+    if gn and GN_EPI and (P in (16, 32) or P % 64 == 0):
+        nseg = P // min(P, 64)
+        gnp = torch.empty(B, K, nseg, 2, device=x.device, dtype=F32)
+    call("skp_wino_out_transform_kt", ptr(M), B, K, H, W, bp, rp, ptr(y), ptr(gnp), stream(x.device))
+    if gnp is not None:
+        y._skp_gn = (y._version, gnp, gnp.shape[2])
     return y
 
 
@@ -1593,7 +1610,7 @@ def _wino_conv(x, weight, flip, bias, residual, K, gn=False):
     kernel can write them (skp_conv3x3_wino2_gn: one split, H and W multiples of 32)."""
     B, C, H, W = x.shape
     if _wino_gemm_ok(B, C, K, H, W):
-        return _wino_gemm_conv(x, weight, flip, bias, residual, K)
+        return _wino_gemm_conv(x, weight, flip, bias, residual, K, gn)
     y = torch.empty(B, K, H, W, device=x.device, dtype=F32)
     # the kernels address x through 32-bit buffer offsets: batches above 2 GiB run in chunks
     per_img = C * H * W * 4
@@ -1601,7 +1618,7 @@ def _wino_conv(x, weight, flip, bias, residual, K, gn=False):
     gnp = None
     if gn and GN_EPI and H % 32 == 0 and W % 32 == 0 and all(
             _wino_plan(min(B, b0 + bmax) - b0, C, K, H, W)[:2] == (True, 1) for b0 in range(0, B, bmax)):
-        nseg = (H // 8) * (W // 32)
+        nseg = (H // 16) * (W // 32)
         gnp = torch.empty(B, K, nseg, 2, device=x.device, dtype=F32)
     for b0 in range(0, B, bmax):
         b1 = min(B, b0 + bmax)

@@ -46,8 +46,8 @@ def test_conv_epilogue_groupnorm_statistics(monkeypatch, B, C, K, H, W, res, shi
     parts = ops._gn_parts_of(y)
     assert parts is not None, "the convolution left no statistics partials"
     gp, nseg = parts
-    assert nseg == (H // 8) * (W // 32)
-    seg = y.double().reshape(B, K, H // 8, 8, W // 32, 32)
+    assert nseg == (H // 16) * (W // 32)
+    seg = y.double().reshape(B, K, H // 16, 16, W // 32, 32)
     s1 = seg.sum(dim=(3, 5)).reshape(B, K, nseg)
     s2 = (seg * seg).sum(dim=(3, 5)).reshape(B, K, nseg)
     a1 = seg.abs().sum(dim=(3, 5)).reshape(B, K, nseg)
@@ -90,3 +90,37 @@ def test_resnet_block_with_epilogue_statistics_matches_plain(monkeypatch):
         outs.append((y.detach(), x.grad))
     for a, b in zip(outs[0], outs[1]):
         assert float((a - b).abs().max()) / float(b.abs().max()) < 1e-4
+
+
+@pytest.mark.parametrize("B,C,K,H,W,res", [(8, 640, 640, 32, 32, True), (8, 1280, 1280, 16, 16, False),
+                                           (4, 256, 256, 16, 32, False), (2, 256, 320, 32, 64, True)])
+def test_wino_gemm_groupnorm_statistics(monkeypatch, B, C, K, H, W, res):
+    """The Winograd-GEMM form (skp_wino_out_transform_kt): the same partials per segment of
+    min(P, 64) tiles, output equal to the (36, T, K) form's within fp32 GEMM rounding."""
+    from stablekeypoints_amd import ops
+    g = torch.Generator(device=DEV).manual_seed(B + C + K + H + W)
+    x = torch.randn(B, C, H, W, device=DEV, generator=g)
+    w = torch.randn(K, C, 3, 3, device=DEV, generator=g) / (3 * C ** 0.5)
+    bias = torch.randn(K, device=DEV, generator=g)
+    r = torch.randn(B, K, H, W, device=DEV, generator=g) if res else None
+    assert ops._wino_gemm_ok(B, C, K, H, W)
+    y = ops.conv3x3(x, w, bias, r)
+    gp, nseg = ops._gn_parts_of(y)
+    th, tw = H // 4, W // 4
+    P = th * tw
+    seg = min(P, 64)
+    assert nseg == P // seg
+    tiles = y.double().reshape(B, K, th, 4, tw, 4)
+    s1 = tiles.sum(dim=(3, 5)).reshape(B, K, nseg, seg).sum(-1)
+    s2 = (tiles * tiles).sum(dim=(3, 5)).reshape(B, K, nseg, seg).sum(-1)
+    a1 = tiles.abs().sum(dim=(3, 5)).reshape(B, K, nseg, seg).sum(-1)
+    assert float(((gp[..., 0].double() - s1).abs() / a1).max()) < 1e-5
+    assert float(((gp[..., 1].double() - s2).abs() / s2).max()) < 1e-5
+    monkeypatch.setattr(ops, "WINO_KT", False)
+    y0 = ops.conv3x3(x, w, bias, r)
+    assert ops._gn_parts_of(y0) is None
+    assert float((y - y0).abs().max()) <= 2e-5 * float(y0.abs().max())
+    ref = torch.nn.functional.conv2d(x.double(), w.double(), bias.double(), padding=1)
+    if r is not None:
+        ref = ref + r.double()
+    assert float((y.double() - ref).abs().max()) <= 3e-5 * float(ref.abs().max())
