@@ -46,6 +46,15 @@ def _c16(t):
     return t if t.data_ptr() % 16 == 0 else t.clone()
 
 
+def _rows16(t):
+    """fp32 with unit-stride, 16-B aligned rows (row stride a multiple of 4 floats, e.g. a column
+    block of a fused projection's output) as it is; anything else through _c16."""
+    if (t.dtype == F32 and t.stride(-1) == 1 and t.stride(-2) % 4 == 0 and t.data_ptr() % 16 == 0
+            and (t.dim() < 3 or t.shape[0] == 1 or t.stride(0) % 4 == 0)):
+        return t
+    return _c16(t)
+
+
 # --------------------------------------------------------------------------- Q·Kᵀ on MFMA
 def bgemm(a, b, alpha=1.0, out=None, accumulate=False):
     """out[z] = alpha · a[z] @ b[z] for 3-D fp32 tensors of any strides (skp_bgemm_f32)."""
@@ -80,11 +89,11 @@ class CaptureLogitsHeads(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, qf, k1, H, scale):
-        qf, k1 = _c16(qf), _c16(k1)
+        qf, k1 = _c16(qf), _rows16(k1)
         B, S, C = qf.shape
-        N, d = k1.shape[1], C // H
+        N, d, rk = k1.shape[1], C // H, k1.stride(1)
         z = torch.empty(B * H, S, N, device=qf.device, dtype=F32)
-        bgemm_2b(qf, (S * C, d, C, 1), k1, (0, d, 1, C), z, (H * S * N, S * N, N, 1), B * H, H, S, N, d, scale)
+        bgemm_2b(qf, (S * C, d, C, 1), k1, (0, d, 1, rk), z, (H * S * N, S * N, N, 1), B * H, H, S, N, d, scale)
         ctx.save_for_backward(qf, k1)
         ctx.meta = (H, float(scale))
         return z
@@ -94,12 +103,12 @@ class CaptureLogitsHeads(torch.autograd.Function):
         qf, k1 = ctx.saved_tensors
         H, scale = ctx.meta
         B, S, C = qf.shape
-        N, d = k1.shape[1], C // H
+        N, d, rk = k1.shape[1], C // H, k1.stride(1)
         dz = _c16(dz)
         dq = dk1 = None
         if ctx.needs_input_grad[0]:
             dq = torch.empty_like(qf)
-            bgemm_2b(dz, (H * S * N, S * N, N, 1), k1, (0, d, C, 1), dq, (S * C, d, C, 1), B * H, H, S, d, N, scale)
+            bgemm_2b(dz, (H * S * N, S * N, N, 1), k1, (0, d, rk, 1), dq, (S * C, d, C, 1), B * H, H, S, d, N, scale)
         if ctx.needs_input_grad[1]:
             dkb = torch.empty(B, N, C, device=qf.device, dtype=F32)
             bgemm_2b(dz, (H * S * N, S * N, 1, N), qf, (S * C, d, C, 1), dkb, (N * C, d, C, 1), B * H, H, N, d, S,
@@ -117,12 +126,12 @@ class AttnPVHeads(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, P, v1, H):
-        P, v1 = _c16(P), _c16(v1)
+        P, v1 = _c16(P), _rows16(v1)
         BH, S, N = P.shape
         B, C = BH // H, v1.shape[2]
-        d = C // H
+        d, rv = C // H, v1.stride(1)
         out = torch.empty(B, S, C, device=P.device, dtype=F32)
-        bgemm_2b(P, (H * S * N, S * N, N, 1), v1, (0, d, C, 1), out, (S * C, d, C, 1), BH, H, S, d, N)
+        bgemm_2b(P, (H * S * N, S * N, N, 1), v1, (0, d, rv, 1), out, (S * C, d, C, 1), BH, H, S, d, N)
         ctx.save_for_backward(P, v1)
         ctx.H = H
         return out
@@ -133,12 +142,12 @@ class AttnPVHeads(torch.autograd.Function):
         H = ctx.H
         BH, S, N = P.shape
         B, C = BH // H, v1.shape[2]
-        d = C // H
+        d, rv = C // H, v1.stride(1)
         dout = _c16(dout)
         dP = dv1 = None
         if ctx.needs_input_grad[0]:
             dP = torch.empty_like(P)
-            bgemm_2b(dout, (S * C, d, C, 1), v1, (0, d, 1, C), dP, (H * S * N, S * N, N, 1), BH, H, S, N, d)
+            bgemm_2b(dout, (S * C, d, C, 1), v1, (0, d, 1, rv), dP, (H * S * N, S * N, N, 1), BH, H, S, N, d)
         if ctx.needs_input_grad[1]:
             dvb = torch.empty(B, N, C, device=P.device, dtype=F32)
             bgemm_2b(P, (H * S * N, S * N, 1, N), dout, (S * C, d, C, 1), dvb, (N * C, d, C, 1), BH, H, N, d, S)
@@ -1379,6 +1388,64 @@ def attention_heads(q, k, v, H, scale):
 
 
 # --------------------------------------------------------------------------- UNet-side: token projections
+_QKV_W = {}   # (id wq, id wk, id wv) -> ((versions), weakref(wq), [wq; wk; wv])
+
+
+def _qkv_weight(*ws):
+    """[w0; w1; …] of frozen projection weights, built once per weight set (and its versions)."""
+    key = tuple(id(w) for w in ws)
+    ver = tuple(w._version for w in ws)
+    ent = _QKV_W.get(key)
+    if ent is not None and ent[0] == ver and ent[1]() is ws[0]:
+        return ent[2]
+    w3 = torch.cat([w.detach() for w in ws], 0).contiguous()
+    _QKV_W[key] = (ver, _weakref.ref(ws[0], lambda _r, key=key: _QKV_W.pop(key, None)), w3)
+    return w3
+
+
+class QKVProjection(torch.autograd.Function):
+    """q, k, v = to_q(x), to_k(x), to_v(x) of a self-attention (diffusers CrossAttention with
+    context = x, bias-free, frozen) as ONE GEMM against [Wq; Wk; Wv] (x read once; q, k, v are
+    column views of the (B, S, 3C) product).  Backward: dx = dq Wq, then dk Wk and dv Wv
+    accumulated into it by the GEMM (beta = 1): no separate gradient-sum passes over dx."""
+
+    @staticmethod
+    def forward(ctx, x, w3, C):
+        out = torch.matmul(x, w3.t())
+        ctx.save_for_backward(w3)
+        ctx.C = C
+        ctx.set_materialize_grads(False)   # an unused projection's gradient stays None (skipped)
+        return tuple(out[..., i * C:(i + 1) * C] for i in range(w3.shape[0] // C))
+
+    @staticmethod
+    def backward(ctx, *grads):
+        (w3,) = ctx.saved_tensors
+        C = ctx.C
+        dx = None
+        for i, g in enumerate(grads):
+            if g is None:
+                continue
+            lead = g.shape[:-1]
+            g2 = g.reshape(-1, C)
+            wi = w3[i * C:(i + 1) * C]
+            if dx is None:
+                dx = torch.mm(g2, wi)
+            else:
+                dx.addmm_(g2, wi)
+        return dx.view(*lead, w3.shape[1]), None, None
+
+
+# A/B (SKP_QKV=0: three nn.Linear calls and autograd's gradient sum)
+QKV_FUSED = os.environ.get("SKP_QKV", "1") != "0"
+
+
+def qkv_projection(x, *ws):
+    """(x W0ᵀ, x W1ᵀ, …) of bias-free projections with equal output widths on the HIP device in
+    one GEMM (QKVProjection): q, k, v of a self-attention, or k, v of the shared context."""
+    _lib.require_device(x)
+    return QKVProjection.apply(x, _qkv_weight(*ws), int(ws[0].shape[0]))
+
+
 class TokensProjIn(torch.autograd.Function):
     """Transformer2DModel.proj_in (1×1 conv) + NCHW→(B, HW, C') as ONE strided batched GEMM:
     h[b] = x[b]ᵀ Wᵀ + bias, x (B, C, HW) read through a transposed view (no permute copy, no

@@ -22,7 +22,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
-from .sd.unet import CaptureComplete, _shared_context, attention_core, kv_projection
+from .sd.unet import CaptureComplete, _shared_context, attention_core, kv_projection, shared_kv
 
 
 # --------------------------------------------------------------------------- A2 controller / store
@@ -182,7 +182,7 @@ def register_attention_control(model, controller, feature_upsample_res=256):
                 s = int(sequence_length ** 0.5)
                 if s * s != sequence_length:
                     raise ValueError(f"capture needs a square token grid, got {sequence_length}")
-                k1, v1 = self.to_k(one), self.to_v(one)
+                k1, v1 = shared_kv(self, one)
                 sim = ops.capture_logits_heads(q, k1, h, self.scale)      # (B·H, s², N), MFMA
                 if getattr(controller, "stores_logits", False):
                     controller({"attn": sim, "size": s, "heads": h}, is_cross, place_in_unet)

@@ -132,13 +132,19 @@ class CrossAttention(nn.Module):
         context = x if context is None else context
         if mask is None and USE_FUSED_GROUPNORM and x.is_cuda and CrossAttention.backend == "math":
             from .. import ops   # attention straight on the (B, S, H·d) projections: no head permutes
-            qf = self.to_q(x)
-            one = _shared_context(context)
-            if one is not None:   # one sequence for the whole batch: projected once
-                k1, v1 = self.to_k(one), self.to_v(one)
-                kf, vf = k1.expand(x.shape[0], -1, -1), v1.expand(x.shape[0], -1, -1)
+            one = None
+            if context is x and ops.QKV_FUSED and _fused(x, self.to_q, self.to_k, self.to_v) and \
+                    self.to_q.bias is None and self.to_k.bias is None and self.to_v.bias is None:
+                # self-attention: q, k, v in one GEMM, their input gradients summed inside it
+                qf, kf, vf = ops.qkv_projection(x, self.to_q.weight, self.to_k.weight, self.to_v.weight)
             else:
-                kf, vf = kv_projection(self, context)
+                qf = self.to_q(x)
+                one = _shared_context(context)
+                if one is not None:   # one sequence for the whole batch: projected once
+                    k1, v1 = shared_kv(self, one)
+                    kf, vf = k1.expand(x.shape[0], -1, -1), v1.expand(x.shape[0], -1, -1)
+                else:
+                    kf, vf = kv_projection(self, context)
             out = ops.attention_heads(qf, kf, vf, self.heads, self.scale)
             if out is None and one is not None and SHARED_HEAD_MAJOR and torch.is_grad_enabled():
                 out = shared_context_attention(qf, k1, v1, self.heads, self.scale)
@@ -176,6 +182,15 @@ def _shared_context(context):
     return None
 
 
+def shared_kv(attn, one):
+    """to_k(one), to_v(one) of the (1, L, C) context the batch shares: one GEMM against [Wk; Wv]
+    whose input gradient sums both projections' (ops.qkv_projection) on the fused path."""
+    from .. import ops
+    if ops.QKV_FUSED and _fused(one, attn.to_k, attn.to_v) and attn.to_k.bias is None and attn.to_v.bias is None:
+        return ops.qkv_projection(one, attn.to_k.weight, attn.to_v.weight)
+    return attn.to_k(one), attn.to_v(one)
+
+
 def shared_context_attention(qf, k1, v1, H, scale):
     """softmax(q kᵀ·scale) v per head for (B, S, H·d) queries against ONE (1, L, H·d) key / value
     sequence shared by the batch, with the heads outermost: q as (H, B·S, d), k / v as (H, L, d),
@@ -199,7 +214,8 @@ def kv_projection(attn, context):
     one = _shared_context(context)
     if one is not None:
         B = context.shape[0]
-        return attn.to_k(one).expand(B, -1, -1), attn.to_v(one).expand(B, -1, -1)
+        k1, v1 = shared_kv(attn, one)
+        return k1.expand(B, -1, -1), v1.expand(B, -1, -1)
     return attn.to_k(context), attn.to_v(context)
 
 

@@ -46,3 +46,29 @@ def test_heads_gemms_match_the_permuted_reference(B, S, N, H, d):
                        ("dv", v.grad, vr.grad)):
         err = float((a.double() - b).abs().max() / b.abs().max())
         assert err < 1e-5, (name, err)
+
+
+@pytest.mark.parametrize("B,S,C", [(8, 4096, 320), (8, 256, 1280), (2, 64, 96)])
+def test_qkv_projection_matches_three_linears(B, S, C):
+    """ops.QKVProjection (one GEMM against [Wq; Wk; Wv], input gradients accumulated by the GEMM)
+    against diffusers' three bias-free to_q / to_k / to_v Linears with autograd's gradient sum."""
+    from stablekeypoints_amd import ops
+    g = torch.Generator(device=DEV).manual_seed(B * S + C)
+    x0 = torch.randn(B, S, C, device=DEV, generator=g)
+    ws = [torch.randn(C, C, device=DEV, generator=g) / C ** 0.5 for _ in range(3)]
+    gs = [torch.randn(B, S, C, device=DEV, generator=g) for _ in range(3)]
+    x = x0.clone().requires_grad_(True)
+    q, k, v = ops.qkv_projection(x, *ws)
+    (q * gs[0] + k * gs[1] + v * gs[2]).sum().backward()
+    xr = x0.double().requires_grad_(True)
+    outs = [xr @ w.double().t() for w in ws]
+    sum((o * gg.double()).sum() for o, gg in zip(outs, gs)).backward()
+    for a, b in zip((q, k, v), outs):
+        assert float((a.double() - b).abs().max() / b.abs().max()) < 1e-5
+    assert float((x.grad.double() - xr.grad).abs().max() / xr.grad.abs().max()) < 1e-5
+    # only some of the three used: the missing gradients are skipped
+    x2 = x0.clone().requires_grad_(True)
+    q2, _, v2 = ops.qkv_projection(x2, *ws)
+    (q2 * gs[0] + v2 * gs[2]).sum().backward()
+    ref = gs[0].double() @ ws[0].double() + gs[2].double() @ ws[2].double()
+    assert float((x2.grad.double() - ref).abs().max() / ref.abs().max()) < 1e-5
