@@ -554,12 +554,6 @@ constexpr int maps_pxw(int qpl) { return (32 / qpl) < 4 ? 4 : ((32 / qpl) > 16 ?
 #ifndef SKP_MAPS_PRIO
 #define SKP_MAPS_PRIO 1   // s_setprio level of the staging phase (0: off; 1, 2, 3 measured 972, 983, 982 vs 1003 us)
 #endif
-#ifndef SKP_MAPS_PF
-// 1: before a slab's pixel work, each wave issues LDS-DMA loads (into a 1 KB sink nobody reads) of
-// the next slab's vertical-pass rows, so that slab's staging loads hit L2 instead of waiting on
-// the Infinity Cache / HBM (no registers held; the DMAs drain at the next barrier); 0 = off (A/B)
-#define SKP_MAPS_PF 1
-#endif
 #ifndef SKP_MAPS_NT
 // 1: the maps and stats leave with non-temporal stores, so the 296 MB write stream does not evict
 // the z_low rows the XCD's other workgroups are about to read: 975 vs 994 µs, FETCH_SIZE 823 vs
@@ -596,31 +590,6 @@ void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nc
   const int jfirst = xcd * per + (blockIdx.x >> 3), jend = min(total, (xcd + 1) * per);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int row = lane >> 4, li = lane & 15;
-#if SKP_MAPS_PF
-  __shared__ __attribute__((aligned(16))) float pf_sink[256];
-  // L2-warm the 4 z_low row segments slab `it` of job `jb` reads (each the chunk's nc consecutive
-  // columns × N tokens, contiguous); bounded buffer descriptors, so nothing past a segment is read
-  auto prefetch = [&](int jb, int it) {
-    const int pxc = jb % nchunks, py = (jb / nchunks) % R, pb = jb / (nchunks * R);
-    const int l = it / H, h = it - l * H;
-    const int s = cl.s[l];
-    const int px0 = pxc * P, pnp = min(P, R - px0);
-    const int c0 = max(bicubic_taps(px0, s, R).lo, 0);
-    const int nc = min(bicubic_taps(px0 + pnp - 1, s, R).lo + 3, s - 1) - c0 + 1;
-    const Taps4 ty = bicubic_taps(py, s, R);
-    const float* zb = cl.z[l] + (size_t)(pb * H + h) * s * s * N;
-    const int seg = nc * N * 4;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (k > 0 && ty.i[k] == ty.i[k - 1]) continue;   // clamped edge rows repeat
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(zb + ((size_t)ty.i[k] * s + c0) * N), (short)0, seg, 0x00020000);
-      for (int off = wid * 1024; off < seg; off += WAVES * 1024)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)pf_sink, 16,
-                                                 off + lane * 16, 0, 0, 0);
-    }
-  };
-#endif
   for (int job = jfirst; job < jend; job += nper) {
     if (job != jfirst) __syncthreads();   // the previous job's store tile (in V) fully read
     const int xc = job % nchunks;
@@ -732,10 +701,6 @@ void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nc
       __builtin_amdgcn_s_setprio(0);
   #endif
       __syncthreads();
-  #if SKP_MAPS_PF
-      if (it + 1 < nslab) prefetch(job, it + 1);
-      else if (job + nper < jend) prefetch(job + nper, 0);
-  #endif
       const int l = it / H, bh = b * H + (it - l * H);
       const f4* V4 = reinterpret_cast<const f4*>(V + (it & 1) * vstride) + li;
       const float4* tw = TW + (l & 1) * P;

@@ -176,13 +176,14 @@ def register_attention_control(model, controller, feature_upsample_res=256):
                 return type(self).forward(self, x, context, mask)
             q = self.to_q(x)
             one = _shared_context(context) if (is_cross and mask is None and x.is_cuda) else None
-            if capture and one is not None and ops.heads_eligible(q, one, h):
+            # the shared embedding's k / v projected once (its (1, N, H·d) projections decide eligibility)
+            k1, v1 = shared_kv(self, one) if (capture and one is not None) else (None, None)
+            if k1 is not None and ops.heads_eligible(q, k1, h):
                 # the capture on the layer's own (B, S, H·d) projection and the ONE projection of the
                 # token embedding the batch shares: no head permutes, no batch-expanded keys / values
                 s = int(sequence_length ** 0.5)
                 if s * s != sequence_length:
                     raise ValueError(f"capture needs a square token grid, got {sequence_length}")
-                k1, v1 = shared_kv(self, one)
                 sim = ops.capture_logits_heads(q, k1, h, self.scale)      # (B·H, s², N), MFMA
                 if getattr(controller, "stores_logits", False):
                     controller({"attn": sim, "size": s, "heads": h}, is_cross, place_in_unet)
@@ -194,7 +195,10 @@ def register_attention_control(model, controller, feature_upsample_res=256):
                     raise CaptureComplete()   # the UNet output is discarded: skip this layer's output too
                 return to_out(ops.attn_pv_heads(sim.softmax(dim=-1), v1, h))
             context = context if is_cross else x
-            k, v = kv_projection(self, context)
+            if k1 is not None:
+                k, v = k1.expand(batch_size, -1, -1), v1.expand(batch_size, -1, -1)
+            else:
+                k, v = kv_projection(self, context)
             q = self.reshape_heads_to_batch_dim(q)
             k = self.reshape_heads_to_batch_dim(k)
             v = self.reshape_heads_to_batch_dim(v)

@@ -143,9 +143,21 @@ def _run(production, images, ctx0, w):
         unet_mod.SHARED_KV = True
 
 
-def test_sd15_fullsize_production_vs_plain_torch():
+def test_sd15_fullsize_production_vs_plain_torch(monkeypatch):
+    from stablekeypoints_amd import ops
     images, ctx0, w = _inputs()
+    calls = {"capture_logits_heads": 0, "qkv_projection": 0}
+    for name in calls:   # the production path must take the in-place head GEMMs and fused projections
+        fn = getattr(ops, name)
+
+        def spy(*a, _fn=fn, _name=name, **k):
+            calls[_name] += 1
+            return _fn(*a, **k)
+        monkeypatch.setattr(ops, name, spy)
     m_p, g_p, lat_p = _run(True, images, ctx0, w)
+    monkeypatch.undo()
+    assert calls["capture_logits_heads"] == 4, calls
+    assert calls["qkv_projection"] > 0, calls
     m_r, g_r, lat_r = _run(False, images, ctx0, w)
     torch.cuda.empty_cache()
     dlat = float((lat_p - lat_r).abs().max())

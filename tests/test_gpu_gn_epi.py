@@ -103,6 +103,7 @@ def test_wino_gemm_groupnorm_statistics(monkeypatch, B, C, K, H, W, res):
     w = torch.randn(K, C, 3, 3, device=DEV, generator=g) / (3 * C ** 0.5)
     bias = torch.randn(K, device=DEV, generator=g)
     r = torch.randn(B, K, H, W, device=DEV, generator=g) if res else None
+    monkeypatch.setattr(ops, "WINO_GEMM_MAX_HW", max(ops.WINO_GEMM_MAX_HW, H * W))   # 2 segments per plane
     assert ops._wino_gemm_ok(B, C, K, H, W)
     y = ops.conv3x3(x, w, bias, r)
     gp, nseg = ops._gn_parts_of(y)
