@@ -31,7 +31,7 @@ class _Calls:
     def __init__(self):
         self.names = []
 
-    def record(self, name, nbytes, flops=0):
+    def record(self, name, nbytes, flops=0, cycles=0):
         self.names.append(name)
 
         class _Ctx:

@@ -26,17 +26,24 @@ def main():
     ap.add_argument("--flop", type=int, required=True, help="algorithmic FLOP per launch (ops.capture_maps_flops)")
     ap.add_argument("--workload", default="")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--launches", default="", help="a:b = each kernel's a-th … (b−1)-th launches in dispatch order")
     args = ap.parse_args()
+    sel = tuple(int(v) for v in args.launches.split(":")) if args.launches else None
     names = [k for k in args.kernel.split(",") if k]
     per = {k: collections.defaultdict(dict) for k in names}
     for r in csv.DictReader(open(args.csv)):
         for k in names:
             if k in r["Kernel_Name"]:
                 per[k][r["Dispatch_Id"]][r["Counter_Name"]] = float(r["Counter_Value"])
+    def launch_rows(k):
+        rows = [per[k][i] for i in sorted(per[k], key=int)
+                if "SQ_ACTIVE_INST_VALU" in per[k][i] and per[k][i].get("GRBM_GUI_ACTIVE")]
+        return rows[sel[0]:sel[1]] if sel else rows
+
     num = den = 0.0
     counts = []
     for k in names:
-        rows = [d for d in per[k].values() if "SQ_ACTIVE_INST_VALU" in d and d.get("GRBM_GUI_ACTIVE")]
+        rows = launch_rows(k)
         if not rows:
             raise SystemExit(f"no counters for {k}")
         counts.append(len(rows))
@@ -44,7 +51,7 @@ def main():
         den += statistics.median(1024 * d["GRBM_GUI_ACTIVE"] / 8 for d in rows)
     busy = [num / den]
     if len(names) == 1:
-        rows = [d for d in per[names[0]].values() if "SQ_ACTIVE_INST_VALU" in d and d.get("GRBM_GUI_ACTIVE")]
+        rows = launch_rows(names[0])
         busy = [4 * d["SQ_ACTIVE_INST_VALU"] / (1024 * d["GRBM_GUI_ACTIVE"] / 8) for d in rows]
     rec = {args.name: {"valu_busy": statistics.median(busy), "launches": min(counts), "kernels": names,
                        "flop_per_launch": args.flop,
