@@ -219,110 +219,6 @@ __global__ __launch_bounds__(256) void sel_adj_kernel(SelSmall t, const float* _
   }
 }
 
-// ------------------------------------------------------------------------------ sel_doth / sel_adjv
-// sel_dot and sel_adj's horizontal pass in one kernel, so the (L, B·8, K, R²) e rows never reach
-// HBM: per (layer, bh, output row y) block the row's e_k[x] stay in LDS and the block reduces them
-// to Hs[k][y][j] = Σ_x A[j][x]·e_k[x] (A the adjoint tap matrix, x ascending — the arithmetic and
-// order of sel_adj's horizontal pass, so Hs and es are bit-identical to the two-kernel form);
-// sel_adjv then applies the vertical pass es[k][i][j] = Σ_y A[i][y]·Hs[k][y][j] per (layer, bh, k).
-// Hs plane of (l, bh, k): R rows × s columns at plane stride R·smax.
-__global__ __launch_bounds__(256) void sel_doth_kernel(SelSmall t, const float* __restrict__ zsel, int BH, int R,
-                                                       int H, int K, int smax, const long long* __restrict__ tok,
-                                                       const float* __restrict__ gsel, float gscale,
-                                                       float* __restrict__ Hs, float2* __restrict__ pix) {
-  extern __shared__ float shd[];
-  const int l = blockIdx.x / (BH * R);
-  const int rem = blockIdx.x - l * (BH * R);
-  const int bh = rem / R, y = rem % R;
-  const int b = bh / H;
-  const int S = t.s[l];
-  const int RP = R + 1;
-  float* Vs = shd;                 // S × K
-  float* A = Vs + S * K;           // S × (R + 1)
-  float* Er = A + S * RP;          // K × (R + 1)
-  const size_t RR = (size_t)R * R;
-  pix += (size_t)l * BH * RR;
-  const float2* stats = t.stats[l];
-  const Taps4 ty = bicubic_taps(y, S, R);
-  const float* zb = zsel + t.zoff[l] + (size_t)bh * S * S * K;
-  for (int e = threadIdx.x; e < S * K; e += blockDim.x) {
-    const int j = e / K, k = e - j * K;
-    float v = ty.w[0] * zb[((size_t)ty.i[0] * S + j) * K + k];
-    v = fmaf(ty.w[1], zb[((size_t)ty.i[1] * S + j) * K + k], v);
-    v = fmaf(ty.w[2], zb[((size_t)ty.i[2] * S + j) * K + k], v);
-    v = fmaf(ty.w[3], zb[((size_t)ty.i[3] * S + j) * K + k], v);
-    Vs[e] = v;
-  }
-  for (int e = threadIdx.x; e < S * RP; e += blockDim.x) A[e] = 0.0f;
-  __syncthreads();
-  for (int x = threadIdx.x; x < R; x += blockDim.x) {   // A[j][x] (one thread per x: fixed order)
-    const Taps4 tx = bicubic_taps(x, S, R);
-#pragma unroll
-    for (int m = 0; m < 4; ++m) A[tx.i[m] * RP + x] += tx.w[m];
-    const size_t p = (size_t)y * R + x;
-    const float2 st = stats[(size_t)bh * RR + p];
-    const float mb = __builtin_amdgcn_logf(st.y) - st.x * L2E;   // v_log_f32 = log2
-    float dot = 0.0f;
-    for (int k = 0; k < K; ++k) {
-      float e = 0.0f;
-      if (tok[(size_t)b * K + k] >= 0) {
-        float z = tx.w[0] * Vs[tx.i[0] * K + k];
-        z = fmaf(tx.w[1], Vs[tx.i[1] * K + k], z);
-        z = fmaf(tx.w[2], Vs[tx.i[2] * K + k], z);
-        z = fmaf(tx.w[3], Vs[tx.i[3] * K + k], z);
-        const float a = __builtin_amdgcn_exp2f(fmaf(z, L2E, mb));
-        e = a * (gsel[((size_t)b * K + k) * RR + p] * gscale);
-      }
-      dot += e;
-      Er[k * RP + x] = e;
-    }
-    pix[(size_t)bh * RR + p] = make_float2(mb, -dot);
-  }
-  __syncthreads();
-  float* hb = Hs + ((size_t)l * BH + bh) * K * (size_t)R * smax + (size_t)y * S;
-  for (int o = threadIdx.x; o < S * K; o += blockDim.x) {
-    const int j = o / K, k = o - j * K;
-    int x0, x1;
-    adj_range(j, S, R, x0, x1);
-    const float* Aj = A + j * RP;
-    const float* Ek = Er + k * RP;
-    float acc = 0.0f;
-    for (int x = x0; x <= x1; ++x) acc = fmaf(Aj[x], Ek[x], acc);
-    hb[(size_t)k * R * smax + j] = acc;
-  }
-}
-
-__global__ __launch_bounds__(256) void sel_adjv_kernel(SelSmall t, const float* __restrict__ Hs, int BHK, int smax,
-                                                       int R, float* __restrict__ es) {
-  extern __shared__ float sh[];
-  const int RP = R + 1;
-  const int l = blockIdx.x / BHK;
-  const int S = t.s[l];
-  float* A = sh;                 // S × (R + 1)
-  float* Hl = A + S * RP;        // R × S
-  const size_t bk = blockIdx.x - (size_t)l * BHK;  // bh·K + k
-  const float* hp = Hs + ((size_t)l * BHK + bk) * (size_t)R * smax;
-  es += (size_t)l * BHK * smax * smax;
-  for (int e = threadIdx.x; e < S * RP; e += blockDim.x) A[e] = 0.0f;
-  for (int e = threadIdx.x; e < R * S; e += blockDim.x) Hl[e] = hp[e];
-  __syncthreads();
-  for (int x = threadIdx.x; x < R; x += blockDim.x) {
-    const Taps4 tx = bicubic_taps(x, S, R);
-#pragma unroll
-    for (int m = 0; m < 4; ++m) A[tx.i[m] * RP + x] += tx.w[m];
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < S * S; e += blockDim.x) {
-    const int i = e / S, j = e - i * S;
-    int y0, y1;
-    adj_range(i, S, R, y0, y1);
-    const float* Ai = A + i * RP;
-    float acc = 0.0f;
-    for (int y = y0; y <= y1; ++y) acc = fmaf(Ai[y], Hl[y * S + j], acc);
-    es[bk * (size_t)S * S + e] = acc;
-  }
-}
-
 // ------------------------------------------------------------------------------ sel_dense
 struct SelLayers {   // up to 4 layers of the same s per launch
   const float* z[4];
@@ -744,30 +640,14 @@ extern "C" int skp_capture_maps_bwd_sel(const float* const* z_low, const int* si
   hipLaunchKernelGGL(sel_gather_kernel, dim3((unsigned)((t.zoff[L] + 255) / 256)), dim3(256), 0, st, t, L, BH, N, H,
                      sel_tok, K, zsel);
   SKP_LAUNCH_CHECK();
-  // SKP_SEL_EROWS=1 (A/B): the e rows through HBM (sel_dot → E → sel_adj)
-  static const bool erows = [] {
-    const char* e = getenv("SKP_SEL_EROWS");
-    return e && atoi(e) == 1;
-  }();
-  if (erows) {
-    hipLaunchKernelGGL(sel_dot_kernel, dim3((unsigned)(L * BH * R)), dim3(std::min(R, 256)),
-                       (size_t)smax * K * sizeof(float), st, t, zsel, BH, R, H, K, sel_tok, gsel, gscale, E, pix);
-    SKP_LAUNCH_CHECK();
-    const int tr = sel_adj_tile(R);
-    hipLaunchKernelGGL(sel_adj_kernel, dim3((unsigned)(L * BH * K)), dim3(256),
-                       (size_t)(smax * (R + 1) + R * smax + tr * (R + 1)) * sizeof(float), st, t, E, BH * K, smax, R,
-                       tr, es);
-    SKP_LAUNCH_CHECK();
-  } else {
-    float* Hs = E;   // (L, BH, K) planes of R × smax: a quarter of the E region at most
-    hipLaunchKernelGGL(sel_doth_kernel, dim3((unsigned)(L * BH * R)), dim3(std::min(R, 256)),
-                       (size_t)(smax * K + smax * (R + 1) + K * (R + 1)) * sizeof(float), st, t, zsel, BH, R, H, K,
-                       smax, sel_tok, gsel, gscale, Hs, pix);
-    SKP_LAUNCH_CHECK();
-    hipLaunchKernelGGL(sel_adjv_kernel, dim3((unsigned)(L * BH * K)), dim3(256),
-                       (size_t)(smax * (R + 1) + R * smax) * sizeof(float), st, t, Hs, BH * K, smax, R, es);
-    SKP_LAUNCH_CHECK();
-  }
+  hipLaunchKernelGGL(sel_dot_kernel, dim3((unsigned)(L * BH * R)), dim3(std::min(R, 256)),
+                     (size_t)smax * K * sizeof(float), st, t, zsel, BH, R, H, K, sel_tok, gsel, gscale, E, pix);
+  SKP_LAUNCH_CHECK();
+  const int tr = sel_adj_tile(R);
+  hipLaunchKernelGGL(sel_adj_kernel, dim3((unsigned)(L * BH * K)), dim3(256),
+                     (size_t)(smax * (R + 1) + R * smax + tr * (R + 1)) * sizeof(float), st, t, E, BH * K, smax, R, tr,
+                     es);
+  SKP_LAUNCH_CHECK();
   // the dense part: layers of equal s share a class (up to 4 per launch); two classes that have
   // a paired kernel (SD-1.5: s = 16 and 32 at R = 128) run as one launch
   SelLayers cls[SKP_MAX_LAYERS];
