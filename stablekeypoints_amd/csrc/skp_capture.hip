@@ -692,7 +692,13 @@ void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nc
     };
     const int nslab = L * H;
     for (int it = 0; it < nslab; ++it) {
-      if (it > 0) __syncthreads();   // V (and at a layer change the tap table) of slab it − 1 consumed
+#ifndef SKP_MAPS_B1
+#define SKP_MAPS_B1 0   // 958 vs 965 us (kbench maps8, profiles/r04u_maps_b1_ab.txt)
+#endif
+      // V and the tap table are double-buffered: slab it writes the buffers slab it − 2 read, and
+      // every thread finished those reads before the previous slab's post-staging barrier, so this
+      // barrier is redundant (SKP_MAPS_B1=0 drops it; A/B)
+      if (SKP_MAPS_B1 && it > 0) __syncthreads();
   #if SKP_MAPS_PRIO
       __builtin_amdgcn_s_setprio(SKP_MAPS_PRIO);   // the staging's loads ahead of the other workgroup's pixels
   #endif
