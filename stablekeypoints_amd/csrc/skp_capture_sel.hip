@@ -219,6 +219,98 @@ __global__ __launch_bounds__(256) void sel_adj_kernel(SelSmall t, const float* _
   }
 }
 
+// sel_adj with the horizontal pass as a rolling window (the capture backward's column trick): one
+// thread per E row streams its R pixels once (16-B loads), keeping the adjoint of the 4 low-res
+// columns lo(x) … lo(x) + 3 its taps reach in registers; a column is complete once lo passes it
+// (lo never decreases) and leaves for Hs in LDS, virtual columns −2, −1 / S, S + 1 folding into 0 /
+// S − 1 as torch's clamped taps.  4 FMAs per pixel and no LDS reads of E or of an adjoint matrix
+// (the per-(row, column) dot products of sel_adj re-read a ≈35-wide band of both per output).
+// The vertical pass is sel_adj's.  Block = (layer, bh, k), R threads (R ≤ 256, a multiple of 16).
+__global__ __launch_bounds__(256) void sel_adjw_kernel(SelSmall t, const float* __restrict__ E, int BHK, int smax,
+                                                       int R, float* __restrict__ es) {
+  extern __shared__ float sh[];
+  const int RP = R + 1;
+  const int l = blockIdx.x / BHK;
+  const int S = t.s[l];
+  float* A = sh;                                   // S × (R + 1), the vertical pass's adjoint matrix
+  float* Hs = A + S * RP;                          // R × S
+  float4* TW = reinterpret_cast<float4*>(Hs + R * S);   // [R] tap weights
+  int* TL = reinterpret_cast<int*>(TW + R);             // [R] first tap (unclamped)
+  const size_t bk = blockIdx.x - (size_t)l * BHK;  // bh·K + k
+  const float* Eb = E + ((size_t)l * BHK + bk) * (size_t)R * R;
+  es += (size_t)l * BHK * smax * smax;
+  const int y = threadIdx.x;
+  for (int e = y; e < S * RP; e += blockDim.x) A[e] = 0.0f;
+  __syncthreads();
+  if (y < R) {
+    const Taps4 tx = bicubic_taps(y, S, R);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) A[tx.i[m] * RP + y] += tx.w[m];
+    TW[y] = make_float4(tx.w[0], tx.w[1], tx.w[2], tx.w[3]);
+    TL[y] = tx.lo;
+  }
+  __syncthreads();
+  if (y < R) {
+    const float4* row = reinterpret_cast<const float4*>(Eb + (size_t)y * R);
+    float* hrow = Hs + y * S;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f, pend = 0.f;
+    int base = -2, pt = 0;
+    auto emit = [&](int c, float v) {   // virtual column c complete; clamped columns accumulate in order
+      const int tt = min(max(c, 0), S - 1);
+      if (tt != pt) {
+        hrow[pt] = pend;
+        pt = tt;
+        pend = v;
+      } else {
+        pend += v;
+      }
+    };
+    // groups of 4 float4 (16 pixels), the next group's loads in flight while this one is reduced
+    float4 cur[4], nxt[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cur[q] = q < R / 4 ? row[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int g0 = 0; g0 < R / 4; g0 += 4) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) nxt[q] = g0 + 4 + q < R / 4 ? row[g0 + 4 + q] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int x = 4 * g0 + u;   // R is a multiple of 16 on this path
+        const float4 ev = cur[u >> 2];
+        const float e1 = (u & 3) == 0 ? ev.x : (u & 3) == 1 ? ev.y : (u & 3) == 2 ? ev.z : ev.w;
+        const int lo = TL[x];
+        while (base < lo) {
+          emit(base, a0);
+          a0 = a1; a1 = a2; a2 = a3; a3 = 0.0f;
+          ++base;
+        }
+        const float4 w = TW[x];
+        a0 = fmaf(w.x, e1, a0);
+        a1 = fmaf(w.y, e1, a1);
+        a2 = fmaf(w.z, e1, a2);
+        a3 = fmaf(w.w, e1, a3);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
+    }
+    emit(base, a0);
+    emit(base + 1, a1);
+    emit(base + 2, a2);
+    emit(base + 3, a3);
+    hrow[pt] = pend;
+    for (int j = pt + 1; j < S; ++j) hrow[j] = 0.0f;   // columns no pixel reaches (none at R ≥ S)
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < S * S; e += blockDim.x) {
+    const int i = e / S, j = e - i * S;
+    int y0, y1;
+    adj_range(i, S, R, y0, y1);
+    const float* Ai = A + i * RP;
+    float acc = 0.0f;
+    for (int yy = y0; yy <= y1; ++yy) acc = fmaf(Ai[yy], Hs[yy * S + j], acc);
+    es[bk * (size_t)S * S + e] = acc;
+  }
+}
+
 // ------------------------------------------------------------------------------ sel_dense
 struct SelLayers {   // up to 4 layers of the same s per launch
   const float* z[4];
@@ -643,10 +735,21 @@ extern "C" int skp_capture_maps_bwd_sel(const float* const* z_low, const int* si
   hipLaunchKernelGGL(sel_dot_kernel, dim3((unsigned)(L * BH * R)), dim3(std::min(R, 256)),
                      (size_t)smax * K * sizeof(float), st, t, zsel, BH, R, H, K, sel_tok, gsel, gscale, E, pix);
   SKP_LAUNCH_CHECK();
-  const int tr = sel_adj_tile(R);
-  hipLaunchKernelGGL(sel_adj_kernel, dim3((unsigned)(L * BH * K)), dim3(256),
-                     (size_t)(smax * (R + 1) + R * smax + tr * (R + 1)) * sizeof(float), st, t, E, BH * K, smax, R, tr,
-                     es);
+  // SKP_SEL_ADJ=1: the rolling-window horizontal pass (sel_adjw_kernel); default: sel_adj's
+  // per-output banded dot products
+  static const bool adj_win = [] {
+    const char* e = getenv("SKP_SEL_ADJ");
+    return e && atoi(e) == 1;
+  }();
+  if (adj_win && R <= 256 && R % 16 == 0) {
+    hipLaunchKernelGGL(sel_adjw_kernel, dim3((unsigned)(L * BH * K)), dim3(R),
+                       (size_t)(smax * (R + 1) + R * smax + 5 * R) * sizeof(float), st, t, E, BH * K, smax, R, es);
+  } else {
+    const int tr = sel_adj_tile(R);
+    hipLaunchKernelGGL(sel_adj_kernel, dim3((unsigned)(L * BH * K)), dim3(256),
+                       (size_t)(smax * (R + 1) + R * smax + tr * (R + 1)) * sizeof(float), st, t, E, BH * K, smax, R,
+                       tr, es);
+  }
   SKP_LAUNCH_CHECK();
   // the dense part: layers of equal s share a class (up to 4 per launch); two classes that have
   // a paired kernel (SD-1.5: s = 16 and 32 at R = 128) run as one launch
