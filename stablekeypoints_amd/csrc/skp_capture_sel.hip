@@ -735,11 +735,11 @@ extern "C" int skp_capture_maps_bwd_sel(const float* const* z_low, const int* si
   hipLaunchKernelGGL(sel_dot_kernel, dim3((unsigned)(L * BH * R)), dim3(std::min(R, 256)),
                      (size_t)smax * K * sizeof(float), st, t, zsel, BH, R, H, K, sel_tok, gsel, gscale, E, pix);
   SKP_LAUNCH_CHECK();
-  // SKP_SEL_ADJ=1: the rolling-window horizontal pass (sel_adjw_kernel); default: sel_adj's
-  // per-output banded dot products
+  // the rolling-window horizontal pass (sel_adjw_kernel: 78 vs 104 us at the bench shape,
+  // profiles/r04aa_sel_adj_ab.txt); SKP_SEL_ADJ=0: sel_adj's per-output banded dot products (A/B)
   static const bool adj_win = [] {
     const char* e = getenv("SKP_SEL_ADJ");
-    return e && atoi(e) == 1;
+    return !(e && atoi(e) == 0);
   }();
   if (adj_win && R <= 256 && R % 16 == 0) {
     hipLaunchKernelGGL(sel_adjw_kernel, dim3((unsigned)(L * BH * K)), dim3(R),
