@@ -513,10 +513,22 @@ constexpr float kPadLogit = -1e30f;   // Σ taps ≈ 1, so padded tokens interpo
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef float f2v __attribute__((ext_vector_type(2)));
 
+// a wave-uniform pointer held in SGPRs: keeps the compiler from re-associating it with lane offsets
+// into per-lane 64-bit address arithmetic (global loads then take the saddr + 32-bit voffset form)
+// (global address space, so the loads stay global_load rather than flat_load)
+template <typename T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* uniform_ptr(T* p) {
+  const unsigned long long u = reinterpret_cast<unsigned long long>(p);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
+  return (__attribute__((address_space(1))) T*)(((unsigned long long)hi << 32) | lo);
+}
+
 struct CapLayers {
   const float* z[SKP_MAX_LAYERS];
   float2* stats[SKP_MAX_LAYERS];
   int s[SKP_MAX_LAYERS];
+  float sc[SKP_MAX_LAYERS];   // (float)s / (float)R, the bicubic scale (no division on the device)
 };
 
 // max / sum over each 16-lane row: four DPP steps, each one VALU op with the DPP source
@@ -605,169 +617,145 @@ void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nc
       for (int c = 0; c < QPL; ++c) acc[g][c] = (f4)0.0f;
 
     const bool vec = (N & 3) == 0;
-    // Per (layer, head) slab: stage the tap table (first head of a layer) and the vertical pass,
-    // then the pixel work; two workgroups per CU overlap one's staging with the other's pixels.
-    // (A software pipeline with double-buffered V measured slower: 1.03 vs 0.94 ms.)
-    auto layer_cols = [&](int l, int& s, int& c0, int& nc) {
-      s = cl.s[l];
-      c0 = max(bicubic_taps(x0, s, R).lo, 0);
-      nc = min(bicubic_taps(x0 + np - 1, s, R).lo + 3, s - 1) - c0 + 1;
-    };
-    auto stage = [&](int it) {   // tap table (first head of a layer) + vertical pass of slab it
-      const int l = it / H, h = it - l * H;
-      int s, c0, nc;
-      layer_cols(l, s, c0, nc);
-      const int buf = it & 1;
-      if (h == 0) {
+    // Per layer: the uniform setup (columns, vertical taps, the tap table) once; per (layer, head)
+    // slab: the vertical pass, then the pixel work; two workgroups per CU overlap one's staging
+    // with the other's pixels.  (A software pipeline with double-buffered V measured slower: 1.03
+    // vs 0.94 ms.)  r05: the layer's setup hoisted out of the head loop into scalar registers and
+    // the z_low rows addressed as uniform bases + 32-bit lane offsets (it had been ≈ 90 VALU per
+    // slab of 64-bit address and tap arithmetic recomputed per head).
+    const unsigned nq = N >> 2;
+    for (int l = 0; l < L; ++l) {
+      const int s = cl.s[l];
+      const float sc = cl.sc[l];
+      const int c0 = max(bicubic_taps_s(x0, s, sc).lo, 0);
+      const int nc = min(bicubic_taps_s(x0 + np - 1, s, sc).lo + 3, s - 1) - c0 + 1;
+      const Taps4 tyv = bicubic_taps_s(y, s, sc);
+      // uniform values: force them into SGPRs for the head loop
+      float wy[4];
+      unsigned ro[4];   // float offsets of the 4 tap rows' first column (c0) inside one (b, h) slab
+  #pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        wy[k] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, tyv.w[k])));
+        ro[k] = (unsigned)__builtin_amdgcn_readfirstlane((tyv.i[k] * s + c0) * N);
+      }
+      const int tot = __builtin_amdgcn_readfirstlane(nc * Npq);
+      {   // tap table of this layer (buffer l & 1: layer l − 1's readers may still run)
         float4* tw = TW + (l & 1) * P;
         int4* tiw = TI + (l & 1) * P;
         for (int x = tid; x < P; x += kMapThreads) {
-          const Taps4 t = bicubic_taps(x0 + min(x, np - 1), s, R);
+          const Taps4 t = bicubic_taps_s(x0 + min(x, np - 1), s, sc);
           tw[x] = make_float4(t.w[0], t.w[1], t.w[2], t.w[3]);
           tiw[x] = make_int4((t.i[0] - c0) * Npq, (t.i[1] - c0) * Npq, (t.i[2] - c0) * Npq, (t.i[3] - c0) * Npq);
         }
       }
-      const Taps4 ty = bicubic_taps(y, s, R);
-      const float* zb = cl.z[l] + (size_t)(b * H + h) * s * s * N;
-      float* Vb = V + buf * vstride;
-      // V[jj][n] = Σ_k wy_k · z[iy_k][c0 + jj][n]
-      if (vec) {
-        const f4* r0 = reinterpret_cast<const f4*>(zb + ((size_t)ty.i[0] * s + c0) * N);
-        const f4* r1 = reinterpret_cast<const f4*>(zb + ((size_t)ty.i[1] * s + c0) * N);
-        const f4* r2 = reinterpret_cast<const f4*>(zb + ((size_t)ty.i[2] * s + c0) * N);
-        const f4* r3 = reinterpret_cast<const f4*>(zb + ((size_t)ty.i[3] * s + c0) * N);
-        const int nq = N >> 2;
-        f4* V4 = reinterpret_cast<f4*>(Vb);
-        // up to VPT outputs per thread with all 4·VPT loads in flight before the first FMA
-  #ifndef SKP_MAPS_VPT
-  #define SKP_MAPS_VPT 1   // vertical outputs per thread per batch (2, 3 measured 1-2% slower)
-  #endif
-        constexpr int VPT = SKP_MAPS_VPT;
-        const int tot = nc * Npq;
-        for (int e0 = tid; e0 < tot; e0 += VPT * kMapThreads) {
-          f4 a[VPT][4];
-  #pragma unroll
-          for (int k = 0; k < VPT; ++k) {
-            const int e = e0 + k * kMapThreads;
-            const int jj = e / Npq, q = e - jj * Npq;
-            if (e < tot && q < nq) {
-              const int o = jj * nq + q;
-              a[k][0] = r0[o];
-              a[k][1] = r1[o];
-              a[k][2] = r2[o];
-              a[k][3] = r3[o];
-            }
-          }
-  #pragma unroll
-          for (int k = 0; k < VPT; ++k) {
-            const int e = e0 + k * kMapThreads;
-            const int jj = e / Npq, q = e - jj * Npq;
-            if (e < tot) {
-              f4 v = (f4)kPadLogit;
-              if (q < nq) {
-                v = a[k][0] * ty.w[0];
-                v = __builtin_elementwise_fma(a[k][1], (f4)ty.w[1], v);
-                v = __builtin_elementwise_fma(a[k][2], (f4)ty.w[2], v);
-                v = __builtin_elementwise_fma(a[k][3], (f4)ty.w[3], v);
-              }
-              V4[e] = v;
-            }
-          }
-        }
-      } else {
-  #pragma unroll 1
-        for (int e = tid; e < nc * Np; e += kMapThreads) {
-          const int jj = e / Np, n = e - jj * Np;
-          float v = kPadLogit;
-          if (n < N) {
-            const int j = c0 + jj;
-            v = ty.w[0] * zb[((size_t)ty.i[0] * s + j) * N + n];
-            v += ty.w[1] * zb[((size_t)ty.i[1] * s + j) * N + n];
-            v += ty.w[2] * zb[((size_t)ty.i[2] * s + j) * N + n];
-            v += ty.w[3] * zb[((size_t)ty.i[3] * s + j) * N + n];
-          }
-          Vb[e] = v;
-        }
-      }
-    };
-    const int nslab = L * H;
-    for (int it = 0; it < nslab; ++it) {
-#ifndef SKP_MAPS_B1
-#define SKP_MAPS_B1 0   // 958 vs 965 us (kbench maps8, profiles/r04u_maps_b1_ab.txt)
-#endif
-      // V and the tap table are double-buffered: slab it writes the buffers slab it − 2 read, and
-      // every thread finished those reads before the previous slab's post-staging barrier, so this
-      // barrier is redundant (SKP_MAPS_B1=0 drops it; A/B)
-      if (SKP_MAPS_B1 && it > 0) __syncthreads();
-  #if SKP_MAPS_PRIO
-      __builtin_amdgcn_s_setprio(SKP_MAPS_PRIO);   // the staging's loads ahead of the other workgroup's pixels
-  #endif
-      stage(it);
-  #if SKP_MAPS_PRIO
-      __builtin_amdgcn_s_setprio(0);
-  #endif
-      __syncthreads();
-      const int l = it / H, bh = b * H + (it - l * H);
-      const f4* V4 = reinterpret_cast<const f4*>(V + (it & 1) * vstride) + li;
       const float4* tw = TW + (l & 1) * P;
       const int4* tiw = TI + (l & 1) * P;
-      float2* st = cl.stats[l];
-  #pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const int xl = wid * PXW + 4 * g + row;              // pixel of this 16-lane row
-        const int xr = min(xl, np - 1);                        // past-the-edge rows redo a valid one
-        const float4 w = tw[xr];
-        const int4 ti = tiw[xr];
-        f4 zc[QPL];
-        float m = kPadLogit;
-  #pragma unroll
-        for (int c = 0; c < QPL; ++c) {
-#ifdef SKP_MAPS_PROBE_LDS2   // timing probe only (wrong maps): half the tap reads
-          const f4 a0 = V4[ti.x + 16 * c], a1 = V4[ti.y + 16 * c];
-          const f4 a2 = a1 * 0.5f, a3 = a0 * 0.25f;
-#else
-          const f4 a0 = V4[ti.x + 16 * c], a1 = V4[ti.y + 16 * c];
-          const f4 a2 = V4[ti.z + 16 * c], a3 = V4[ti.w + 16 * c];
-#endif
-          // token pairs on the packed f32 VALU: z = ((w0·a0 + w1·a1) + w2·a2) + w3·a3
-          f4 v = a0 * w.x;
-          v = __builtin_elementwise_fma(a1, (f4)w.y, v);
-          v = __builtin_elementwise_fma(a2, (f4)w.z, v);
-          v = __builtin_elementwise_fma(a3, (f4)w.w, v);
-          zc[c] = v;
-#ifndef SKP_MAPS_PROBE_NOMAX   // timing probe only: no max
-          m = __builtin_fmaxf(__builtin_fmaxf(m, v.x), v.y);
-          m = __builtin_fmaxf(__builtin_fmaxf(m, v.z), v.w);
-#endif
-          if (QPL > 4 || (c & 1)) __builtin_amdgcn_sched_barrier(0);   // bound the LDS reads in flight (registers)
+      for (int h = 0; h < H; ++h) {
+        const int it = l * H + h;
+        const int bh = b * H + h;
+  #if SKP_MAPS_PRIO
+        __builtin_amdgcn_s_setprio(SKP_MAPS_PRIO);   // the staging's loads ahead of the other workgroup's pixels
+  #endif
+        // V and the tap table are double-buffered: slab it writes the buffers slab it − 2 read, and
+        // every thread finished those reads before the previous slab's post-staging barrier
+        float* Vb = V + (it & 1) * vstride;
+        const float* zb = cl.z[l] + (size_t)bh * s * s * N;
+        if (vec) {
+          // V[jj][n] = Σ_k wy_k · z[iy_k][c0 + jj][n]: thread element e = tid + k·threads, lane
+          // offset o = jj·nq + q (a 32-bit offset from each uniform row base)
+          const auto* r0 = uniform_ptr(reinterpret_cast<const f4*>(zb + ro[0]));
+          const auto* r1 = uniform_ptr(reinterpret_cast<const f4*>(zb + ro[1]));
+          const auto* r2 = uniform_ptr(reinterpret_cast<const f4*>(zb + ro[2]));
+          const auto* r3 = uniform_ptr(reinterpret_cast<const f4*>(zb + ro[3]));
+          f4* V4 = reinterpret_cast<f4*>(Vb);
+          constexpr unsigned JS = kMapThreads / Npq;   // columns per thread step (4 at 8 waves, QPL 8)
+          static_assert(kMapThreads % Npq == 0, "thread step must cover whole columns");
+          const unsigned q = (unsigned)tid % Npq;
+          unsigned ob = (((unsigned)tid / Npq) * nq + q) * 16u;   // byte offset (saddr + 32-bit voffset loads)
+          const unsigned obs = JS * nq * 16u;
+          using gcf4 = const __attribute__((address_space(1))) f4;
+          using gcc = const __attribute__((address_space(1))) char;
+  #pragma unroll 1
+          for (int e = tid; e < tot; e += kMapThreads, ob += obs) {
+            f4 v = (f4)kPadLogit;
+            if (q < nq) {
+              const f4 a0 = *reinterpret_cast<gcf4*>(reinterpret_cast<gcc*>(r0) + ob);
+              const f4 a1 = *reinterpret_cast<gcf4*>(reinterpret_cast<gcc*>(r1) + ob);
+              const f4 a2 = *reinterpret_cast<gcf4*>(reinterpret_cast<gcc*>(r2) + ob);
+              const f4 a3 = *reinterpret_cast<gcf4*>(reinterpret_cast<gcc*>(r3) + ob);
+              v = a0 * wy[0];
+              v = __builtin_elementwise_fma(a1, (f4)wy[1], v);
+              v = __builtin_elementwise_fma(a2, (f4)wy[2], v);
+              v = __builtin_elementwise_fma(a3, (f4)wy[3], v);
+            }
+            V4[e] = v;
+          }
+        } else {
+  #pragma unroll 1
+          for (int e = tid; e < nc * Np; e += kMapThreads) {
+            const int jj = e / Np, n = e - jj * Np;
+            float v = kPadLogit;
+            if (n < N) {
+              const int j = c0 + jj;
+              v = wy[0] * zb[((size_t)tyv.i[0] * s + j) * N + n];
+              v += wy[1] * zb[((size_t)tyv.i[1] * s + j) * N + n];
+              v += wy[2] * zb[((size_t)tyv.i[2] * s + j) * N + n];
+              v += wy[3] * zb[((size_t)tyv.i[3] * s + j) * N + n];
+            }
+            Vb[e] = v;
+          }
         }
-#ifdef SKP_MAPS_PROBE_NOMAX
-        m = 0.0f;
-#else
-        m = row16_max(m);
-#endif
-        const f4 mb = (f4)(-m * L2E);
-        f4 sv = (f4)0.0f;
+  #if SKP_MAPS_PRIO
+        __builtin_amdgcn_s_setprio(0);
+  #endif
+        __syncthreads();
+        const f4* V4 = reinterpret_cast<const f4*>(Vb) + li;
+        // this (head, row, chunk)'s stats run: a uniform base, lane offsets xl
+        auto* st = cl.stats[l] ? uniform_ptr(reinterpret_cast<f2v*>(cl.stats[l]) + ((size_t)bh * R + y) * R + x0) : nullptr;
   #pragma unroll
-        for (int c = 0; c < QPL; ++c) {
-          f4 t = __builtin_elementwise_fma(zc[c], (f4)L2E, mb);
-#ifndef SKP_MAPS_PROBE_NOEXP   // timing probe only: no exp
-          t.x = __builtin_amdgcn_exp2f(t.x);
-          t.y = __builtin_amdgcn_exp2f(t.y);
-          t.z = __builtin_amdgcn_exp2f(t.z);
-          t.w = __builtin_amdgcn_exp2f(t.w);
-#endif
-          zc[c] = t;
-          sv += t;
+        for (int g = 0; g < G; ++g) {
+          const int xl = wid * PXW + 4 * g + row;              // pixel of this 16-lane row
+          const int xr = min(xl, np - 1);                        // past-the-edge rows redo a valid one
+          const float4 w = tw[xr];
+          const int4 ti = tiw[xr];
+          f4 zc[QPL];
+          float m = kPadLogit;
+  #pragma unroll
+          for (int c = 0; c < QPL; ++c) {
+            const f4 a0 = V4[ti.x + 16 * c], a1 = V4[ti.y + 16 * c];
+            const f4 a2 = V4[ti.z + 16 * c], a3 = V4[ti.w + 16 * c];
+            // token pairs on the packed f32 VALU: z = ((w0·a0 + w1·a1) + w2·a2) + w3·a3
+            f4 v = a0 * w.x;
+            v = __builtin_elementwise_fma(a1, (f4)w.y, v);
+            v = __builtin_elementwise_fma(a2, (f4)w.z, v);
+            v = __builtin_elementwise_fma(a3, (f4)w.w, v);
+            zc[c] = v;
+            m = __builtin_fmaxf(__builtin_fmaxf(m, v.x), v.y);
+            m = __builtin_fmaxf(__builtin_fmaxf(m, v.z), v.w);
+            if (QPL > 4 || (c & 1)) __builtin_amdgcn_sched_barrier(0);   // bound the LDS reads in flight (registers)
+          }
+          m = row16_max(m);
+          const f4 mb = (f4)(-m * L2E);
+          f4 sv = (f4)0.0f;
+  #pragma unroll
+          for (int c = 0; c < QPL; ++c) {
+            f4 t = __builtin_elementwise_fma(zc[c], (f4)L2E, mb);
+            t.x = __builtin_amdgcn_exp2f(t.x);
+            t.y = __builtin_amdgcn_exp2f(t.y);
+            t.z = __builtin_amdgcn_exp2f(t.z);
+            t.w = __builtin_amdgcn_exp2f(t.w);
+            zc[c] = t;
+            sv += t;
+          }
+          const float inv = __builtin_amdgcn_rcpf(row16_sum((sv.x + sv.y) + (sv.z + sv.w)));
+  #pragma unroll
+          for (int c = 0; c < QPL; ++c) acc[g][c] = __builtin_elementwise_fma(zc[c], (f4)inv, acc[g][c]);
+          if (st && li == 0 && xl < np) {
+            const f2v mi = {m, inv};
+            SKP_MAPS_ST(st[(unsigned)xl], mi);
+          }
+          __builtin_amdgcn_sched_barrier(0);   // keep the next pixels' LDS reads from being hoisted (registers)
         }
-        const float inv = __builtin_amdgcn_rcpf(row16_sum((sv.x + sv.y) + (sv.z + sv.w)));
-  #pragma unroll
-        for (int c = 0; c < QPL; ++c) acc[g][c] = __builtin_elementwise_fma(zc[c], (f4)inv, acc[g][c]);
-        if (st && li == 0 && xl < np) {
-        const f2v mi = {m, inv};
-        SKP_MAPS_ST(reinterpret_cast<f2v*>(st)[((size_t)bh * R + y) * R + x0 + xl], mi);
-      }
-        __builtin_amdgcn_sched_barrier(0);   // keep the next pixels' LDS reads from being hoisted (registers)
       }
     }
     // token-major store: round r stages tokens [128r, 128r + 128) of all P pixels in LDS; lane li
@@ -799,6 +787,223 @@ void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nc
         if (n + 1 < N) SKP_MAPS_ST(ob[(size_t)(n + 1) * R * R + xl], v.y);
         if (n + 2 < N) SKP_MAPS_ST(ob[(size_t)(n + 2) * R * R + xl], v.z);
         if (n + 3 < N) SKP_MAPS_ST(ob[(size_t)(n + 3) * R * R + xl], v.w);
+      }
+    }
+  }
+}
+
+// Tiled form of capture_maps_kernel (r05; default where it applies): ONE 16-wave workgroup per CU
+// owns a TY-row × TX-pixel tile of image b (TY·TX = 16 waves × PXW pixels: 2 × 32 or 4 × 16 at
+// N = 500).  The TY output rows of a tile tap at most TY + 3 consecutive z_low rows (lo(y) rises
+// by ≤ 1 per output row since s ≤ R), so each z_low value a thread loads feeds the vertical pass
+// of every row of the tile: per pixel the z_low load volume is 0.48× (2 × 32) or 0.40× (4 × 16)
+// that of the one-row form, whose per-slab staging was bound by the L2 → CU load rate (9.4 GB per
+// launch at the bench shape, §5).  V is double-buffered and the slab loop has ONE barrier: waves
+// 0-7 stage slab it + 1 before their pixels of slab it, waves 8-15 after them, so on every SIMD
+// two waves wait on their staging loads while the other two compute.  Per pixel the arithmetic is
+// the one-row kernel's operation for operation (same vertical FMA chain on the same z_low values,
+// same taps, max, exp, sums and accumulation order), so maps and stats are bit-identical to it.
+constexpr int kTileLdsFloats = 160 * 1024 / 4;   // the whole CU's LDS, statically (one workgroup per CU)
+template <int QPL, int TY, bool STAG>
+__global__ __launch_bounds__(16 * WAVE) __attribute__((amdgpu_waves_per_eu(4)))
+void capture_maps_tile_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nchunks, int vstride, float count,
+                              float* __restrict__ maps) {
+  __shared__ __attribute__((aligned(16))) float lds[kTileLdsFloats];
+  constexpr int kT = 16 * WAVE;
+  constexpr int PXW = maps_pxw(QPL);          // pixels per wave (one row of the tile)
+  constexpr int G = PXW / 4;
+  constexpr int WPR = 16 / TY;                // waves per tile row
+  constexpr int TX = WPR * PXW;               // pixels per tile row
+  constexpr int NR = TY + 3;                  // z_low rows one tile can tap
+  constexpr int Np = 64 * QPL;
+  constexpr int Npq = Np / 4;
+  constexpr float L2E = 1.4426950408889634f;
+  float4* TW = reinterpret_cast<float4*>(lds);              // [2][TX] tap weights (by layer parity)
+  int4* TI = reinterpret_cast<int4*>(lds + 8 * TX);          // [2][TX] tap offsets (column − c0) · Npq
+  float* V = lds + 16 * TX;                                  // [2 bufs][TY rows][vstride] (then the store tile)
+
+  const int nty = (R + TY - 1) / TY;
+  const int total = B * nty * nchunks;
+  const int per = (total + 7) / 8;
+  const int xcd = blockIdx.x & 7, nper = gridDim.x >> 3;
+  const int jfirst = xcd * per + (blockIdx.x >> 3), jend = min(total, (xcd + 1) * per);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int row = lane >> 4, li = lane & 15;
+  const int ry = wid / WPR;                   // this wave's tile row
+  const int nq = N >> 2;
+  const bool late = STAG && wid >= 8;        // stages after its pixels (see above)
+  for (int job = jfirst; job < jend; job += nper) {
+    const int xc = job % nchunks;
+    const int t = (job / nchunks) % nty;
+    const int b = job / (nchunks * nty);
+    const int y0 = TY * t;
+    const int ny = min(TY, R - y0);           // rows past the image redo its last row, stored never
+    const int x0 = xc * TX;
+    const int np = min(TX, R - x0);
+
+    f4 acc[G][QPL];
+  #pragma unroll
+    for (int g = 0; g < G; ++g)
+  #pragma unroll
+      for (int c = 0; c < QPL; ++c) acc[g][c] = (f4)0.0f;
+
+    // tap table (first head of a layer) + the tile rows' vertical passes of slab it into V[it & 1]
+    auto stage = [&](int it) {
+      const int l = it / H, h = it - l * H;
+      const int s = cl.s[l];
+      const int c0 = max(bicubic_taps(x0, s, R).lo, 0);
+      const int nc = min(bicubic_taps(x0 + np - 1, s, R).lo + 3, s - 1) - c0 + 1;
+      if (h == 0) {
+        float4* tw = TW + (l & 1) * TX;
+        int4* tiw = TI + (l & 1) * TX;
+        for (int x = tid; x < TX; x += kT) {
+          const Taps4 tx = bicubic_taps(x0 + min(x, np - 1), s, R);
+          tw[x] = make_float4(tx.w[0], tx.w[1], tx.w[2], tx.w[3]);
+          tiw[x] = make_int4((tx.i[0] - c0) * Npq, (tx.i[1] - c0) * Npq, (tx.i[2] - c0) * Npq, (tx.i[3] - c0) * Npq);
+        }
+      }
+      const int lo0 = bicubic_taps(y0, s, R).lo;
+      const int nraw = bicubic_taps(min(y0 + TY - 1, R - 1), s, R).lo - lo0 + 4;   // ≤ NR
+      const float* zb = cl.z[l] + (size_t)(b * H + h) * s * s * N + (size_t)c0 * N;
+      f4* Vb = reinterpret_cast<f4*>(V + (it & 1) * TY * vstride);
+      const int tot = nc * Npq;
+  #pragma unroll 1
+      for (int e = tid; e < tot; e += kT) {
+        const int jj = e / Npq, q = e - jj * Npq;
+        const bool ok = q < nq;
+        const int o = jj * nq + q;
+        f4 a[NR];
+  #pragma unroll
+        for (int m = 0; m < NR; ++m) {
+          const int zr = min(max(lo0 + m, 0), s - 1);
+          a[m] = (ok && m < nraw) ? reinterpret_cast<const f4*>(zb + (size_t)zr * s * N)[o] : (f4)0.0f;
+        }
+  #pragma unroll
+        for (int r = 0; r < TY; ++r) {
+          const Taps4 ty = bicubic_taps(min(y0 + r, R - 1), s, R);
+          const int d = ty.lo - lo0;            // uniform: this row's taps are a[d .. d + 3]
+          f4 v = (f4)kPadLogit;
+          if (ok) {
+  #pragma unroll
+            for (int dd = 0; dd <= (TY - 1 < 3 ? TY - 1 : 3); ++dd) {
+              if (dd == d) {   // uniform branch: fixed register indices per case
+                v = a[dd] * ty.w[0];
+                v = __builtin_elementwise_fma(a[dd + 1], (f4)ty.w[1], v);
+                v = __builtin_elementwise_fma(a[dd + 2], (f4)ty.w[2], v);
+                v = __builtin_elementwise_fma(a[dd + 3], (f4)ty.w[3], v);
+              }
+            }
+          }
+          Vb[r * (vstride / 4) + e] = v;
+        }
+      }
+    };
+
+    if (job != jfirst) __syncthreads();   // the previous job's store tile (in V) fully read
+    stage(0);
+    __syncthreads();
+    const int nslab = L * H;
+    for (int it = 0; it < nslab; ++it) {
+      if ((!STAG || !late) && it + 1 < nslab) {
+  #if SKP_MAPS_PRIO
+        __builtin_amdgcn_s_setprio(SKP_MAPS_PRIO);
+  #endif
+        stage(it + 1);
+  #if SKP_MAPS_PRIO
+        __builtin_amdgcn_s_setprio(0);
+  #endif
+      }
+      const int l = it / H, bh = b * H + (it - l * H);
+      const f4* V4 = reinterpret_cast<const f4*>(V + ((it & 1) * TY + ry) * vstride) + li;
+      const float4* tw = TW + (l & 1) * TX;
+      const int4* tiw = TI + (l & 1) * TX;
+      float2* st = cl.stats[l];
+      const int yr = y0 + ry;
+  #pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const int xl = (wid - ry * WPR) * PXW + 4 * g + row;   // pixel of this 16-lane row
+        const int xr = min(xl, np - 1);
+        const float4 w = tw[xr];
+        const int4 ti = tiw[xr];
+        f4 zc[QPL];
+        float m = kPadLogit;
+  #pragma unroll
+        for (int c = 0; c < QPL; ++c) {
+          const f4 a0 = V4[ti.x + 16 * c], a1 = V4[ti.y + 16 * c];
+          const f4 a2 = V4[ti.z + 16 * c], a3 = V4[ti.w + 16 * c];
+          f4 v = a0 * w.x;
+          v = __builtin_elementwise_fma(a1, (f4)w.y, v);
+          v = __builtin_elementwise_fma(a2, (f4)w.z, v);
+          v = __builtin_elementwise_fma(a3, (f4)w.w, v);
+          zc[c] = v;
+          m = __builtin_fmaxf(__builtin_fmaxf(m, v.x), v.y);
+          m = __builtin_fmaxf(__builtin_fmaxf(m, v.z), v.w);
+          if (QPL > 4 || (c & 1)) __builtin_amdgcn_sched_barrier(0);
+        }
+        m = row16_max(m);
+        const f4 mb = (f4)(-m * L2E);
+        f4 sv = (f4)0.0f;
+  #pragma unroll
+        for (int c = 0; c < QPL; ++c) {
+          f4 ex = __builtin_elementwise_fma(zc[c], (f4)L2E, mb);
+          ex.x = __builtin_amdgcn_exp2f(ex.x);
+          ex.y = __builtin_amdgcn_exp2f(ex.y);
+          ex.z = __builtin_amdgcn_exp2f(ex.z);
+          ex.w = __builtin_amdgcn_exp2f(ex.w);
+          zc[c] = ex;
+          sv += ex;
+        }
+        const float inv = __builtin_amdgcn_rcpf(row16_sum((sv.x + sv.y) + (sv.z + sv.w)));
+  #pragma unroll
+        for (int c = 0; c < QPL; ++c) acc[g][c] = __builtin_elementwise_fma(zc[c], (f4)inv, acc[g][c]);
+        if (st && li == 0 && xl < np && ry < ny) {
+          const f2v mi = {m, inv};
+          SKP_MAPS_ST(reinterpret_cast<f2v*>(st)[((size_t)bh * R + yr) * R + x0 + xl], mi);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (STAG && late && it + 1 < nslab) {
+  #if SKP_MAPS_PRIO
+        __builtin_amdgcn_s_setprio(SKP_MAPS_PRIO);
+  #endif
+        stage(it + 1);
+  #if SKP_MAPS_PRIO
+        __builtin_amdgcn_s_setprio(0);
+  #endif
+      }
+      __syncthreads();
+    }
+    // token-major store: tile row p = ry·TX + xl; round rd stages tokens [128 rd, 128 rd + 128)
+    constexpr int TS = 128 + 4;
+    constexpr int P = TY * TX;
+    float* tile = V;
+    float* ob = maps + (size_t)b * N * R * R + (size_t)y0 * R + x0;
+    const float rc = 1.0f / count;
+  #pragma unroll
+    for (int rd = 0; rd < (QPL + 1) / 2; ++rd) {
+      if (rd > 0) __syncthreads();
+  #pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const int p = ry * TX + (wid - ry * WPR) * PXW + 4 * g + row;
+  #pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const int c = 2 * rd + h2;
+          if (c < QPL) *reinterpret_cast<f4*>(tile + p * TS + 4 * (li + 16 * h2)) = acc[g][c] * rc;
+        }
+      }
+      __syncthreads();
+      const int nr = min(128, Np - 128 * rd) / 4;
+      for (int e = tid; e < P * nr; e += kT) {
+        const int p = e % P, jq = e / P;
+        const int r = p / TX, xl = p - r * TX;
+        if (xl >= np || r >= ny) continue;
+        const f4 v = *reinterpret_cast<const f4*>(tile + p * TS + 4 * jq);
+        const int n = 128 * rd + 4 * jq;
+        float* o = ob + (size_t)r * R + xl;
+        if (n < N) SKP_MAPS_ST(o[(size_t)n * R * R], v.x);
+        if (n + 1 < N) SKP_MAPS_ST(o[(size_t)(n + 1) * R * R], v.y);
+        if (n + 2 < N) SKP_MAPS_ST(o[(size_t)(n + 2) * R * R], v.z);
+        if (n + 3 < N) SKP_MAPS_ST(o[(size_t)(n + 3) * R * R], v.w);
       }
     }
   }
@@ -1392,6 +1597,64 @@ void launch_maps_w(int waves, const CapLayers& cl, int L, int B, int H, int N, i
   if (waves == 16) launch_maps<QPL, 16>(cl, L, B, H, N, R, vstride, lds, maps, st);
   else launch_maps<QPL, 8>(cl, L, B, H, N, R, vstride, lds, maps, st);
 }
+
+// tiled form (capture_maps_tile_kernel): one 16-wave workgroup per CU, TY-row × TX-pixel tiles
+constexpr int maps_tile_tx(int qpl, int ty) { return (16 / ty) * maps_pxw(qpl); }
+int maps_tile_vstride(const int* sizes, int L, int R, int qpl, int ty) {   // floats per V row buffer
+  const int TX = maps_tile_tx(qpl, ty), Np = 64 * qpl;
+  int ncmax = 1;
+  for (int l = 0; l < L; ++l) {
+    const int s = sizes[l];
+    ncmax = std::max(ncmax, std::min(s, (int)(((long long)TX * s + R - 1) / R) + 4));
+  }
+  const int tile = ty * TX * (128 + 4);   // the store tile fits in the 2 · TY row buffers
+  return (std::max(ncmax * Np, (tile + 2 * ty - 1) / (2 * ty)) + 3) & ~3;
+}
+size_t maps_tile_lds(int vstride, int qpl, int ty) {
+  return (16 * (size_t)maps_tile_tx(qpl, ty) + 2 * (size_t)ty * vstride) * sizeof(float);
+}
+
+// SKP_MAPS_TILE: rows per tile of the tiled kernel (2 or 4), 0 (default) = the one-row kernel
+int maps_tile_rows() {   // read per call (A/B tests switch it in-process)
+  const char* e = getenv("SKP_MAPS_TILE");
+  if (!e) return 0;
+  const int v = atoi(e);
+  return (v == 2 || v == 4) ? v : 0;
+}
+
+// SKP_MAPS_STAGGER=1: waves 8-15 stage after their pixels (A/B; default off)
+bool maps_tile_stagger() {
+  const char* e = getenv("SKP_MAPS_STAGGER");
+  return e && atoi(e) == 1;
+}
+
+template <int QPL, int TY>
+void launch_maps_tile(const CapLayers& cl, int L, int B, int H, int N, int R, int vstride, size_t lds, float* maps,
+                      hipStream_t st) {
+  constexpr int TX = maps_tile_tx(QPL, TY);
+  const int nchunks = (R + TX - 1) / TX;
+  const int total = B * ((R + TY - 1) / TY) * nchunks;
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    return std::max(8, n / 8 * 8);
+  }();
+  const int grid = std::min(8 * ((total + 7) / 8), ncu);   // persistent: one workgroup per CU, multiple of 8
+  (void)lds;   // static LDS (kTileLdsFloats); the caller checked lds <= its size
+  if (maps_tile_stagger())
+    hipLaunchKernelGGL((capture_maps_tile_kernel<QPL, TY, true>), dim3(grid), dim3(16 * WAVE), 0, st, cl, L, B, H, N, R,
+                       nchunks, vstride, (float)L * (float)H, maps);
+  else
+    hipLaunchKernelGGL((capture_maps_tile_kernel<QPL, TY, false>), dim3(grid), dim3(16 * WAVE), 0, st, cl, L, B, H, N,
+                       R, nchunks, vstride, (float)L * (float)H, maps);
+}
+template <int QPL>
+void launch_maps_tile_ty(int ty, const CapLayers& cl, int L, int B, int H, int N, int R, int vstride, size_t lds,
+                         float* maps, hipStream_t st) {
+  if (ty == 4) launch_maps_tile<QPL, 4>(cl, L, B, H, N, R, vstride, lds, maps, st);
+  else launch_maps_tile<QPL, 2>(cl, L, B, H, N, R, vstride, lds, maps, st);
+}
 }  // namespace
 
 extern "C" int skp_capture_maps_fwd(const float* const* z_low, const int* sizes, int L, int B, int H, int N, int R,
@@ -1409,15 +1672,27 @@ extern "C" int skp_capture_maps_fwd(const float* const* z_low, const int* sizes,
     SKP_CHECK_ARG(sizes[l] > 0 && sizes[l] <= R, "layer size must be in [1, R]");
     cl.z[l] = z_low[l];
     cl.s[l] = sizes[l];
+    cl.sc[l] = (float)sizes[l] / (float)R;
     cl.stats[l] = stats ? reinterpret_cast<float2*>(stats[l]) : nullptr;
     aligned = aligned && ((reinterpret_cast<uintptr_t>(z_low[l]) & 15) == 0);
   }
   SKP_CHECK_ARG(aligned || (N % 4) != 0, "z_low pointers must be 16-B aligned");
+  hipStream_t st = as_stream(stream);
+  const int ty = maps_tile_rows();
+  if (ty > 0 && (N % 4) == 0 && qpl >= 4 && qpl <= 8) {
+    const int vstride = maps_tile_vstride(sizes, L, R, qpl, ty);
+    const size_t lds = maps_tile_lds(vstride, qpl, ty);
+    if (lds <= sizeof(float) * kTileLdsFloats) {
+      if (qpl == 4) launch_maps_tile_ty<4>(ty, cl, L, B, H, N, R, vstride, lds, maps, st);
+      else launch_maps_tile_ty<8>(ty, cl, L, B, H, N, R, vstride, lds, maps, st);
+      SKP_LAUNCH_CHECK();
+      return SKP_OK;
+    }
+  }
   const int waves = maps_waves();
   const int vstride = maps_vstride(sizes, L, R, qpl, waves);
   const size_t lds = maps_lds(vstride, qpl, waves);
   SKP_CHECK_ARG(lds <= 160 * 1024, "s*N too large for LDS");
-  hipStream_t st = as_stream(stream);
   switch (qpl) {
     case 1: launch_maps_w<1>(waves, cl, L, B, H, N, R, vstride, lds, maps, st); break;
     case 2: launch_maps_w<2>(waves, cl, L, B, H, N, R, vstride, lds, maps, st); break;

@@ -143,18 +143,21 @@ struct Taps4 {
   int lo;       // first tap before clamping (floor(src) - 1, in [-2, n_in - 2])
 };
 
-__device__ __forceinline__ float cubic1(float x) {  // |x| <= 1
+// The contractions are explicit (the ones the compiler had chosen in every kernel through r04), so
+// every kernel — and every inlining context, whatever the SLP vectorizer does — computes the same
+// weights bit for bit.
+__device__ __forceinline__ float cubic1(float x) {  // |x| <= 1: ((A + 2)·x − (A + 3))·x·x + 1
   const float A = -0.75f;
-  return ((A + 2.0f) * x - (A + 3.0f)) * x * x + 1.0f;
+  return __builtin_fmaf(__builtin_fmaf(A + 2.0f, x, -(A + 3.0f)) * x, x, 1.0f);
 }
-__device__ __forceinline__ float cubic2(float x) {  // 1 < |x| < 2
+__device__ __forceinline__ float cubic2(float x) {  // 1 < |x| < 2: ((A·x − 5A)·x + 8A)·x − 4A
   const float A = -0.75f;
-  return ((A * x - 5.0f * A) * x + 8.0f * A) * x - 4.0f * A;
+  return __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(A, x, -5.0f * A), x, 8.0f * A), x, -4.0f * A);
 }
 
-__device__ __forceinline__ Taps4 bicubic_taps(int dst, int n_in, int n_out) {
-  const float scale = (float)n_in / (float)n_out;
-  const float src = scale * ((float)dst + 0.5f) - 0.5f;
+// scale = (float)n_in / (float)n_out, e.g. precomputed on the host (the same IEEE quotient)
+__device__ __forceinline__ Taps4 bicubic_taps_s(int dst, int n_in, float scale) {
+  const float src = __builtin_fmaf(scale, (float)dst + 0.5f, -0.5f);
   const float f = floorf(src);
   const float t = src - f;
   const int i0 = (int)f;
@@ -167,6 +170,9 @@ __device__ __forceinline__ Taps4 bicubic_taps(int dst, int n_in, int n_out) {
   for (int k = 0; k < 4; ++k) r.i[k] = min(max(i0 - 1 + k, 0), n_in - 1);
   r.lo = i0 - 1;
   return r;
+}
+__device__ __forceinline__ Taps4 bicubic_taps(int dst, int n_in, int n_out) {
+  return bicubic_taps_s(dst, n_in, (float)n_in / (float)n_out);
 }
 
 // torch bilinear, align_corners=False: src = max((dst+0.5)·in/out − 0.5, 0), upper tap clamped.
