@@ -367,7 +367,7 @@ __device__ __forceinline__ void sel_dense_body(const SelLayers& sl, int BH, int 
   const float* zl = sl.z[l] + (size_t)bh * S * S * N;
   const float2* pixl = sl.pix[l] + (size_t)bh * R * R;
   float* dzl = sl.dz[l] + (size_t)bh * S * S * N;
-  const float* esl = sl.es[l] + (size_t)bh * K * S * S;
+  const float* esl = sl.es[l] ? sl.es[l] + (size_t)bh * K * S * S : nullptr;
   // the selected rows this lane's token pair (n0, n0 + 1) carries (bit k: tok_k; duplicates add)
   unsigned mx = 0u, my = 0u;
   for (int k = 0; k < K; ++k) {
@@ -445,8 +445,10 @@ __device__ __forceinline__ void sel_dense_body(const SelLayers& sl, int BH, int 
         for (int w2 = wlo; w2 <= whi; ++w2) s += M[(w2 * NC + j + 2 - w2 * CS) * LW + lane];
       }
       if (n < N) {
-        for (unsigned m = mx; m; m &= m - 1) s.x += esl[((size_t)__builtin_ctz(m) * S + r) * S + j];   // k order
-        for (unsigned m = my; m; m &= m - 1) s.y += esl[((size_t)__builtin_ctz(m) * S + r) * S + j];
+        if (esl) {   // es added here (single-stream order); else by sel_es_add_kernel after this launch
+          for (unsigned m = mx; m; m &= m - 1) s.x += esl[((size_t)__builtin_ctz(m) * S + r) * S + j];   // k order
+          for (unsigned m = my; m; m &= m - 1) s.y += esl[((size_t)__builtin_ctz(m) * S + r) * S + j];
+        }
         *reinterpret_cast<f2*>(dzl + ((size_t)r * S + j) * N + n) = s;
       }
     }
@@ -632,6 +634,56 @@ bool dense_supported(int R, int S) {
   return false;
 }
 
+// The sparse part's final pass (r05: sel_adjw runs on a second stream beside sel_dense, so sel_dense
+// stores the dense part alone and the selected tokens get their es here): one thread per (layer,
+// head, low-res pixel q) adds es[l][bh][k][q] to dz[l][bh][q][tok_k] in k order — the order sel_dense's
+// emit used, so the result is bit-identical to adding them there.
+struct SelEs {
+  float* dz[SKP_MAX_LAYERS];
+  const float* es[SKP_MAX_LAYERS];
+  int s[SKP_MAX_LAYERS];
+  long long qoff[SKP_MAX_LAYERS + 1];   // prefix of BH·s² over layers
+};
+__global__ void sel_es_add_kernel(SelEs t, int L, int BH, int H, int N, int K, const long long* __restrict__ tok) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= t.qoff[L]) return;
+  int l = 0;
+  while (l + 1 < L && e >= t.qoff[l + 1]) ++l;
+  const long long le = e - t.qoff[l];
+  const int SS = t.s[l] * t.s[l];
+  const int bh = (int)(le / SS), q = (int)(le % SS);
+  const int b = bh / H;
+  float* dz = t.dz[l] + ((size_t)bh * SS + q) * N;
+  const float* es = t.es[l] + (size_t)bh * K * SS;   // [bh][k][S][S] at the layer's s (sel_adjw's layout)
+  for (int k = 0; k < K; ++k) {
+    const long long tk = tok[(size_t)b * K + k];
+    if (tk >= 0 && tk < N) dz[tk] += es[(size_t)k * SS + q];
+  }
+}
+
+// per-thread auxiliary stream + fork/join events of the current device (created once per thread and
+// device; a caller's stream is never shared across threads through them)
+struct AuxStream {
+  int dev = -1;
+  hipStream_t st = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+AuxStream* aux_stream() {
+  static thread_local AuxStream a[16];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
+  AuxStream& x = a[dev];
+  if (x.dev != dev) {
+    int least = 0, greatest = 0;   // the auxiliary work yields the CUs to the caller's stream
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = 0;
+    if (hipStreamCreateWithPriority(&x.st, hipStreamNonBlocking, least) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&x.join, hipEventDisableTiming) != hipSuccess) return nullptr;
+    x.dev = dev;
+  }
+  return &x;
+}
+
 // dense gradient from the sparse one (fallback): g[b][tok_k][p] = Σ_k gsel[b][k][p] (k order)
 __global__ void sel_scatter_kernel(const long long* __restrict__ tok, const float* __restrict__ gsel, int B, int K,
                                    int N, long long RR, float* __restrict__ g) {
@@ -735,6 +787,23 @@ extern "C" int skp_capture_maps_bwd_sel(const float* const* z_low, const int* si
   hipLaunchKernelGGL(sel_dot_kernel, dim3((unsigned)(L * BH * R)), dim3(std::min(R, 256)),
                      (size_t)smax * K * sizeof(float), st, t, zsel, BH, R, H, K, sel_tok, gsel, gscale, E, pix);
   SKP_LAUNCH_CHECK();
+  // SKP_SEL_FORK=1: the sparse part es = bicubicᵀ(E) (sel_adjw / sel_adj), which needs only E, on a
+  // low-priority auxiliary stream concurrently with sel_dense, whose emits then leave es out;
+  // sel_es_add_kernel adds it once both are done (bit-identical).  Measured SLOWER at the bench shape
+  // (mapssel8 1223-1237 vs 1145-1161 us, profiles/r05g_sel_fork_ab.txt: the small blocks take CU
+  // slots from sel_dense's last round), so the default (0) keeps one stream, es added in the emits.
+  const bool fork_env = [] {   // read per call (the A/B test switches it in-process)
+    const char* e = getenv("SKP_SEL_FORK");
+    return e && atoi(e) == 1;
+  }();
+  AuxStream* aux = fork_env ? aux_stream() : nullptr;
+  hipStream_t adj_st = st;
+  if (aux) {   // E is complete here; the auxiliary stream's sel_adjw is enqueued after sel_dense
+    SKP_CHECK_ARG(hipEventRecord(aux->fork, st) == hipSuccess && hipStreamWaitEvent(aux->st, aux->fork, 0) == hipSuccess,
+                  "fork event failed");
+    adj_st = aux->st;
+  }
+  auto launch_adj = [&]() -> int {
   // the rolling-window horizontal pass (sel_adjw_kernel: 78 vs 104 us at the bench shape,
   // profiles/r04aa_sel_adj_ab.txt); SKP_SEL_ADJ=0: sel_adj's per-output banded dot products (A/B)
   static const bool adj_win = [] {
@@ -743,14 +812,39 @@ extern "C" int skp_capture_maps_bwd_sel(const float* const* z_low, const int* si
   }();
   if (adj_win && R <= 256 && R % 16 == 0) {
     hipLaunchKernelGGL(sel_adjw_kernel, dim3((unsigned)(L * BH * K)), dim3(R),
-                       (size_t)(smax * (R + 1) + R * smax + 5 * R) * sizeof(float), st, t, E, BH * K, smax, R, es);
+                       (size_t)(smax * (R + 1) + R * smax + 5 * R) * sizeof(float), adj_st, t, E, BH * K, smax, R, es);
   } else {
     const int tr = sel_adj_tile(R);
     hipLaunchKernelGGL(sel_adj_kernel, dim3((unsigned)(L * BH * K)), dim3(256),
-                       (size_t)(smax * (R + 1) + R * smax + tr * (R + 1)) * sizeof(float), st, t, E, BH * K, smax, R,
+                       (size_t)(smax * (R + 1) + R * smax + tr * (R + 1)) * sizeof(float), adj_st, t, E, BH * K, smax, R,
                        tr, es);
   }
   SKP_LAUNCH_CHECK();
+  if (aux) SKP_CHECK_ARG(hipEventRecord(aux->join, aux->st) == hipSuccess, "join event failed");
+  return SKP_OK;
+  };
+  if (!aux) {   // single stream: es before sel_dense, which adds it in its emits
+    const int rc = launch_adj();
+    if (rc != SKP_OK) return rc;
+  }
+  auto finish = [&]() -> int {   // launch the auxiliary sel_adjw, join it, add es at the selected tokens
+    if (!aux) return SKP_OK;
+    const int rc = launch_adj();
+    if (rc != SKP_OK) return rc;
+    SKP_CHECK_ARG(hipStreamWaitEvent(st, aux->join, 0) == hipSuccess, "join wait failed");
+    SelEs te{};
+    te.qoff[0] = 0;
+    for (int l = 0; l < L; ++l) {
+      te.dz[l] = dz_low[l];
+      te.es[l] = es + (size_t)l * BH * K * smax * smax;
+      te.s[l] = sizes[l];
+      te.qoff[l + 1] = te.qoff[l] + (long long)BH * sizes[l] * sizes[l];
+    }
+    hipLaunchKernelGGL(sel_es_add_kernel, dim3((unsigned)((te.qoff[L] + 255) / 256)), dim3(256), 0, st, te, L, BH, H, N,
+                       K, sel_tok);
+    SKP_LAUNCH_CHECK();
+    return SKP_OK;
+  };
   // the dense part: layers of equal s share a class (up to 4 per launch); two classes that have
   // a paired kernel (SD-1.5: s = 16 and 32 at R = 128) run as one launch
   SelLayers cls[SKP_MAX_LAYERS];
@@ -764,7 +858,7 @@ extern "C" int skp_capture_maps_bwd_sel(const float* const* z_low, const int* si
       if (done[m] || sizes[m] != sizes[l]) continue;
       sl.z[nl] = z_low[m];
       sl.pix[nl] = pix + (size_t)m * BH * RR;
-      sl.es[nl] = es + (size_t)m * BH * K * smax * smax;
+      sl.es[nl] = aux ? nullptr : es + (size_t)m * BH * K * smax * smax;
       sl.dz[nl] = dz_low[m];
       done[m] = true;
       ++nl;
@@ -777,7 +871,7 @@ extern "C" int skp_capture_maps_bwd_sel(const float* const* z_low, const int* si
   if (ncls == 2 && dense_pair_launch(R, cls_s[0], cls[0], cls_n[0], cls_s[1], cls[1], cls_n[1], BH, H, N, K, sel_tok,
                                      st)) {
     SKP_LAUNCH_CHECK();
-    return SKP_OK;
+    return finish();
   }
   for (int c = 0; c < ncls; ++c) {
     if (!dense_launch(R, cls_s[c], cls[c], cls_n[c], BH, H, N, K, sel_tok, st)) {
@@ -785,5 +879,5 @@ extern "C" int skp_capture_maps_bwd_sel(const float* const* z_low, const int* si
     }
     SKP_LAUNCH_CHECK();
   }
-  return SKP_OK;
+  return finish();
 }

@@ -164,3 +164,24 @@ def test_select_more_rows_than_the_sparse_kernel_takes():
         assert torch.isfinite(a.grad).all()
         err = (a.grad - b.grad).abs().max().item() / b.grad.abs().max().item()
         assert err < 2e-5, err
+
+
+@pytest.mark.parametrize("B,H,sizes,R,Nn,K,dup,ragged", [
+    (8, 8, (16, 16, 16, 32), 128, 500, 10, False, False),  # the bench shape (the paired sel_dense launch)
+    (2, 4, (4, 8), 32, 64, 5, True, True),                # duplicated token, ragged rows
+    (2, 2, (4, 8, 16), 64, 64, 32, True, False),          # K = 32, three sizes
+])
+def test_forked_sparse_part_equals_single_stream(monkeypatch, B, H, sizes, R, Nn, K, dup, ragged):
+    """SKP_SEL_FORK=1 (A/B option, measured slower: sel_adjw on a second stream beside sel_dense, the selected tokens'
+    es added by a final pass in k order) is bit-identical to SKP_SEL_FORK=0 (default: es added inside
+    sel_dense's emit, one stream): the same additions in the same order."""
+    from stablekeypoints_amd import ops
+    zs, tok, gsel = _case(77 + K, B, H, sizes, R, Nn, K, dup, ragged)
+    zt = [T(z) for z in zs]
+    _, stats = _fwd(zt, list(sizes), B, H, R)
+    out = {}
+    for fork in ("0", "1"):
+        monkeypatch.setenv("SKP_SEL_FORK", fork)
+        out[fork] = _sel_abi(zt, list(sizes), B, H, R, T(tok), T(gsel), 0.03125, stats)
+    for a, b in zip(out["0"], out["1"]):
+        assert torch.equal(a, b), (a - b).abs().max().item()
