@@ -144,6 +144,12 @@ int skp_topk_gaussian_batch(const float* maps, int nb, int T, int h, int w, int 
                             float epsilon, int num_subjects, long long* out, double* kl, void* workspace,
                             void* stream);
 
+/* The ranking step of find_top_k_gaussian / entropy_sort (`torch.argsort(keys)[:top_k]`,
+ * ptp_utils.py:110-112 and :185) for nb segments of T fp64 keys: ascending, NaN last, ties by
+ * index; keys (nb, T), out (nb, top_k).  skp_topk_gaussian_batch with top_k = 0 and this call
+ * together are skp_topk_gaussian_batch with top_k > 0.                                        */
+int skp_topk_keys(const double* keys, int nb, int T, int top_k, long long* out, void* stream);
+
 /* ptp_utils.entropy_sort (ptp_utils.py:165-187): ascending softmax entropy.     */
 int skp_entropy_sort(const float* maps, int T, int h, int w, int top_k, long long* out, double* ent,
                      void* workspace, void* stream);

@@ -37,6 +37,7 @@ _SIGS = {
     "skp_topk_gaussian": [_p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_float, _c_int, _p, _p, _p, _p],
     "skp_topk_gaussian_batch": [_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _c_float, _c_int, _p, _p, _p,
                                 _p],
+    "skp_topk_keys": [_p, _c_int, _c_int, _c_int, _p, _p],
     "skp_entropy_sort": [_p, _c_int, _c_int, _c_int, _c_int, _p, _p, _p, _p],
     "skp_fps": [_p, _c_int, _c_int, _c_int, _p, _c_int, _c_int, _p, _p, _p, _p],
     "skp_fps_batch": [_p, _c_int, _c_int, _c_int, _c_int, _p, _c_int, _c_int, _p, _p, _p, _p],

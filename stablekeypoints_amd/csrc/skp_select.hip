@@ -7,6 +7,8 @@
 // Every map row is reduced by one 256-thread workgroup (4 waves) with shuffle
 // reductions; index outputs follow torch.argmax (first occurrence, NaN is max) and the
 // reference's strict '>' first-wins loops, so they are bit-exact on identical maps.
+#include <algorithm>
+
 #include "skp_common.h"
 
 using namespace skp;
@@ -507,6 +509,34 @@ __global__ __launch_bounds__(1024) void sort_topk_kernel(const double* __restric
   for (int i = threadIdx.x; i < top_k; i += blockDim.x) out[i] = id[i];
 }
 
+// r05: the first top_k of that order by ranking instead of sorting: key i's position in the ascending
+// order is rank_i = #{j : key_less(k_j, j, k_i, i)} (a strict total order: NaN last, ties by index),
+// so out[rank_i] = i for rank_i < top_k — the sort's first top_k exactly, with one barrier instead of
+// the bitonic network's log²(n) (at T = 500: 45 barrier-separated stages of a 1024-thread block).
+// blockIdx.x = segment; T ≤ 8192 keys staged in LDS (as doubles).
+__global__ __launch_bounds__(1024) void rank_topk_kernel(const double* __restrict__ keys, int T, int top_k,
+                                                         long long* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* k = reinterpret_cast<double*>(smem);
+  keys += (size_t)blockIdx.x * T;
+  out += (size_t)blockIdx.x * top_k;
+  for (int i = threadIdx.x; i < T; i += blockDim.x) k[i] = keys[i];
+  __syncthreads();
+  for (int i = threadIdx.x; i < T; i += blockDim.x) {
+    const double ki = k[i];
+    int r = 0;
+    if (isnan(ki)) {   // after every non-NaN key and every NaN of a lower index
+      for (int j = 0; j < T; ++j) r += (!isnan(k[j]) || j < i) ? 1 : 0;
+    } else {
+      for (int j = 0; j < T; ++j) {
+        const double kj = k[j];   // (NaN compares false: never before ki)
+        r += (kj < ki || (kj == ki && j < i)) ? 1 : 0;
+      }
+    }
+    if (r < top_k) out[r] = i;
+  }
+}
+
 // Furthest-point sampling over candidate positions (ptp_utils.py:115-159), one wave.
 __global__ __launch_bounds__(64) void fps_kernel(const float* __restrict__ cpos, const long long* __restrict__ cand,
                                                  int C, int h, int top_k, long long* __restrict__ out,
@@ -712,11 +742,21 @@ extern "C" int skp_gaussian_target(const float* pos, int num, int T, int size, f
 }
 
 static int launch_sort(const double* keys, int T, int top_k, long long* out, hipStream_t st, int nb = 1) {
-  int n2 = 1;
-  while (n2 < T) n2 <<= 1;
-  SKP_CHECK_ARG(n2 <= 8192, "T > 8192 tokens is not supported by the selection sort");
-  const size_t lds = (size_t)n2 * (sizeof(double) + sizeof(int));
-  hipLaunchKernelGGL(sort_topk_kernel, dim3(nb), dim3(1024), lds, st, keys, T, n2, top_k, out);
+  SKP_CHECK_ARG(T <= 8192, "T > 8192 tokens is not supported by the selection sort");
+  // SKP_TOPK_SORT=1: the r04 bitonic sort (A/B); default: the ranking kernel (same indices)
+  static const bool bitonic = [] {
+    const char* e = getenv("SKP_TOPK_SORT");
+    return e && atoi(e) == 1;
+  }();
+  if (bitonic) {
+    int n2 = 1;
+    while (n2 < T) n2 <<= 1;
+    const size_t lds = (size_t)n2 * (sizeof(double) + sizeof(int));
+    hipLaunchKernelGGL(sort_topk_kernel, dim3(nb), dim3(1024), lds, st, keys, T, n2, top_k, out);
+  } else {
+    const int threads = std::min(1024, (T + 63) / 64 * 64);
+    hipLaunchKernelGGL(rank_topk_kernel, dim3(nb), dim3(threads), (size_t)T * sizeof(double), st, keys, T, top_k, out);
+  }
   SKP_LAUNCH_CHECK();
   return SKP_OK;
 }
@@ -772,6 +812,14 @@ extern "C" int skp_topk_gaussian_batch(const float* maps, int nb, int T, int h, 
   SKP_LAUNCH_CHECK();
   if (top_k == 0) return SKP_OK;
   return launch_sort(keys, T, top_k, out, st, nb);
+}
+
+extern "C" int skp_topk_keys(const double* keys, int nb, int T, int top_k, long long* out, void* stream) {
+  SKP_CHECK_ARG(keys && out, "null pointer");
+  SKP_CHECK_ARG(nb > 0 && T > 0, "non-positive shape");
+  SKP_CHECK_ARG(top_k >= 0 && top_k <= T, "top_k out of range");
+  if (top_k == 0) return SKP_OK;
+  return launch_sort(keys, T, top_k, out, as_stream(stream), nb);
 }
 
 extern "C" int skp_topk_gaussian(const float* maps, int T, int h, int w, int top_k, float sigma, float epsilon,

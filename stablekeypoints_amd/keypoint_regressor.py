@@ -69,9 +69,9 @@ def find_best_indices(ldm, context, num_steps=100, device="cuda", noise_level=-1
         image), on the device via pinned memory without waiting for the queued GPU work."""
         groups = [_next(state)["img"] for _ in range(c)]
         mine = torch.cat([g[rank:rank + 1] if world > 1 else g for g in groups])
-        if torch.device(device).type == "cuda":
+        if torch.device(device).type == "cuda" and mine.device.type == "cpu":
             return mine.pin_memory().to(device, non_blocking=True)
-        return mine.to(device)
+        return mine.to(device)   # a dataset that yields device tensors (or a CPU run)
 
     done = 0
     nxt = load(min(chunk, steps)) if steps > 0 else None
@@ -128,19 +128,22 @@ def find_best_indices(ldm, context, num_steps=100, device="cuda", noise_level=-1
 def _select_batched(strategy, top_k, n_cand):
     """The one-launch-per-stage selection applies: a batched candidate ranking exists for the
     strategy and the FPS kernel's bounds hold (top_k ≥ 2 picks from ≥ 2 candidates)."""
-    return strategy in ("gaussian", "consistent") and top_k >= 2 and n_cand >= 2
+    return strategy in ("gaussian", "entropy", "consistent") and top_k >= 2 and n_cand >= 2
 
 
 def _select_stack(stack, top_k, n_cand, strategy, sigma, num_subjects):
     """The reference's per-image candidates + furthest-point sampling (keypoint_regressor.py:95-112)
-    for every image of a (B, N, S, S) stack: one skp_topk_gaussian_batch (or the consistent
-    arange) and one skp_fps_batch launch.  Returns the device tensors ((B, top_k) picks, (B,)
+    for every image of a (B, N, S, S) stack: one skp_topk_gaussian_batch + skp_topk_keys (the entropy
+    strategy: the entropy kernel over all rows + skp_topk_keys; consistent: an arange) and one
+    skp_fps_batch launch.  Returns the device tensors ((B, top_k) picks, (B,)
     counts): image b's picks are the first counts[b] (fewer when its FPS ran out of candidates, as
     the reference's list, ptp_utils.py:156-157)."""
     from . import ops
     B, N = stack.shape[:2]
     if strategy == "gaussian":
         cand = ops.find_top_k_gaussian_batch(stack, n_cand, sigma=sigma, num_subjects=num_subjects)
+    elif strategy == "entropy":   # keypoint_regressor.py:104-105, every image in two launches
+        cand = ops.entropy_sort_batch(stack, n_cand)
     else:
         cand = torch.arange(n_cand, device=stack.device).expand(B, n_cand)
     return ops.furthest_point_sampling_batch(stack, top_k, cand)

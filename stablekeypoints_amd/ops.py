@@ -699,10 +699,14 @@ def find_top_k_gaussian_batch(maps, top_k, sigma=3, epsilon=1e-5, num_subjects=1
     top_k = min(int(top_k), T)
     out = torch.empty(nb, top_k, device=maps.device, dtype=torch.int64)
     kl = torch.empty(nb, T, device=maps.device, dtype=torch.float64)
-    # algorithmic bytes: every map read once (the KL ranking; the sort's 8·T B per image are noise)
-    with _timed("skp_topk_gaussian_batch", maps.numel() * 4 + nb * T * 16):
-        call("skp_topk_gaussian_batch", ptr(maps), nb, T, h, w, int(top_k), float(sigma), float(epsilon),
+    # the KL ranking (algorithmic bytes: every map read once, the keys written) and the top-k of the
+    # keys as two launches, timed apart in the bench's kernels block
+    with _timed("skp_topk_gaussian_batch", maps.numel() * 4 + nb * T * 8):
+        call("skp_topk_gaussian_batch", ptr(maps), nb, T, h, w, 0, float(sigma), float(epsilon),
              int(num_subjects), ptr(out), ptr(kl), ptr(kl), stream(maps.device))
+    if top_k > 0:
+        with _timed("skp_topk_keys", nb * T * 8 + nb * top_k * 8):
+            call("skp_topk_keys", ptr(kl), nb, T, int(top_k), ptr(out), stream(maps.device))
     return out
 
 
@@ -721,6 +725,22 @@ def furthest_point_sampling_batch(maps, top_k, candidates):
     call("skp_fps_batch", ptr(maps), nb, T, h, w, ptr(cand), cand.shape[1], int(top_k), ptr(out), ptr(n_out),
          ptr(ws), stream(maps.device))
     return out, n_out
+
+
+def entropy_sort_batch(maps, top_k):
+    """entropy_sort of every image of a (nb, T, h, w) stack: the entropies of all nb·T rows in one
+    launch (skp_entropy_sort's kernel, no ranking), then the per-image ascending top_k of them in
+    one skp_topk_keys launch.  (nb, top_k) int64, row b = entropy_sort(maps[b], top_k)."""
+    _lib.require_device(maps)
+    maps = _c(maps)
+    nb, T, h, w = maps.shape
+    top_k = min(int(top_k), T)
+    out = torch.empty(nb, top_k, device=maps.device, dtype=torch.int64)
+    ent = torch.empty(nb, T, device=maps.device, dtype=torch.float64)
+    call("skp_entropy_sort", ptr(maps), nb * T, h, w, 0, ptr(out), ptr(ent), ptr(ent), stream(maps.device))
+    if top_k > 0:
+        call("skp_topk_keys", ptr(ent), nb, T, int(top_k), ptr(out), stream(maps.device))
+    return out
 
 
 def entropy_sort(maps, top_k, return_entropy=False):

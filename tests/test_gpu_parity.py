@@ -229,6 +229,45 @@ def test_selection_batched_equals_per_image(num_subjects):
         assert np.array_equal(N(sel[0]), g["fps10"])
 
 
+@pytest.mark.parametrize("nb,Tn,top_k", [(4, 500, 25), (1, 1, 1), (2, 8192, 8192), (3, 777, 100), (2, 64, 64)])
+def test_topk_keys_rank_kernel_vs_stable_argsort(nb, Tn, top_k):
+    """skp_topk_keys (the ranking kernel: out[rank_i] = i) against numpy's stable ascending argsort
+    — NaN last, ties by index, as the r04 bitonic sort (key_less) — on keys with many exact ties,
+    NaNs and ±inf: bit-exact indices (torch.argsort(keys)[:k], ptp_utils.py:110-112, 185)."""
+    import ctypes
+    from stablekeypoints_amd._lib import call, ptr, stream
+    rng = np.random.default_rng(Tn + top_k)
+    keys = np.round(rng.standard_normal((nb, Tn)) * 4) / 4   # coarse: many exact ties
+    keys[:, ::17] = np.nan
+    keys[:, 5::23] = np.inf
+    keys[:, 7::29] = -np.inf
+    out = torch.full((nb, top_k), -7, dtype=torch.int64, device=DEV)
+    call("skp_topk_keys", ptr(T(keys)), nb, Tn, top_k, ptr(out), stream(DEV))
+    torch.cuda.synchronize()
+    ref = np.argsort(keys, axis=1, kind="stable")[:, :top_k]
+    assert np.array_equal(N(out), ref)
+
+
+def test_entropy_sort_batch_equals_per_image():
+    """ops.entropy_sort_batch (the entropies of all images' rows in one launch, the per-image
+    top-k in one skp_topk_keys launch: the batched `entropy` strategy of find_best_indices,
+    keypoint_regressor.py:104-105) equals entropy_sort image by image; image 0 is the golden's."""
+    from stablekeypoints_amd import ops
+    g = load_golden("select")
+    maps = np.stack([recipes.attention_like_maps(31, 500, 128) * 100.0] +
+                    [recipes.attention_like_maps(80 + i, 500, 128) * 100.0 for i in range(2)]).astype(np.float32)
+    got = ops.entropy_sort_batch(T(maps), 25)
+    for i in range(3):
+        assert torch.equal(got[i], ops.entropy_sort(T(maps[i]), 25))
+    assert np.array_equal(N(got[0]), g["entropy25_sharp"])
+    # find_best_indices' batched selection with the entropy strategy: candidates + FPS per image
+    from stablekeypoints_amd import keypoint_regressor as kr
+    sel, n = kr._select_stack(T(maps), 10, 25, "entropy", 2.0, 1)
+    for i in range(3):
+        one, k = ops.furthest_point_sampling(T(maps[i]), 10, ops.entropy_sort(T(maps[i]), 25))
+        assert int(n[i]) == int(k) and torch.equal(sel[i, :int(k)], one[:int(k)])
+
+
 @pytest.mark.parametrize("num_subjects", [1, 2])
 def test_losses_batched_equal_per_image(num_subjects):
     """ops.sharpening_loss_batch / equivariance_loss_batch (one launch per direction for the pass's
