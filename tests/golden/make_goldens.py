@@ -666,6 +666,14 @@ def gen_entropy_ref():
     np.savez_compressed(os.path.join(HERE, "entropy_ref.npz"), entropy_f32=_np(rec[0]), entropy25=_np(order))
 
 
+def gen_sdxl_store():
+    """The reference's SDXL-era AttentionStore (sdxl_monkey_patch.py:8-86, plain torch) driven by
+    recipes.sdxl_store_scenario: returned tensors, counters, per-place stores, averages."""
+    from unsupervised_keypoints import sdxl_monkey_patch as sm
+    assert os.path.abspath(sm.__file__).startswith(REF), sm.__file__
+    np.savez_compressed(os.path.join(HERE, "sdxl_store.npz"), **recipes.sdxl_store_scenario(sm.AttentionStore))
+
+
 def gen_interp():
     """Torch interpolation/warp numerics the kernels restate."""
     import torch.nn.functional as F
@@ -686,7 +694,7 @@ if __name__ == "__main__":
     torch.set_num_threads(8)
     which = sys.argv[1:] or ["capture_small", "capture_sd15", "argmax", "gaussian", "select", "losses",
                              "step_tiny", "interp", "eval_tiny", "best_indices_tiny", "regressor", "celeba_reader", "evaluate_tiny",
-                             "cub_reader", "theta_inv", "entropy_ref"]
+                             "cub_reader", "theta_inv", "entropy_ref", "sdxl_store"]
     for w in which:
         print("generating", w, flush=True)
         globals()["gen_" + w]()

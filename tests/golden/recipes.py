@@ -165,3 +165,53 @@ def write_mini_cub(root, seed=0):
             sfm[j]["scale"], sfm[j]["trans"], sfm[j]["rot"] = sfms[k]
         sio.savemat(os.path.join(cache, "data", f"{split}_cub_cleaned.mat"), {"images": imgs})
         sio.savemat(os.path.join(cache, "sfm", f"anno_{split}.mat"), {"sfm_anno": sfm})
+
+
+# The SDXL store scenario (sdxl_monkey_patch.py:8-86): a sequence of attention-probability calls
+# driven through an ``AttentionStore`` class (the reference's when the golden is made, this
+# package's in the test), five layers per diffusion step, three steps, then a fourth step with a
+# subclass that marks the first two layers unconditional.  Returns the numpy record the golden
+# holds.  (shape, is_cross, place): 1024 pixels is kept (the 32² boundary), 1025 is not.
+SDXL_STORE_CALLS = [((4, 1024, 7), True, "down"), ((4, 1025, 7), True, "up"), ((4, 64, 64), False, "mid"),
+                    ((4, 256, 7), True, "up"), ((2, 16, 16), False, "down")]
+
+
+def sdxl_store_scenario(store_cls):
+    import torch
+    out = {}
+
+    def drive(ctl, steps, tag):
+        for st in range(steps):
+            for ci, (shape, is_cross, place) in enumerate(SDXL_STORE_CALLS):
+                g = torch.Generator().manual_seed(1000 * st + ci + (7 if tag == "uncond" else 0))
+                attn = torch.rand(shape, generator=g).softmax(dim=-1)
+                ret = ctl(attn, is_cross, place)
+                assert ret is attn
+                if shape[1] <= 256:
+                    out[f"{tag}_ret_{st}_{ci}"] = ret.numpy().copy()
+            out[f"{tag}_counters_{st}"] = np.array([ctl.cur_step, ctl.cur_att_layer])
+        for key, maps in ctl.attention_store.items():
+            out[f"{tag}_nstore_{key}"] = np.array(len(maps))
+            for i, m in enumerate(maps):
+                out[f"{tag}_store_{key}_{i}"] = m.numpy().copy()
+        for key, maps in ctl.get_average_attention().items():
+            for i, m in enumerate(maps):
+                out[f"{tag}_avg_{key}_{i}"] = m.numpy().copy()
+        out[f"{tag}_keys"] = np.array(list(ctl.get_empty_store().keys()))
+
+    ctl = store_cls()
+    ctl.num_att_layers = len(SDXL_STORE_CALLS)
+    drive(ctl, 3, "plain")
+    ctl.reset()
+    out["plain_after_reset"] = np.array([ctl.cur_step, ctl.cur_att_layer, len(ctl.attention_store),
+                                         sum(len(v) for v in ctl.step_store.values())])
+
+    class Uncond(store_cls):
+        @property
+        def num_uncond_att_layers(self):
+            return 2
+
+    ctl = Uncond()
+    ctl.num_att_layers = len(SDXL_STORE_CALLS) - 2
+    drive(ctl, 2, "uncond")
+    return out

@@ -58,3 +58,24 @@ def test_attention_store_maps_need_logits():
         assert "logits" in str(e)
     else:
         raise AssertionError("maps_per_image on stored attention must raise")
+
+
+def test_sdxl_store_bit_exact_vs_reference_fixture():
+    """The SDXL-era store API (sdxl_monkey_patch.py:8-86) — per-place keys, the 32² pixel filter,
+    the conditional half attn[h // 2:], the layer counter / between_steps accumulation (in place,
+    into the first step's tensors), get_average_attention, reset, num_uncond_att_layers — against
+    the reference's own class driven through the same scenario (tests/golden/sdxl_store.npz, made
+    by make_goldens.gen_sdxl_store): every recorded array bit-identical, the same keys."""
+    import os
+    import sys
+    import numpy as np
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(here, "golden"))
+    import recipes
+    from unsupervised_keypoints import sdxl_monkey_patch as sm
+    gold = np.load(os.path.join(here, "golden", "sdxl_store.npz"))
+    ours = recipes.sdxl_store_scenario(sm.AttentionStore)
+    assert sorted(ours) == sorted(gold.files)
+    for k in gold.files:
+        assert np.array_equal(ours[k], gold[k]), k
+    assert int(gold["plain_nstore_up_cross"]) == 1 and int(gold["plain_nstore_down_cross"]) == 1   # 1025 px dropped
