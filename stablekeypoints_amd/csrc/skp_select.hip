@@ -512,29 +512,35 @@ __global__ __launch_bounds__(1024) void sort_topk_kernel(const double* __restric
 // r05: the first top_k of that order by ranking instead of sorting: key i's position in the ascending
 // order is rank_i = #{j : key_less(k_j, j, k_i, i)} (a strict total order: NaN last, ties by index),
 // so out[rank_i] = i for rank_i < top_k — the sort's first top_k exactly, with one barrier instead of
-// the bitonic network's log²(n) (at T = 500: 45 barrier-separated stages of a 1024-thread block).
-// blockIdx.x = segment; T ≤ 8192 keys staged in LDS (as doubles).
-__global__ __launch_bounds__(1024) void rank_topk_kernel(const double* __restrict__ keys, int T, int top_k,
-                                                         long long* __restrict__ out) {
+// the bitonic network's log²(n) (at T = 500: 45 barrier-separated stages of one 1024-thread block per
+// image).  A 16-lane row of a wave counts for one key (each lane over every 16th key, then one DPP
+// row sum), so a 256-thread block ranks 16 keys; grid = (images, ⌈T / 16⌉).  The block stages its
+// image's T keys (≤ 8192) in LDS.
+__global__ __launch_bounds__(256) void rank_topk_kernel(const double* __restrict__ keys, int T, int top_k,
+                                                        long long* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* k = reinterpret_cast<double*>(smem);
-  keys += (size_t)blockIdx.x * T;
-  out += (size_t)blockIdx.x * top_k;
+  const int b = blockIdx.y;
+  keys += (size_t)b * T;
+  out += (size_t)b * top_k;
   for (int i = threadIdx.x; i < T; i += blockDim.x) k[i] = keys[i];
   __syncthreads();
-  for (int i = threadIdx.x; i < T; i += blockDim.x) {
-    const double ki = k[i];
-    int r = 0;
-    if (isnan(ki)) {   // after every non-NaN key and every NaN of a lower index
-      for (int j = 0; j < T; ++j) r += (!isnan(k[j]) || j < i) ? 1 : 0;
-    } else {
-      for (int j = 0; j < T; ++j) {
-        const double kj = k[j];   // (NaN compares false: never before ki)
-        r += (kj < ki || (kj == ki && j < i)) ? 1 : 0;
-      }
-    }
-    if (r < top_k) out[r] = i;
+  const int li = threadIdx.x & 15;
+  const int i = blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int ii = min(i, T - 1);
+  const double ki = k[ii];
+  const bool ni = isnan(ki);
+  int r = 0;
+  for (int j = li; j < T; j += 16) {
+    const double kj = k[j];   // NaN kj compares false: never before a number
+    r += ni ? ((!isnan(kj) || j < ii) ? 1 : 0) : ((kj < ki || (kj == ki && j < ii)) ? 1 : 0);
   }
+  // Σ over the 16-lane row (integers: exact in any order)
+  r += __shfl_xor(r, 1, 16);
+  r += __shfl_xor(r, 2, 16);
+  r += __shfl_xor(r, 4, 16);
+  r += __shfl_xor(r, 8, 16);
+  if (li == 0 && i < T && r < top_k) out[r] = i;
 }
 
 // Furthest-point sampling over candidate positions (ptp_utils.py:115-159), one wave.
@@ -754,8 +760,8 @@ static int launch_sort(const double* keys, int T, int top_k, long long* out, hip
     const size_t lds = (size_t)n2 * (sizeof(double) + sizeof(int));
     hipLaunchKernelGGL(sort_topk_kernel, dim3(nb), dim3(1024), lds, st, keys, T, n2, top_k, out);
   } else {
-    const int threads = std::min(1024, (T + 63) / 64 * 64);
-    hipLaunchKernelGGL(rank_topk_kernel, dim3(nb), dim3(threads), (size_t)T * sizeof(double), st, keys, T, top_k, out);
+    hipLaunchKernelGGL(rank_topk_kernel, dim3((T + 15) / 16, nb), dim3(256), (size_t)T * sizeof(double), st, keys, T,
+                       top_k, out);
   }
   SKP_LAUNCH_CHECK();
   return SKP_OK;

@@ -11,6 +11,12 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 
 
+def _sample(o):
+    if isinstance(o, dict):
+        return o["sample"]
+    return o[0] if isinstance(o, tuple) else getattr(o, "sample", o)
+
+
 def test_sdxl_store_filled_by_tiny_sdxl_pass():
     from stablekeypoints_amd.optimize_token import load_ldm
     from stablekeypoints_amd.sd import SDXLUNet
@@ -22,16 +28,14 @@ def test_sdxl_store_filled_by_tiny_sdxl_pass():
     lat = torch.randn(1, 4, 32, 32, generator=g).to(DEV).repeat(2, 1, 1, 1)        # (uncond, cond) halves
     ctx = torch.randn(2, 12, unet.cross_attention_dim, generator=g).to(DEV)
     with torch.no_grad():
-        ref = unet(lat, 10, ctx)
-        ref = ref.sample if hasattr(ref, "sample") else ref[0] if isinstance(ref, tuple) else ref
+        ref = _sample(unet(lat, 10, ctx))
     n_mod = sum(1 for name, net in unet.named_children() if any(p in name for p in ("down", "mid", "up"))
                 for m in net.modules() if m.__class__.__name__ == "CrossAttention")
     store = sm.AttentionStore()
     count = sm.register_attention_control(ldm, store)
     assert count == n_mod and store.num_att_layers == n_mod and count > 0
     with torch.no_grad():
-        out = unet(lat, 10, ctx)
-        out = out.sample if hasattr(out, "sample") else out[0] if isinstance(out, tuple) else out
+        out = _sample(unet(lat, 10, ctx))
     # one UNet pass = one diffusion step: between_steps moved the step's lists into attention_store
     assert store.cur_step == 1 and store.cur_att_layer == 0
     assert set(store.attention_store) == set(sm.AttentionStore.get_empty_store())
