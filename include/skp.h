@@ -216,7 +216,7 @@ int skp_wino_out_transform(const float* M, int B, int K, int H, int W, const flo
                            float* y, void* stream);
 /* skp_wino_out_transform with the GEMM product laid out M[p][k][t] (the operands swapped: M[p] =
  * U[p]ᵀ · V[p]), so the tiles leave as coalesced image-row runs; gn_part (optional): the next
- * GroupNorm's (Σ, Σ²) per (image, channel, segment of min(P, 64) tiles), P = (H/4)·(W/4) tiles per
+ * GroupNorm's (mean, M2) per (image, channel, segment of min(P, 64) tiles), P = (H/4)·(W/4) tiles per
  * plane (16, 32 or a multiple of 64), nseg = P / min(P, 64) — the layout skp_groupnorm_fwd_part
  * reads. */
 int skp_wino_out_transform_kt(const float* M, int B, int K, int H, int W, const float* bias, const float* residual,
@@ -256,8 +256,10 @@ int skp_groupnorm_bwd(const float* x, const float* dy, const float* gamma, const
                       const float* stats, int B, int C, long long HW, int G, int act, float* dx, double* partial,
                       void* stream);
 /* skp_groupnorm_fwd with the statistics pass replaced by the producing convolution's per-segment
- * sums: part (B, C, nseg) float2 (Σx, Σx²) as skp_conv3x3_wino2_gn writes them (nseg = H/16 · W/32);
- * the shift is folded into the sums per channel.  Same output and saved (mean, rstd) layout. */
+ * statistics: part (B, C, nseg) float2 (mean, M2 = Σ(x − mean)²) per segment of n = HW / nseg
+ * pixels, as skp_conv3x3_wino2_gn / skp_wino_out_transform_kt write them; combined in fp64 by
+ * Chan's formula with the shift folded into each segment mean.  Same output and saved
+ * (mean, rstd) layout. */
 int skp_groupnorm_fwd_part(const float* x, const float* gamma, const float* beta, const float* shift, const float* part,
                            int nseg, int B, int C, long long HW, int G, float eps, int act, float* y, float* stats,
                            double* partial, void* stream);
@@ -362,8 +364,9 @@ int skp_wino2_weights(const float* w, int K, int C, int flip, float* U, void* st
 int skp_conv3x3_wino2(const float* x, const float* U, const float* bias, const float* residual, float* y, int B,
                       int C, int K, int H, int W, int nsplit, float* ws, void* stream);
 /* skp_conv3x3_wino2 that also writes the next GroupNorm's statistics from its epilogue: gn_part
- * (B, K, H/16 · W/32) float2 = (Σy, Σy²) of the final output (bias and residual included) per channel
- * over each 16-row × 32-pixel segment (nsplit = 1, H and W multiples of 32; may be null).  The
+ * (B, K, H/16 · W/32) float2 = (mean, M2 = Σ(y − mean)²) of the final output (bias and residual
+ * included) per channel over each 16-row × 32-pixel segment, accumulated around a pivot value of
+ * the segment (nsplit = 1, H and W multiples of 32; may be null).  The
  * consumer is skp_groupnorm_fwd_part: the frozen UNet / VAE's GroupNorm(+SiLU) after a 3×3 convolution
  * (diffusers resnet.py) then reads its input once instead of twice. */
 int skp_conv3x3_wino2_gn(const float* x, const float* U, const float* bias, const float* residual, float* y, int B,

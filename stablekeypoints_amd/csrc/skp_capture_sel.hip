@@ -234,7 +234,8 @@ __global__ __launch_bounds__(256) void sel_adjw_kernel(SelSmall t, const float* 
   const int S = t.s[l];
   float* A = sh;                                   // S × (R + 1), the vertical pass's adjoint matrix
   float* Hs = A + S * RP;                          // R × S
-  float4* TW = reinterpret_cast<float4*>(Hs + R * S);   // [R] tap weights
+  // [R] tap weights, 16-B aligned whatever S is (the launch sizes the LDS for the rounding)
+  float4* TW = reinterpret_cast<float4*>(Hs + ((R * S + S * RP + 3) & ~3) - S * RP);
   int* TL = reinterpret_cast<int*>(TW + R);             // [R] first tap (unclamped)
   const size_t bk = blockIdx.x - (size_t)l * BHK;  // bh·K + k
   const float* Eb = E + ((size_t)l * BHK + bk) * (size_t)R * R;
@@ -812,7 +813,8 @@ extern "C" int skp_capture_maps_bwd_sel(const float* const* z_low, const int* si
   }();
   if (adj_win && R <= 256 && R % 16 == 0) {
     hipLaunchKernelGGL(sel_adjw_kernel, dim3((unsigned)(L * BH * K)), dim3(R),
-                       (size_t)(smax * (R + 1) + R * smax + 5 * R) * sizeof(float), adj_st, t, E, BH * K, smax, R, es);
+                       (size_t)(smax * (R + 1) + R * smax + 3 + 5 * R) * sizeof(float), adj_st, t, E, BH * K, smax, R,
+                       es);
   } else {
     const int tr = sel_adj_tile(R);
     hipLaunchKernelGGL(sel_adj_kernel, dim3((unsigned)(L * BH * K)), dim3(256),

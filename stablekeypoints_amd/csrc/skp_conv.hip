@@ -975,7 +975,10 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
     // each consecutive pair is one 16-row × 32-pixel segment of one channel: the GroupNorm
     // statistics below accumulate a pair in registers and reduce the wave's 4 segments together
     static_assert(TXB != 8 || NIT == 8, "TXB 8: eight wave instructions per wave");
-    float g1[4] = {0.f, 0.f, 0.f, 0.f}, g2[4] = {0.f, 0.f, 0.f, 0.f};
+    // (Σd, Σd²) of d = v − p around a pivot p per segment (a value of the segment: its first wave
+    // instruction's lane-0 x), so a channel whose mean is far from 0 relative to its spread loses
+    // nothing to cancellation; the segment leaves as (mean, M2) for Chan's combine (r05)
+    float g1[4] = {0.f, 0.f, 0.f, 0.f}, g2[4] = {0.f, 0.f, 0.f, 0.f}, piv[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
       const int idx = TXB == 8 ? (((tid >> 6) * NIT + i) << 6) + (tid & 63) : i * NT + tid;
@@ -1000,9 +1003,12 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
       }
       if (dbg & 128) __builtin_nontemporal_store(f32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<f32x4*>(y + o));
       else if (!(dbg & 64)) *reinterpret_cast<float4*>(y + o) = v;
-      if (TXB == 8 && gnp) {   // the next GroupNorm's statistics: this lane's share of (Σv, Σv²)
-        g1[i >> 1] += (v.x + v.y) + (v.z + v.w);
-        g2[i >> 1] += (v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w);
+      if (TXB == 8 && gnp) {   // the next GroupNorm's statistics: this lane's share of (Σd, Σd²)
+        if ((i & 1) == 0) piv[i >> 1] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v.x)));
+        const float p = piv[i >> 1];
+        const float dx = v.x - p, dy = v.y - p, dz = v.z - p, dw = v.w - p;
+        g1[i >> 1] += (dx + dy) + (dz + dw);
+        g2[i >> 1] += (dx * dx + dy * dy) + (dz * dz + dw * dw);
       }
     }
     if (TXB == 8 && gnp) {
@@ -1032,13 +1038,17 @@ __device__ __forceinline__ void wino2_body(const W2Smem& sm, const float* __rest
       x += dpp_read<0x141>(x);                  // row_half_mirror
       x += dpp_read<0x4E>(x);                   // quad_perm [2,3,0,1]
       x += dpp_read<0xB1>(x);                   // quad_perm [1,0,3,2]
-      if ((lane & 7) == 0) {
-        const int r = lane >> 4, h = (lane >> 3) & 1;
+      const float x2 = __shfl_xor(x, 8, 64);    // lane 16r: Σd of segment r, x2 its Σd²
+      if ((lane & 15) == 0) {
+        const int r = lane >> 4;
         const int J = (tid >> 6) * NIT + 2 * r;   // the segment's first wave instruction
         const int c = (J << 6) / PCF, piece = ((J << 6) % PCF) >> 6;
         const int k = kb * w2::kNC + 16 * blk + c;
         const int seg = ((y0 + 8 * piece) >> 4) * (W >> 5) + (x0 >> 5);
-        reinterpret_cast<float*>(gnp)[2 * (((size_t)img * K + k) * (size_t)((H >> 4) * (W >> 5)) + seg) + h] = x;
+        const float p = r == 0 ? piv[0] : r == 1 ? piv[1] : r == 2 ? piv[2] : piv[3];
+        constexpr float inv_n = 1.0f / 512.0f;   // 16 rows × 32 pixels
+        gnp[((size_t)img * K + k) * (size_t)((H >> 4) * (W >> 5)) + seg] =
+            make_float2(p + x * inv_n, fmaxf(x2 - x * (x * inv_n), 0.0f));
       }
     }
     if (blk == 0) __syncthreads();

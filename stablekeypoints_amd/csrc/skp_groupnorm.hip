@@ -90,9 +90,12 @@ __global__ __launch_bounds__(kThreads) void gn_stats_kernel(const float* __restr
 }
 
 // Statistics from the producing convolution's epilogue (skp_conv3x3_wino2_gn): part[b][c][seg] =
-// (Σx, Σx²) over pixel segment seg (HW / nseg pixels) of channel c.  One block per (sample, group),
-// one pass over the group's cpg·nseg segments in fp64 with the channel's shift folded in per
-// segment (Σ(x+t) = Σx + n·t, Σ(x+t)² = Σx² + 2tΣx + n·t², n = the segment's pixels) and one block
+// (mean, M2) of pixel segment seg (n = HW / nseg pixels) of channel c — computed there around a
+// pivot inside the segment, so they carry no cancellation however far the channel's mean is from 0
+// (r05; the r04 form stored fp32 (Σx, Σx²) and lost the variance to E[x²] − mean² when
+// |mean| ≫ std).  One block per (sample, group), one pass over the group's cpg·nseg
+// segments in fp64 with the channel's shift folded into the segment mean: Σ(x+t) = n·(mean + t),
+// Σ(x+t)² = M2 + n·(mean + t)² (Chan's combination, exact up to fp64 rounding), then one block
 // reduction; the group totals go to chunk 0 of the layout gn_apply_kernel reads (the other chunks
 // zero), so the apply pass is the one skp_groupnorm_fwd uses.
 __global__ __launch_bounds__(kThreads) void gn_part_combine_kernel(const float2* __restrict__ part, int nseg,
@@ -107,8 +110,9 @@ __global__ __launch_bounds__(kThreads) void gn_part_combine_kernel(const float2*
   for (int e = threadIdx.x; e < sh.cpg * nseg; e += kThreads) {
     const float2 v = pg[e];
     const double t = shift ? (double)shift[(size_t)b * sh.C + g * sh.cpg + e / nseg] : 0.0;
-    s1 += (double)v.x + n * t;
-    s2 += (double)v.y + t * (2.0 * (double)v.x + n * t);
+    const double mt = (double)v.x + t;
+    s1 += n * mt;
+    s2 += (double)v.y + n * mt * mt;
   }
   block_sum2(s1, s2, sd);
   if (threadIdx.x < sh.nsplit) {

@@ -133,9 +133,10 @@ __global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__
 // operands swapped): one thread per (output channel, tile), a block's threads over consecutive
 // tiles of one channel, so the 36 loads per thread are coalesced over t AND the 4×4 tiles leave as
 // contiguous image-row runs (the [p][t][k] form above stores one 16-B piece per lane into 64
-// different channel planes).  gnp (optional): the next GroupNorm's (Σ, Σ²) of the output per
+// different channel planes).  gnp (optional): the next GroupNorm's (mean, M2) of the output per
 // segment of min(P, 64) tiles of one channel plane (P = tiles per plane, 16, 32 or a multiple of
-// 64), nseg = P / min(P, 64) per plane, reduced over the segment's lanes.
+// 64), nseg = P / min(P, 64) per plane: (Σd, Σd²) around a pivot (the segment's first value),
+// reduced over the segment's lanes, then mean = pivot + Σd/n, M2 = Σd² − (Σd)²/n.
 __global__ __launch_bounds__(256) void wino_out_kt_kernel(const float* __restrict__ M, int B, int K, int H, int W,
                                                           const float* __restrict__ bias,
                                                           const float* __restrict__ res, float* __restrict__ y,
@@ -167,7 +168,8 @@ __global__ __launch_bounds__(256) void wino_out_kt_kernel(const float* __restric
     }
   const float bk = bias ? bias[k] : 0.0f;
   const size_t base = ((size_t)b * K + k) * H * W + (size_t)(4 * ty) * W + 4 * tx;
-  float s1 = 0.0f, s2 = 0.0f;
+  const int seg = P < 64 ? P : 64;
+  float s1 = 0.0f, s2 = 0.0f, piv = 0.0f;   // (Σd, Σd²) of d = v − piv, piv = the segment's first value
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     float o[4];
@@ -189,12 +191,16 @@ __global__ __launch_bounds__(256) void wino_out_kt_kernel(const float* __restric
       v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
     }
     if (live) *reinterpret_cast<float4*>(y + off) = v;
-    s1 += (v.x + v.y) + (v.z + v.w);
-    s2 += (v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w);
+    if (gnp) {
+      if (q == 0) piv = __shfl(v.x, (int)(threadIdx.x & 63) & ~(seg - 1), 64);   // the segment's lane 0
+      const float dx = v.x - piv, dy = v.y - piv, dz = v.z - piv, dw = v.w - piv;
+      s1 += (dx + dy) + (dz + dw);
+      s2 += (dx * dx + dy * dy) + (dz * dz + dw * dw);
+    }
   }
-  if (gnp) {   // uniform: the segment's lanes all take part (dead lanes of a ragged tail add 0)
+  if (gnp) {   // uniform: the segment's lanes all take part (segments are whole planes' tiles: all
+               // live or all past the last image)
     if (!live) s1 = s2 = 0.0f;
-    const int seg = P < 64 ? P : 64;
     // reduce over aligned groups of `seg` lanes (16, 32 or 64; lanes of a segment are one plane)
     s1 += dpp_read<0xB1>(s1); s2 += dpp_read<0xB1>(s2);
     s1 += dpp_read<0x4E>(s1); s2 += dpp_read<0x4E>(s2);
@@ -202,9 +208,10 @@ __global__ __launch_bounds__(256) void wino_out_kt_kernel(const float* __restric
     s1 += dpp_read<0x140>(s1); s2 += dpp_read<0x140>(s2);
     if (seg >= 32) { s1 += __shfl_xor(s1, 16, 64); s2 += __shfl_xor(s2, 16, 64); }
     if (seg >= 64) { s1 += __shfl_xor(s1, 32, 64); s2 += __shfl_xor(s2, 32, 64); }
-    if (live && (threadIdx.x & (seg - 1)) == 0) {
+    if (live && (threadIdx.x & (seg - 1)) == 0) {   // (mean, M2) of the segment's 16·seg outputs
       const int nseg = P / seg;
-      gnp[((size_t)b * K + k) * nseg + r / seg] = make_float2(s1, s2);
+      const float inv_n = 1.0f / (float)(16 * seg);
+      gnp[((size_t)b * K + k) * nseg + r / seg] = make_float2(piv + s1 * inv_n, fmaxf(s2 - s1 * (s1 * inv_n), 0.0f));
     }
   }
 }

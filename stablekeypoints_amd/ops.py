@@ -929,14 +929,14 @@ def equivariance_loss_batch(A, At, theta_inv, nb):
 
 
 # --------------------------------------------------------------------------- UNet-side GroupNorm(+SiLU)
-# A/B switch (SKP_GN_EPI=0 off): the Winograd convolution's epilogue writes per-segment (Σ, Σ²) of
+# A/B switch (SKP_GN_EPI=0 off): the Winograd convolution's epilogue writes per-segment (mean, M2) of
 # its output (skp_conv3x3_wino2_gn) and a GroupNorm reading that output takes its statistics from
 # them (skp_groupnorm_fwd_part) instead of a pass over the activation.
 GN_EPI = os.environ.get("SKP_GN_EPI", "1") != "0"
 
 
 def _gn_parts_of(x):
-    """The (Σ, Σ²) segment partials the producing convolution left on ``x`` (None: none, or x was
+    """The (mean, M2) segment partials the producing convolution left on ``x`` (None: none, or x was
     modified in place since)."""
     ent = getattr(x, "_skp_gn", None)
     if ent is None or ent[0] != x._version:
@@ -1412,14 +1412,18 @@ _QKV_W = {}   # (id wq, id wk, id wv) -> ((versions), weakref(wq), [wq; wk; wv])
 
 
 def _qkv_weight(*ws):
-    """[w0; w1; …] of frozen projection weights, built once per weight set (and its versions)."""
+    """[w0; w1; …] of frozen projection weights, built once per weight set (and its versions): the
+    entry is reused only while EVERY weight is still the object it was built from (a weakref per
+    weight, so a replaced to_k / to_v never meets a stale concatenation through a reused id) with
+    the same storage and version; it is dropped when any of them is collected."""
     key = tuple(id(w) for w in ws)
-    ver = tuple(w._version for w in ws)
+    sig = tuple((w._version, w.data_ptr()) for w in ws)
     ent = _QKV_W.get(key)
-    if ent is not None and ent[0] == ver and ent[1]() is ws[0]:
+    if ent is not None and ent[0] == sig and all(r() is w for r, w in zip(ent[1], ws)):
         return ent[2]
     w3 = torch.cat([w.detach() for w in ws], 0).contiguous()
-    _QKV_W[key] = (ver, _weakref.ref(ws[0], lambda _r, key=key: _QKV_W.pop(key, None)), w3)
+    drop = lambda _r, key=key: _QKV_W.pop(key, None)   # noqa: E731
+    _QKV_W[key] = (sig, tuple(_weakref.ref(w, drop) for w in ws), w3)
     return w3
 
 
@@ -1434,6 +1438,7 @@ class QKVProjection(torch.autograd.Function):
         out = torch.matmul(x, w3.t())
         ctx.save_for_backward(w3)
         ctx.C = C
+        ctx.x_shape = x.shape
         ctx.set_materialize_grads(False)   # an unused projection's gradient stays None (skipped)
         return tuple(out[..., i * C:(i + 1) * C] for i in range(w3.shape[0] // C))
 
@@ -1445,14 +1450,15 @@ class QKVProjection(torch.autograd.Function):
         for i, g in enumerate(grads):
             if g is None:
                 continue
-            lead = g.shape[:-1]
             g2 = g.reshape(-1, C)
             wi = w3[i * C:(i + 1) * C]
             if dx is None:
                 dx = torch.mm(g2, wi)
             else:
                 dx.addmm_(g2, wi)
-        return dx.view(*lead, w3.shape[1]), None, None
+        if dx is None:   # no projection received a gradient
+            return None, None, None
+        return dx.view(ctx.x_shape), None, None
 
 
 # A/B (SKP_QKV=0: three nn.Linear calls and autograd's gradient sum)

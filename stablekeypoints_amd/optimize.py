@@ -465,13 +465,18 @@ class TokenOptimizer:
 
     def optimizer_step(self):
         if self.world > 1:
+            # ONE all-reduce per optimiser step: the embedding gradient and the three loss statistics
+            # in one flat buffer (SUM, then ÷ world: the reference's mean over replicas,
+            # optimize.py:428-443)
             import torch.distributed as dist
-            dist.all_reduce(self.context.grad, op=dist.ReduceOp.SUM)
-            self.context.grad.div_(self.world)
-            stats = torch.stack([torch.as_tensor(x, device=self.context.device, dtype=torch.float32).reshape(())
+            g = self.context.grad
+            stats = torch.stack([torch.as_tensor(x, device=g.device, dtype=g.dtype).reshape(())
                                  for x in (self.run_tot, self.run_eq, self.run_sh)])
-            dist.all_reduce(stats, op=dist.ReduceOp.SUM)
-            self.run_tot, self.run_eq, self.run_sh = (stats / self.world).unbind(0)
+            flat = torch.cat([g.reshape(-1), stats])
+            dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+            flat.div_(self.world)
+            g.copy_(flat[:g.numel()].view_as(g))
+            self.run_tot, self.run_eq, self.run_sh = flat[g.numel():].unbind(0)
         self.optimizer.step()
         self.optimizer.zero_grad()
         self._grad_acc = None

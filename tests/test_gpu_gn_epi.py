@@ -2,8 +2,9 @@
 skp_groupnorm_fwd_part): the UNet / VAE resnet's conv → GroupNorm(+SiLU) pair (diffusers resnet.py, the
 network the reference's capture rides on, ptp_utils.py:481-506).
 
-Checks: the per-segment (Σ, Σ²) partials against fp64 sums of the stored output (1e-5 of the
-segment's Σ|y| / Σy²); the GroupNorm output against fp64 torch GroupNorm of the same conv output
+Checks: the per-segment (mean, M2) partials (r05: accumulated around a pivot inside the segment,
+then Chan's combination) against fp64 segment means (1e-5 of the segment's mean |y|) and centred
+second moments (1e-5 relative, plus a floor); the GroupNorm output against fp64 torch GroupNorm of the same conv output
 (2e-5 of max |y|, the same bound the plain statistics pass meets) and against the statistics-pass
 path (SKP_GN_EPI=0); an in-place write to the conv output drops the partials."""
 import pytest
@@ -47,12 +48,8 @@ def test_conv_epilogue_groupnorm_statistics(monkeypatch, B, C, K, H, W, res, shi
     assert parts is not None, "the convolution left no statistics partials"
     gp, nseg = parts
     assert nseg == (H // 16) * (W // 32)
-    seg = y.double().reshape(B, K, H // 16, 16, W // 32, 32)
-    s1 = seg.sum(dim=(3, 5)).reshape(B, K, nseg)
-    s2 = (seg * seg).sum(dim=(3, 5)).reshape(B, K, nseg)
-    a1 = seg.abs().sum(dim=(3, 5)).reshape(B, K, nseg)
-    assert float(((gp[..., 0].double() - s1).abs() / a1).max()) < 1e-5
-    assert float(((gp[..., 1].double() - s2).abs() / s2).max()) < 1e-5
+    _check_parts(gp, y.double().reshape(B, K, H // 16, 16, W // 32, 32).permute(0, 1, 2, 4, 3, 5)
+                 .reshape(B, K, nseg, 512))
 
     out = ops.group_norm_act(y, gamma, beta, 32, 1e-5, act, sh)
     ref = _gn_ref(y, sh, gamma, beta, 32, 1e-5, act)
@@ -68,6 +65,43 @@ def test_conv_epilogue_groupnorm_statistics(monkeypatch, B, C, K, H, W, res, shi
     out2 = ops.group_norm_act(y, gamma, beta, 32, 1e-5, act, sh)
     ref2 = _gn_ref(y, sh, gamma, beta, 32, 1e-5, act)
     assert float((out2.double() - ref2).abs().max()) / float(ref2.abs().max()) < 2e-5
+
+
+def _check_parts(gp, vals):
+    """gp (B, K, nseg) float2 (mean, M2) vs fp64 over vals (B, K, nseg, n)."""
+    mean = vals.mean(-1)
+    m2 = ((vals - mean[..., None]) ** 2).sum(-1)
+    a1 = vals.abs().mean(-1)
+    assert float(((gp[..., 0].double() - mean).abs() / a1).max()) < 1e-5
+    assert float(((gp[..., 1].double() - m2).abs() / (m2 + 1e-6 * a1 * a1 * vals.shape[-1])).max()) < 1e-5
+
+
+@pytest.mark.parametrize("offset", [50.0, 400.0])
+def test_conv_epilogue_groupnorm_large_offset(offset):
+    """A channel mean far from 0 relative to its spread (bias ≈ 50, std ≈ 1, plus a time
+    -embedding shift): the epilogue statistics (pivoted (mean, M2), Chan's combination in fp64) give
+    the GroupNorm output within 2e-5 of fp64 torch; E[x²] − mean² from fp32 (Σx, Σx²), the r04 form,
+    lost the variance here."""
+    from stablekeypoints_amd import ops
+    B, C, K, H, W = 4, 128, 128, 64, 64
+    g = torch.Generator(device=DEV).manual_seed(int(offset))
+    x = torch.randn(B, C, H, W, device=DEV, generator=g)
+    w = torch.randn(K, C, 3, 3, device=DEV, generator=g) / (3 * C ** 0.5)   # output std ≈ 1
+    bias = offset + torch.randn(K, device=DEV, generator=g) * 0.1
+    sh = torch.randn(B, K, device=DEV, generator=g) * (offset / 5)
+    gamma = torch.randn(K, device=DEV, generator=g)
+    beta = torch.randn(K, device=DEV, generator=g)
+    y = ops.conv3x3(x, w, bias)
+    parts = ops._gn_parts_of(y)
+    assert parts is not None
+    gp, nseg = parts
+    _check_parts(gp, y.double().reshape(B, K, H // 16, 16, W // 32, 32).permute(0, 1, 2, 4, 3, 5)
+                 .reshape(B, K, nseg, 512))
+    out = ops.group_norm_act(y, gamma, beta, 32, 1e-5, True, sh)
+    ref = _gn_ref(y, sh, gamma, beta, 32, 1e-5, True)
+    err = float((out.double() - ref).abs().max()) / float(ref.abs().max())
+    print(f"\nGroupNorm from epilogue statistics at offset {offset}: rel-max {err:.1e}")
+    assert err < 2e-5, err
 
 
 def test_resnet_block_with_epilogue_statistics_matches_plain(monkeypatch):
@@ -111,12 +145,8 @@ def test_wino_gemm_groupnorm_statistics(monkeypatch, B, C, K, H, W, res):
     P = th * tw
     seg = min(P, 64)
     assert nseg == P // seg
-    tiles = y.double().reshape(B, K, th, 4, tw, 4)
-    s1 = tiles.sum(dim=(3, 5)).reshape(B, K, nseg, seg).sum(-1)
-    s2 = (tiles * tiles).sum(dim=(3, 5)).reshape(B, K, nseg, seg).sum(-1)
-    a1 = tiles.abs().sum(dim=(3, 5)).reshape(B, K, nseg, seg).sum(-1)
-    assert float(((gp[..., 0].double() - s1).abs() / a1).max()) < 1e-5
-    assert float(((gp[..., 1].double() - s2).abs() / s2).max()) < 1e-5
+    tiles = y.double().reshape(B, K, th, 4, tw, 4).permute(0, 1, 2, 4, 3, 5).reshape(B, K, P, 16)
+    _check_parts(gp, tiles.reshape(B, K, nseg, seg * 16))
     monkeypatch.setattr(ops, "WINO_KT", False)
     y0 = ops.conv3x3(x, w, bias, r)
     assert ops._gn_parts_of(y0) is None
