@@ -675,20 +675,37 @@ void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nc
           const unsigned obs = JS * nq * 16u;
           using gcf4 = const __attribute__((address_space(1))) f4;
           using gcc = const __attribute__((address_space(1))) char;
+#ifndef SKP_MAPS_VPT
+#define SKP_MAPS_VPT 1   // elements per thread whose loads are in flight together (A/B build)
+#endif
+          constexpr int VPT = SKP_MAPS_VPT;
   #pragma unroll 1
-          for (int e = tid; e < tot; e += kMapThreads, ob += obs) {
-            f4 v = (f4)kPadLogit;
-            if (q < nq) {
-              const f4 a0 = *reinterpret_cast<gcf4*>(reinterpret_cast<gcc*>(r0) + ob);
-              const f4 a1 = *reinterpret_cast<gcf4*>(reinterpret_cast<gcc*>(r1) + ob);
-              const f4 a2 = *reinterpret_cast<gcf4*>(reinterpret_cast<gcc*>(r2) + ob);
-              const f4 a3 = *reinterpret_cast<gcf4*>(reinterpret_cast<gcc*>(r3) + ob);
-              v = a0 * wy[0];
-              v = __builtin_elementwise_fma(a1, (f4)wy[1], v);
-              v = __builtin_elementwise_fma(a2, (f4)wy[2], v);
-              v = __builtin_elementwise_fma(a3, (f4)wy[3], v);
+          for (int e0 = tid; e0 < tot; e0 += VPT * kMapThreads, ob += VPT * obs) {
+            f4 a[VPT][4];
+  #pragma unroll
+            for (int k = 0; k < VPT; ++k) {
+              if (e0 + k * kMapThreads < tot && q < nq) {
+                const unsigned o = ob + k * obs;
+                a[k][0] = *reinterpret_cast<gcf4*>(reinterpret_cast<gcc*>(r0) + o);
+                a[k][1] = *reinterpret_cast<gcf4*>(reinterpret_cast<gcc*>(r1) + o);
+                a[k][2] = *reinterpret_cast<gcf4*>(reinterpret_cast<gcc*>(r2) + o);
+                a[k][3] = *reinterpret_cast<gcf4*>(reinterpret_cast<gcc*>(r3) + o);
+              }
             }
-            V4[e] = v;
+  #pragma unroll
+            for (int k = 0; k < VPT; ++k) {
+              const int e = e0 + k * kMapThreads;
+              if (e < tot) {
+                f4 v = (f4)kPadLogit;
+                if (q < nq) {
+                  v = a[k][0] * wy[0];
+                  v = __builtin_elementwise_fma(a[k][1], (f4)wy[1], v);
+                  v = __builtin_elementwise_fma(a[k][2], (f4)wy[2], v);
+                  v = __builtin_elementwise_fma(a[k][3], (f4)wy[3], v);
+                }
+                V4[e] = v;
+              }
+            }
           }
         } else {
   #pragma unroll 1
@@ -1558,13 +1575,12 @@ size_t maps_lds(int vstride, int qpl, int waves) {   // [2][P] taps ×2 + [2][vs
   return (16 * (size_t)waves * maps_pxw(qpl) + 2 * (size_t)vstride) * sizeof(float);
 }
 
-// workgroup size: 8 waves (two workgroups per CU) unless SKP_MAPS_WAVES=16 (A/B switch)
+// workgroup size: 8 waves (two workgroups per CU) unless SKP_MAPS_WAVES=16 (one per CU) or 4 (four
+// per CU) (A/B switch, read per call)
 int maps_waves() {
-  static const int w = [] {
-    const char* e = getenv("SKP_MAPS_WAVES");
-    return (e && atoi(e) == 16) ? 16 : 8;
-  }();
-  return w;
+  const char* e = getenv("SKP_MAPS_WAVES");
+  const int v = e ? atoi(e) : 8;
+  return (v == 16 || v == 4) ? v : 8;
 }
 
 template <int QPL, int WAVES>
@@ -1585,7 +1601,7 @@ void launch_maps(const CapLayers& cl, int L, int B, int H, int N, int R, int vst
         n = 256;
       return std::max(8, n / 8 * 8);
     }();
-    grid = std::min(grid, (WAVES == 8 ? 2 : 1) * ncu);   // multiple of 8
+    grid = std::min(grid, (16 / WAVES) * ncu);   // multiple of 8
   }
   hipLaunchKernelGGL((capture_maps_kernel<QPL, WAVES>), dim3(grid), dim3(WAVES * WAVE), lds, st, cl, L, B, H, N, R,
                      nchunks, vstride, (float)L * (float)H, maps);
@@ -1595,6 +1611,7 @@ template <int QPL>
 void launch_maps_w(int waves, const CapLayers& cl, int L, int B, int H, int N, int R, int vstride, size_t lds,
                    float* maps, hipStream_t st) {
   if (waves == 16) launch_maps<QPL, 16>(cl, L, B, H, N, R, vstride, lds, maps, st);
+  else if (waves == 4) launch_maps<QPL, 4>(cl, L, B, H, N, R, vstride, lds, maps, st);
   else launch_maps<QPL, 8>(cl, L, B, H, N, R, vstride, lds, maps, st);
 }
 
