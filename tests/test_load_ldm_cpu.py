@@ -113,13 +113,15 @@ def test_unsupervised_keypoints_import_path():
         return_regressor, return_regressor_visible, return_regressor_human36m  # noqa: F401
     from unsupervised_keypoints.eval import evaluate, run_image_with_context_augmented, find_max_pixel  # noqa: F401
     from unsupervised_keypoints.invertable_transform import RandomAffineWithInverse  # noqa: F401
-    from unsupervised_keypoints.sdxl_monkey_patch import AttentionStore as XLStore
+    from unsupervised_keypoints.sdxl_monkey_patch import AttentionStore as XLStore, register_attention_control
     import stablekeypoints_amd.eval, stablekeypoints_amd.keypoint_regressor  # noqa: E401
     assert ptp_utils is skp.ptp_utils and optimize is skp.optimize and ot is skp.optimize_token
     assert ev is stablekeypoints_amd.eval and keypoint_regressor is stablekeypoints_amd.keypoint_regressor
     assert invertable_transform is skp.invertable_transform
     assert ref_load_ldm is load_ldm and optimize_embedding is skp.optimize.optimize_embedding
-    assert XLStore is skp.ptp_utils.AttentionStore
+    # the SDXL store API is its own restatement (sdxl_monkey_patch.py:8-214), not ptp_utils' store
+    import stablekeypoints_amd.sdxl_monkey_patch as xl
+    assert XLStore is xl.AttentionStore and register_attention_control is xl.register_attention_control
     import unsupervised_keypoints.main as m
     assert m.main is skp.main.main and m.build_parser is skp.main.build_parser
 
