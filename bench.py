@@ -107,6 +107,29 @@ def _pmc_record(path, name, key, value):
     return rec.get(value), src
 
 
+def _sel_bwd_split():
+    """Average per-call device time of the sparse backward's phases in the timed region, from the
+    HIP events libskp records between its launches on the call's stream (skp_sel_bwd_timing_read),
+    or None when no fast-path call was recorded."""
+    import ctypes
+
+    from stablekeypoints_amd import _lib
+    L = _lib.lib()
+    if not hasattr(L, "skp_sel_bwd_timing_read"):
+        return None
+    ms = (ctypes.c_double * 4)()
+    n = ctypes.c_int(0)
+    rc = L.skp_sel_bwd_timing_read(ms, ctypes.byref(n))
+    L.skp_sel_bwd_timing(0)
+    if rc != 0 or n.value == 0:
+        return None
+    names = ("sel_gather", "sel_doth", "sel_adjv", "sel_dense")
+    out = {k: ms[i] / n.value for i, k in enumerate(names)}
+    out["calls"] = n.value
+    out["timing_source"] = "HIP events recorded by libskp between the phases' launches (skp_sel_bwd_timing)"
+    return out
+
+
 # ------------------------------------------------------------------------------ CPU baseline (port)
 def _cgroup_cpus():
     """The job's CPU quota from cgroup v2 ``cpu.max`` ("quota period" or "max period"): raw text and
@@ -569,6 +592,9 @@ def main():
     barrier()
     torch.cuda.synchronize()
     timer.enabled = True
+    from stablekeypoints_amd import _lib
+    if hasattr(_lib.lib(), "skp_sel_bwd_timing"):
+        _lib.lib().skp_sel_bwd_timing(1)   # per-phase events inside the sparse backward (split below)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         rec = step()
@@ -576,6 +602,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     timer.enabled = False
+    sel_split = _sel_bwd_split()
     if world > 1:
         import torch.distributed as dist
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -643,6 +670,8 @@ def main():
                            "algorithmic_bytes_per_call": bw["bytes_per_launch"],
                            "valu_busy_pmc": vb, "valu_busy_source": vb_src,
                            "issue_roofline": issue_roofline(bw, "ops.capture_maps_sel_bwd_issue_cycles (the dense part)")}
+            if name == "skp_capture_maps_bwd_sel" and sel_split:
+                extra[name]["split_ms"] = sel_split
     agg = timer.summary("skp_aggregate")
     if agg:
         achieved = agg["bytes_per_launch"] / (agg["avg_ms"] * 1e-3)
@@ -668,7 +697,11 @@ def main():
             "bound": "hbm", "avg_ms": sel["avg_ms"], "launches": sel["launches"], "timing_source": timing_src,
             "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,
             "algorithmic_bytes_per_launch": sel["bytes_per_launch"], "traffic": traffic, "traffic_source": traffic_src,
-            "note": "the A8 KL ranking (kl_gauss_win_kernel) of every image of a pass, one launch"}
+            "note": ("the A8 call: KL ranking of every image of a pass with each image's top-k ranked by its last "
+                     "block, one launch (kl_gauss_win_kernel)" if ops.A8_FUSED else
+                     "the A8 KL ranking (kl_gauss_win_kernel) of every image of a pass, one launch")}
+        if ops.A8_FUSED:
+            extra["a8_call_ms"] = sel["avg_ms"]
     tk = timer.summary("skp_topk_keys")
     if tk:
         extra["skp_topk_keys"] = {"avg_ms": tk["avg_ms"], "launches": tk["launches"], "timing_source": timing_src,

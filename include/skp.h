@@ -89,6 +89,14 @@ long long skp_capture_maps_bwd_sel_workspace(const int* sizes, int L, int B, int
 int skp_capture_maps_bwd_sel(const float* const* z_low, const int* sizes, int L, int B, int H, int N, int R,
                              const long long* sel_tok, int K, const float* gsel, float gscale,
                              const float* const* stats, float* const* dz_low, float* workspace, void* stream);
+/* Per-phase device time of skp_capture_maps_bwd_sel's fast path (measurement only, not on the
+ * reference's interface): skp_sel_bwd_timing(1) makes every later single-stream call record HIP
+ * events between its phases on its stream (at most 256 calls), skp_sel_bwd_timing(0) stops;
+ * skp_sel_bwd_timing_read waits for the recorded calls and returns the summed ms of
+ * ms[0] sel_gather, ms[1] sel_doth (sel_dot), ms[2] the adjoint's vertical pass (sel_adjw), ms[3]
+ * sel_dense, and the number of calls, then clears the record.                              */
+int skp_sel_bwd_timing(int enable);
+int skp_sel_bwd_timing_read(double* ms, int* calls);
 
 /* ---------------------------------------------------------------- A3 aggregate
  * optimize.collect_maps (optimize.py:27-79), token-major output:

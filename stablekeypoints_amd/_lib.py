@@ -25,6 +25,8 @@ _SIGS = {
                              _c_float, ctypes.POINTER(_p), ctypes.POINTER(_p), _p, _p],
     "skp_capture_maps_bwd_sel": [ctypes.POINTER(_p), ctypes.POINTER(_c_int), _c_int, _c_int, _c_int, _c_int, _c_int,
                                  _p, _c_int, _p, _c_float, ctypes.POINTER(_p), ctypes.POINTER(_p), _p, _p],
+    "skp_sel_bwd_timing": [_c_int],
+    "skp_sel_bwd_timing_read": [_p, _p],
     "skp_capture_maps_bwd_sel_workspace": [ctypes.POINTER(_c_int), _c_int, _c_int, _c_int, _c_int, _c_int, _c_int],
     "skp_aggregate": [ctypes.POINTER(_p), _c_int, _c_int, _c_int, _c_int, _p, _c_int, _p, _p],
     "skp_resize_bilinear": [_p, _c_int, _c_int, _c_int, _p, _p],
@@ -92,6 +94,8 @@ _SIGS = {
 
 
 _RESTYPE = {"skp_capture_maps_bwd_sel_workspace": _c_ll}
+# measurement hooks (not on the reference's interface) that A/B runs against older builds may lack
+_MEASUREMENT_ONLY = {"skp_sel_bwd_timing", "skp_sel_bwd_timing_read"}
 
 
 class SkpLibraryError(RuntimeError):
@@ -113,6 +117,8 @@ def lib():
         except OSError as e:
             raise SkpLibraryError(f"cannot load {LIB_PATH}: {e}") from e
         for name, args in _SIGS.items():
+            if name in _MEASUREMENT_ONLY and not hasattr(L, name):
+                continue   # an older library in an A/B run (SKP_LIB): the bench skips what it lacks
             f = getattr(L, name)
             f.argtypes = args
             f.restype = _RESTYPE.get(name, _c_int)

@@ -19,6 +19,8 @@
 //                with mb = log2(1/Σ) − max·log2e, so a = exp2(z·log2e + mb)
 //   sel_adj      per (bh, k): es[bh][k] = bicubicᵀ(E[bh][k])  (R² → s², separable through an LDS table
 //                of the adjoint weights, deterministic)
+//   (r05 default: sel_doth = sel_dot + the horizontal half of sel_adj, E never leaves LDS, and
+//    sel_adjv = the vertical half on the R × s rows sel_doth wrote)
 //   sel_dense    per (bh, 128-token chunk): the dense part's adjoint, plus es at the selected tokens
 // sel_dense is the hot kernel.  One workgroup = R/PW bands of 64 (or, at R/s = 4, 32) lanes; band
 // w owns output columns [PW·w, PW·w + PW) of every row and lanes own token pairs (packed f32:
@@ -36,6 +38,7 @@
 // added at the selected tokens, and the row leaves as coalesced 512-B token runs.
 // Every output element has one owner and a fixed summation order: deterministic, no atomics.
 #include <algorithm>
+#include <vector>
 
 #include "skp_common.h"
 
@@ -77,6 +80,21 @@ __global__ void sel_gather_kernel(SelSmall t, int L, int BH, int N, int H, const
   const int bh = (int)(bq / SS);
   const long long tk = tok[(long long)(bh / H) * K + k];
   zsel[e] = (tk >= 0 && tk < N) ? t.z[l][bq * N + tk] : 0.0f;
+}
+
+// The per-pixel pair sel_dense reads: (mb, d) with d = −dot and a = exp2(z·log2e + mb).  With
+// SKP_SEL_DFOLD (default) |d| is folded into the exponent, (mb + log2|d|, d): sel_dense then gets
+// a·|d| from its exp2 and d's sign from its tap weights' sign bits (scalar xors), one packed
+// multiply per (pixel, token pair) less (d = 0 gives exp2(−inf) = 0).
+#ifndef SKP_SEL_DFOLD
+#define SKP_SEL_DFOLD 1
+#endif
+__device__ __forceinline__ float2 sel_pix(float mb, float dot) {
+#if SKP_SEL_DFOLD
+  return make_float2(mb + __builtin_amdgcn_logf(fabsf(dot)), -dot);   // v_log_f32 = log2
+#else
+  return make_float2(mb, -dot);
+#endif
 }
 
 // output indices whose taps can reach low-res index j: src ∈ [j − 2, j + 2) (clamped edges included)
@@ -137,7 +155,124 @@ __global__ __launch_bounds__(256) void sel_dot_kernel(SelSmall t, const float* _
       dot += e;
       E[((size_t)bh * K + k) * RR + p] = e;
     }
-    pix[(size_t)bh * RR + p] = make_float2(mb, -dot);
+    pix[(size_t)bh * RR + p] = sel_pix(mb, dot);
+  }
+}
+
+// ------------------------------------------------------------------------------ sel_doth
+// sel_dot with the horizontal half of the sparse part's bicubicᵀ fused in (r05): the row's e_k stay
+// in LDS and leave as Hs[l][bh][k][y][j] = Σ_x A[j][x]·e_k[y][x] (R·s floats per (bh, k) instead
+// of E's R², so E's write + re-read — 2 × 168 MB at the bench shape — is gone; sel_adjv does the
+// vertical half).  One block per (layer, bh, y), R threads (R ≤ 256).
+// At R = RATIO·s (RATIO a power of two) virtual column c takes its taps from the 4·RATIO pixels
+// x = RATIO·(c − 2) + RATIO/2 + t, t ∈ [0, 4·RATIO), with weight W[t] = w_{3 − t/RATIO} of pixel
+// phase (RATIO/2 + t) mod RATIO: one fixed filter for every column, so column c is a 4·RATIO-tap dot
+// product against the row's e (zero-padded past both edges), and the clamped edge columns add their
+// virtual columns −2, −1, 0 / S − 1, S, S + 1 in that order.  Per column the terms run x ascending
+// from 0 — exactly sel_adjw's rolling-window sums and its edge order, so Hs (and es) are
+// bit-identical to the E path's.
+constexpr int DOTH_PAD = 64;   // zero floats each side of a row's e (≥ 3.5·RATIO at RATIO ≤ 16)
+
+// virtual columns c = cv − 2, cv ∈ [0, S + 4): Vc[cv][k] = Σ_t W[t]·e_k[RATIO·(c − 2) + RATIO/2 + t]
+// (one fixed-length dot product per lane, lanes over k first: rows k sit 2 banks apart)
+template <int RATIO>
+__device__ __forceinline__ void doth_columns(const float* __restrict__ W, const float* __restrict__ Ep, int EP, int K,
+                                             int S, float* __restrict__ Vc) {
+  constexpr int NT = 4 * RATIO;
+  float w[NT];
+#pragma unroll
+  for (int q = 0; q < NT; ++q) w[q] = W[q];
+  for (int e = threadIdx.x; e < K * (S + 4); e += blockDim.x) {
+    const int k = e % K, cv = e / K;
+    const float* src = Ep + k * EP + DOTH_PAD + RATIO / 2 - 4 * RATIO + RATIO * cv;
+    float a = 0.0f;
+#pragma unroll
+    for (int q = 0; q < NT; ++q) a = fmaf(w[q], src[q], a);
+    Vc[e] = a;
+  }
+}
+
+template <int RMAX>
+__global__ __launch_bounds__(256) void sel_doth_kernel(SelSmall t, const float* __restrict__ zsel, int BH, int R,
+                                                       int H, int K, const long long* __restrict__ tok,
+                                                       const float* __restrict__ gsel, float gscale, int smax,
+                                                       float* __restrict__ Hs, float2* __restrict__ pix) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int l = blockIdx.x / (BH * R);
+  const int rem = blockIdx.x - l * (BH * R);
+  const int bh = rem / R, y = rem % R;
+  const int b = bh / H;
+  const int S = t.s[l];
+  const int ratio = R / S;
+  const int EP = R + 2 * DOTH_PAD + 2;
+  float* W = sm;                        // [64] the column filter
+  float* Vs = W + 64;                   // S × K
+  float* Ep = Vs + ((S * K + 3) & ~3);  // K × EP, the row's e at [DOTH_PAD, DOTH_PAD + R)
+  const size_t RR = (size_t)R * R;
+  pix += (size_t)l * BH * RR;
+  const float2* stats = t.stats[l];
+  const Taps4 ty = bicubic_taps(y, S, R);
+  const float* zb = zsel + t.zoff[l] + (size_t)bh * S * S * K;
+  for (int e = threadIdx.x; e < S * K; e += blockDim.x) {
+    const int j = e / K, k = e - j * K;
+    float v = ty.w[0] * zb[((size_t)ty.i[0] * S + j) * K + k];
+    v = fmaf(ty.w[1], zb[((size_t)ty.i[1] * S + j) * K + k], v);
+    v = fmaf(ty.w[2], zb[((size_t)ty.i[2] * S + j) * K + k], v);
+    v = fmaf(ty.w[3], zb[((size_t)ty.i[3] * S + j) * K + k], v);
+    Vs[e] = v;
+  }
+  for (int e = threadIdx.x; e < K * 2 * DOTH_PAD; e += blockDim.x) {   // the zero pads
+    const int k = e / (2 * DOTH_PAD), q = e - k * (2 * DOTH_PAD);
+    Ep[k * EP + (q < DOTH_PAD ? q : R + q)] = 0.0f;
+  }
+  const int x = threadIdx.x;   // blockDim.x == R
+  const Taps4 tx = bicubic_taps(x, S, R);
+  if (x < ratio) {   // phase x's weights into the filter
+#pragma unroll
+    for (int m = 0; m < 4; ++m) W[ratio * (3 - m) + (x + ratio / 2) % ratio] = tx.w[m];
+  }
+  __syncthreads();
+  const size_t p = (size_t)y * R + x;
+  const float2 st = stats[(size_t)bh * RR + p];
+  const float mb = __builtin_amdgcn_logf(st.y) - st.x * L2E;   // v_log_f32 = log2
+  float dot = 0.0f;
+  for (int k = 0; k < K; ++k) {
+    float e = 0.0f;
+    if (tok[(size_t)b * K + k] >= 0) {
+      float z = tx.w[0] * Vs[tx.i[0] * K + k];
+      z = fmaf(tx.w[1], Vs[tx.i[1] * K + k], z);
+      z = fmaf(tx.w[2], Vs[tx.i[2] * K + k], z);
+      z = fmaf(tx.w[3], Vs[tx.i[3] * K + k], z);
+      const float a = __builtin_amdgcn_exp2f(fmaf(z, L2E, mb));
+      e = a * (gsel[((size_t)b * K + k) * RR + p] * gscale);
+    }
+    dot += e;
+    Ep[k * EP + DOTH_PAD + x] = e;
+  }
+  pix[(size_t)bh * RR + p] = sel_pix(mb, dot);
+  __syncthreads();
+  float* hb = Hs + ((size_t)l * BH + bh) * K * R * smax + (size_t)y * smax;
+  float* Vc = Ep + K * EP;   // [S + 4][K]
+  if (RMAX >= 16 && ratio == 16) doth_columns<(RMAX >= 16 ? 16 : 8)>(W, Ep, EP, K, S, Vc);
+  else if (ratio == 8) doth_columns<8>(W, Ep, EP, K, S, Vc);
+  else doth_columns<4>(W, Ep, EP, K, S, Vc);
+  __syncthreads();
+  // clamped edge columns: their virtual columns in sel_adjw's order (−2, −1, 0 / S − 1, S, S + 1)
+  for (int e = threadIdx.x; e < K * S; e += blockDim.x) {
+    const int j = e % S, k = e / S;   // lanes over j: each k's row of s columns leaves contiguous
+    float s;
+    if (j == 0) {
+      s = Vc[k];
+      s += Vc[K + k];
+      s += Vc[2 * K + k];
+    } else if (j == S - 1) {
+      s = Vc[(S + 1) * K + k];
+      s += Vc[(S + 2) * K + k];
+      s += Vc[(S + 3) * K + k];
+    } else {
+      s = Vc[(j + 2) * K + k];
+    }
+    hb[(size_t)k * R * smax + j] = s;   // Hs[l][bh][k][y][j]
   }
 }
 
@@ -299,6 +434,43 @@ __global__ __launch_bounds__(256) void sel_adjw_kernel(SelSmall t, const float* 
     emit(base + 3, a3);
     hrow[pt] = pend;
     for (int j = pt + 1; j < S; ++j) hrow[j] = 0.0f;   // columns no pixel reaches (none at R ≥ S)
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < S * S; e += blockDim.x) {
+    const int i = e / S, j = e - i * S;
+    int y0, y1;
+    adj_range(i, S, R, y0, y1);
+    const float* Ai = A + i * RP;
+    float acc = 0.0f;
+    for (int yy = y0; yy <= y1; ++yy) acc = fmaf(Ai[yy], Hs[yy * S + j], acc);
+    es[bk * (size_t)S * S + e] = acc;
+  }
+}
+
+// The vertical half of the sparse part's bicubicᵀ after sel_doth: es[i][j] = Σ_y A[i][y]·Hs[y][j]
+// (sel_adjw's final pass, y ascending) on the R × s rows sel_doth left in HBM.  Block = (layer,
+// bh, k), 256 threads; LDS: the adjoint matrix A[S][R + 1] and the block's Hs rows [R][S].
+__global__ __launch_bounds__(256) void sel_adjv_kernel(SelSmall t, const float* __restrict__ Hsg, int BH, int BHK,
+                                                       int smax, int R, float* __restrict__ es) {
+  extern __shared__ float sh[];
+  const int RP = R + 1;
+  const int l = blockIdx.x / BHK;
+  const int S = t.s[l];
+  float* A = sh;               // S × (R + 1)
+  float* Hs = A + S * RP;      // R × S
+  const size_t bk = blockIdx.x - (size_t)l * BHK;  // bh·K + k
+  const float* hb = Hsg + ((size_t)l * BHK + bk) * (size_t)R * smax;   // [y][j] rows of sel_doth
+  es += (size_t)l * BHK * smax * smax;
+  for (int e = threadIdx.x; e < S * RP; e += blockDim.x) A[e] = 0.0f;
+  for (int e = threadIdx.x; e < R * S; e += blockDim.x) {
+    const int yy = e / S, j = e - yy * S;
+    Hs[e] = hb[(size_t)yy * smax + j];
+  }
+  __syncthreads();
+  for (int y = threadIdx.x; y < R; y += blockDim.x) {
+    const Taps4 ty = bicubic_taps(y, S, R);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) A[ty.i[m] * RP + y] += ty.w[m];
   }
   __syncthreads();
   for (int e = threadIdx.x; e < S * S; e += blockDim.x) {
@@ -487,7 +659,14 @@ __device__ __forceinline__ void sel_dense_body(const SelLayers& sl, int BH, int 
       for (int t = 0; t < PW; ++t) {
         const int ut = t % RATIO;
         const int c0 = lo_rel(t, RATIO) + 2;                             // band slot of the first tap
-        const float2 pd = pp[t];                                         // (mb, d), uniform per band
+        // (mb, d), uniform per band: a scalar load where the band is the wave (read-only here)
+        float2 pd;
+        if constexpr (LW == WAVE && SKP_SEL_DFOLD) {
+          using cu64 = __attribute__((address_space(4))) const unsigned long long;
+          pd = __builtin_bit_cast(float2, reinterpret_cast<cu64*>(reinterpret_cast<uintptr_t>(pp))[t]);
+        } else {
+          pd = pp[t];
+        }
         f2 zv = V[c0] * wt[ut][0];
         zv = __builtin_elementwise_fma(V[c0 + 1], (f2)wt[ut][1], zv);
         zv = __builtin_elementwise_fma(V[c0 + 2], (f2)wt[ut][2], zv);
@@ -495,11 +674,24 @@ __device__ __forceinline__ void sel_dense_body(const SelLayers& sl, int BH, int 
         f2 ex = __builtin_elementwise_fma(zv, l2e, (f2)pd.x);
         ex.x = __builtin_amdgcn_exp2f(ex.x);
         ex.y = __builtin_amdgcn_exp2f(ex.y);
+        float w4[4] = {wt[ut][0], wt[ut][1], wt[ut][2], wt[ut][3]};
+#if SKP_SEL_DFOLD
+        if constexpr (LW == WAVE) {
+          // ex = a·|d| (sel_pix); d's sign (uniform: one band per wave) flips the tap weights'
+          // sign bits in SGPRs — no VALU
+          const unsigned sg = __builtin_bit_cast(unsigned, pd.y) & 0x80000000u;
+#pragma unroll
+          for (int m = 0; m < 4; ++m) w4[m] = __builtin_bit_cast(float, __builtin_bit_cast(unsigned, w4[m]) ^ sg);
+        } else {   // two bands per wave: the sign as a packed multiply, as without the fold
+          ex *= (f2)__builtin_copysignf(1.0f, pd.y);
+        }
+#else
         ex *= pd.y;
-        Hs[c0] = __builtin_elementwise_fma(ex, (f2)wt[ut][0], Hs[c0]);
-        Hs[c0 + 1] = __builtin_elementwise_fma(ex, (f2)wt[ut][1], Hs[c0 + 1]);
-        Hs[c0 + 2] = __builtin_elementwise_fma(ex, (f2)wt[ut][2], Hs[c0 + 2]);
-        Hs[c0 + 3] = __builtin_elementwise_fma(ex, (f2)wt[ut][3], Hs[c0 + 3]);
+#endif
+        Hs[c0] = __builtin_elementwise_fma(ex, (f2)w4[0], Hs[c0]);
+        Hs[c0 + 1] = __builtin_elementwise_fma(ex, (f2)w4[1], Hs[c0 + 1]);
+        Hs[c0 + 2] = __builtin_elementwise_fma(ex, (f2)w4[2], Hs[c0 + 2]);
+        Hs[c0 + 3] = __builtin_elementwise_fma(ex, (f2)w4[3], Hs[c0 + 3]);
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k)
@@ -717,6 +909,35 @@ SelWs sel_ws(const int* sizes, int L, int B, int H, int R, int K) {
   return w;
 }
 
+// Per-phase timing of the fast path (skp_sel_bwd_timing*): when enabled, each single-stream call
+// records 5 events on its stream — before sel_gather, after sel_gather, after sel_dot(h), after
+// the adjoint (sel_adjv / sel_adjw / sel_adj), after sel_dense — into a pool read back by
+// skp_sel_bwd_timing_read.  Off by default (no events recorded).
+struct SelTiming {
+  bool on = false;
+  int n = 0;                       // calls recorded since the last read
+  std::vector<hipEvent_t> ev;      // 5 per call
+};
+SelTiming& sel_timing() {
+  static SelTiming t;
+  return t;
+}
+bool getenv_fork_off() {
+  const char* e = getenv("SKP_SEL_FORK");
+  return !(e && atoi(e) == 1);
+}
+constexpr int SEL_TIMING_MAX_CALLS = 256;
+hipEvent_t* sel_timing_slot() {   // this call's 5 events, or null (off / pool full)
+  SelTiming& t = sel_timing();
+  if (!t.on || t.n >= SEL_TIMING_MAX_CALLS) return nullptr;
+  while ((int)t.ev.size() < 5 * (t.n + 1)) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    t.ev.push_back(e);
+  }
+  return &t.ev[5 * t.n++];
+}
+
 bool fast_path(const int* sizes, int L, int R, int N) {
   if (N % 2 != 0 || N < 2) return false;
   for (int l = 0; l < L; ++l)
@@ -782,12 +1003,35 @@ extern "C" int skp_capture_maps_bwd_sel(const float* const* z_low, const int* si
     t.s[l] = sizes[l];
     t.zoff[l + 1] = t.zoff[l] + (long long)BH * sizes[l] * sizes[l] * K;
   }
+  // r05 default: sel_doth + sel_adjv (the horizontal half of bicubicᵀ in the dot kernel, no R² E
+  // rows in HBM); SKP_SEL_DOTH=0: sel_dot + sel_adjw / sel_adj through E (A/B), read per call
+  const bool doth = [] {
+    const char* e = getenv("SKP_SEL_DOTH");
+    return !(e && atoi(e) == 0);
+  }() && R <= 256;
+  hipEvent_t* tev = getenv_fork_off() ? sel_timing_slot() : nullptr;
+  if (tev) (void)hipEventRecord(tev[0], st);
   hipLaunchKernelGGL(sel_gather_kernel, dim3((unsigned)((t.zoff[L] + 255) / 256)), dim3(256), 0, st, t, L, BH, N, H,
                      sel_tok, K, zsel);
   SKP_LAUNCH_CHECK();
-  hipLaunchKernelGGL(sel_dot_kernel, dim3((unsigned)(L * BH * R)), dim3(std::min(R, 256)),
-                     (size_t)smax * K * sizeof(float), st, t, zsel, BH, R, H, K, sel_tok, gsel, gscale, E, pix);
+  if (tev) (void)hipEventRecord(tev[1], st);
+  if (doth) {
+    int rmax = 1;
+    for (int l = 0; l < L; ++l) rmax = std::max(rmax, R / sizes[l]);
+    const size_t lds = (size_t)(64 + ((smax * K + 3) & ~3) + K * (R + 2 * DOTH_PAD + 2) + K * (R / 4 + 4)) *
+                       sizeof(float);
+    if (rmax <= 8)
+      hipLaunchKernelGGL(sel_doth_kernel<8>, dim3((unsigned)(L * BH * R)), dim3(R), lds, st, t, zsel, BH, R, H, K,
+                         sel_tok, gsel, gscale, smax, E, pix);
+    else
+      hipLaunchKernelGGL(sel_doth_kernel<16>, dim3((unsigned)(L * BH * R)), dim3(R), lds, st, t, zsel, BH, R, H, K,
+                         sel_tok, gsel, gscale, smax, E, pix);
+  } else {
+    hipLaunchKernelGGL(sel_dot_kernel, dim3((unsigned)(L * BH * R)), dim3(std::min(R, 256)),
+                       (size_t)smax * K * sizeof(float), st, t, zsel, BH, R, H, K, sel_tok, gsel, gscale, E, pix);
+  }
   SKP_LAUNCH_CHECK();
+  if (tev) (void)hipEventRecord(tev[2], st);
   // SKP_SEL_FORK=1: the sparse part es = bicubicᵀ(E) (sel_adjw / sel_adj), which needs only E, on a
   // low-priority auxiliary stream concurrently with sel_dense, whose emits then leave es out;
   // sel_es_add_kernel adds it once both are done (bit-identical).  Measured SLOWER at the bench shape
@@ -811,7 +1055,10 @@ extern "C" int skp_capture_maps_bwd_sel(const float* const* z_low, const int* si
     const char* e = getenv("SKP_SEL_ADJ");
     return !(e && atoi(e) == 0);
   }();
-  if (adj_win && R <= 256 && R % 16 == 0) {
+  if (doth) {   // E holds sel_doth's Hs rows [l][bh][k][R][smax]
+    hipLaunchKernelGGL(sel_adjv_kernel, dim3((unsigned)(L * BH * K)), dim3(256),
+                       (size_t)(smax * (R + 1) + R * smax) * sizeof(float), adj_st, t, E, BH, BH * K, smax, R, es);
+  } else if (adj_win && R <= 256 && R % 16 == 0) {
     hipLaunchKernelGGL(sel_adjw_kernel, dim3((unsigned)(L * BH * K)), dim3(R),
                        (size_t)(smax * (R + 1) + R * smax + 3 + 5 * R) * sizeof(float), adj_st, t, E, BH * K, smax, R,
                        es);
@@ -828,8 +1075,10 @@ extern "C" int skp_capture_maps_bwd_sel(const float* const* z_low, const int* si
   if (!aux) {   // single stream: es before sel_dense, which adds it in its emits
     const int rc = launch_adj();
     if (rc != SKP_OK) return rc;
+    if (tev) (void)hipEventRecord(tev[3], st);
   }
   auto finish = [&]() -> int {   // launch the auxiliary sel_adjw, join it, add es at the selected tokens
+    if (tev) (void)hipEventRecord(tev[4], st);
     if (!aux) return SKP_OK;
     const int rc = launch_adj();
     if (rc != SKP_OK) return rc;
@@ -882,4 +1131,29 @@ extern "C" int skp_capture_maps_bwd_sel(const float* const* z_low, const int* si
     SKP_LAUNCH_CHECK();
   }
   return finish();
+}
+
+extern "C" int skp_sel_bwd_timing(int enable) {
+  SelTiming& t = sel_timing();
+  t.on = enable != 0;
+  t.n = 0;
+  return SKP_OK;
+}
+
+extern "C" int skp_sel_bwd_timing_read(double* ms, int* calls) {
+  SKP_CHECK_ARG(ms && calls, "null pointer");
+  SelTiming& t = sel_timing();
+  for (int k = 0; k < 4; ++k) ms[k] = 0.0;
+  for (int c = 0; c < t.n; ++c) {
+    hipEvent_t* e = &t.ev[5 * c];
+    SKP_CHECK_ARG(hipEventSynchronize(e[4]) == hipSuccess, "event sync failed");
+    for (int k = 0; k < 4; ++k) {
+      float v = 0.0f;
+      SKP_CHECK_ARG(hipEventElapsedTime(&v, e[k], e[k + 1]) == hipSuccess, "elapsed time failed");
+      ms[k] += v;
+    }
+  }
+  *calls = t.n;
+  t.n = 0;
+  return SKP_OK;
 }

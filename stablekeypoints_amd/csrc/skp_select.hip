@@ -363,9 +363,19 @@ __device__ __forceinline__ void block_sum_n(double (&v)[N], double* sd) {
 // window only (≈33² pixels at σ = 2, re-read from L2).  Agrees with the per-pixel kernel above to
 // fp32 rounding (≈3e-7 absolute on KL ≈ 5, tests/test_gpu_parity.py); rows of HW ≤ 4·NV·BT
 // floats, 16-B aligned, HW % 4 == 0 (the launcher checks); blockIdx.x = row of a (rows, HW) stack.
+// r05: with `out` set, the top_k of each image's keys is fused behind the rows (one launch for the
+// A8 call): every block bumps its image's arrival counter (device-scope atomic) once its key is
+// stored at the coherence point; the image's LAST block reads the T keys from there into LDS and ranks
+// them as rank_topk_kernel does (same strict order: NaN last, ties by index, so the same indices),
+// then re-arms the counter for the next launch.  Counters: kTopkFusedMax per library, zero at load;
+// one fused launch at a time per device (the callers' single compute stream).
+constexpr int kTopkFusedMax = 1024;
+__device__ int g_topk_arrivals[kTopkFusedMax];
+
 template <int BT, int NV>
 __global__ __launch_bounds__(BT) void kl_gauss_win_kernel(const float* __restrict__ maps, int h, int w, float two_sig2,
-                                                         float eps, int wr, double* __restrict__ kl) {
+                                                         float eps, int wr, double* __restrict__ kl, int T = 0,
+                                                         int top_k = 0, long long* __restrict__ out = nullptr) {
   __shared__ float sv[BT / 64];
   __shared__ int si[BT / 64];
   __shared__ double sd[6 * (BT / 64)];
@@ -437,8 +447,38 @@ __global__ __launch_bounds__(BT) void kl_gauss_win_kernel(const float* __restric
     const double St = red[2] + nO * e;
     const double Stl = red[3] + (nO > 0.0 ? nO * e * (double)logf(eps) : 0.0);
     const double Stu = red[4] + e * (red[1] - red[5]);
-    kl[blockIdx.x] = (Stl - Stu) / St - log(St) + log(red[0]);
+    const double key = (Stl - Stu) / St - log(St) + log(red[0]);
+    if (out == nullptr) {
+      kl[blockIdx.x] = key;
+    } else {
+      // the key goes to the device's coherence point (agent-scope atomic store) and is acknowledged
+      // before the arrival is counted, so the image's last block — on any XCD — reads it there; no
+      // L2-wide release fence per block (measured: one per block made the launch 4x longer)
+      __hip_atomic_store(kl + blockIdx.x, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_s_waitcnt(0);
+    }
   }
+  if (out == nullptr) return;   // uniform
+  __shared__ int last;
+  const int b = blockIdx.x / T;
+  if (threadIdx.x == 0) last = atomicAdd(&g_topk_arrivals[b], 1) == T - 1;   // device scope
+  __syncthreads();
+  if (!last) return;
+  extern __shared__ __attribute__((aligned(16))) double ks[];   // T keys
+  double* kb = kl + (size_t)b * T;
+  for (int i = threadIdx.x; i < T; i += BT) ks[i] = __hip_atomic_load(kb + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  for (int i = threadIdx.x; i < T; i += BT) {
+    const double ki = ks[i];
+    const bool ni = isnan(ki);
+    int r = 0;
+    for (int j = 0; j < T; ++j) {   // every lane reads the same ks[j]: LDS broadcast
+      const double kj = ks[j];      // NaN kj compares false: never before a number
+      r += ni ? ((!isnan(kj) || j < i) ? 1 : 0) : ((kj < ki || (kj == ki && j < i)) ? 1 : 0);
+    }
+    if (r < top_k) out[(size_t)b * top_k + r] = i;
+  }
+  if (threadIdx.x == 0) g_topk_arrivals[b] = 0;   // re-armed for the next launch
 }
 
 // entropy of softmax(map) (ptp_utils.py:179-182; torch Categorical renormalises and clamps)
@@ -797,12 +837,24 @@ extern "C" int skp_topk_gaussian_batch(const float* maps, int nb, int T, int h, 
       const double r = ceil(sqrt((double)two_sig2 * kk));
       if (r < (double)wr) wr = (int)r;
     }
+    // the top-k fused behind the KL rows (SKP_TOPK_FUSED=0, or SKP_TOPK_SORT=1: separate launch, A/B)
+    const bool fused = top_k > 0 && nb <= kTopkFusedMax && T <= 4096 && [] {
+      const char* e = getenv("SKP_TOPK_FUSED");
+      const char* f = getenv("SKP_TOPK_SORT");
+      return !(e && atoi(e) == 0) && !(f && atoi(f) == 1);
+    }();
+    const size_t lds = fused ? (size_t)T * sizeof(double) : 0;
+    long long* fo = fused ? out : nullptr;
     if (HW <= 4 * 16 * 256)
-      hipLaunchKernelGGL((kl_gauss_win_kernel<256, 16>), dim3(rows), dim3(256), 0, st, maps, h, w, two_sig2, epsilon,
-                         wr, keys);
+      hipLaunchKernelGGL((kl_gauss_win_kernel<256, 16>), dim3(rows), dim3(256), lds, st, maps, h, w, two_sig2, epsilon,
+                         wr, keys, T, top_k, fo);
     else
-      hipLaunchKernelGGL((kl_gauss_win_kernel<1024, 16>), dim3(rows), dim3(1024), 0, st, maps, h, w, two_sig2, epsilon,
-                         wr, keys);
+      hipLaunchKernelGGL((kl_gauss_win_kernel<1024, 16>), dim3(rows), dim3(1024), lds, st, maps, h, w, two_sig2,
+                         epsilon, wr, keys, T, top_k, fo);
+    SKP_LAUNCH_CHECK();
+    if (fused) return SKP_OK;
+    if (top_k == 0) return SKP_OK;
+    return launch_sort(keys, T, top_k, out, st, nb);
   } else if (reg && HW <= 4 * 1 * kRowThreads)
     hipLaunchKernelGGL(kl_gauss_reg_kernel<1>, dim3(rows), dim3(kRowThreads), 0, st, maps, h, w, num_subjects,
                        radius2, two_sig2, epsilon, keys);

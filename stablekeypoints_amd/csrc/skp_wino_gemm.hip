@@ -28,14 +28,16 @@ __device__ constexpr float kAt[4][6] = {{1.f, 1.f, 1.f, 1.f, 1.f, 0.f},
                                         {0.f, 1.f, 1.f, 0.25f, 4.f, 0.f},
                                         {0.f, 1.f, -1.f, 0.125f, -8.f, 1.f}};
 
-// one thread per (channel, tile); a block's threads take consecutive tiles of one channel, so the
-// 36 stores per thread are coalesced runs over t and the patch loads overlap between neighbours
+// one thread per (channel, tile), flattened channel-major: consecutive threads take consecutive
+// tiles of a channel (then the next channel's), so the 36 stores per thread are coalesced runs over
+// t, the patch loads overlap between neighbours, and blocks stay full when a channel has fewer
+// than 256 tiles (the UNet's 16² / 8² layers: 128 / 32 tiles at batch 8)
 __global__ __launch_bounds__(256) void wino_in_kernel(const float* __restrict__ x, int B, int C, int H, int W,
                                                       float* __restrict__ V) {
   const int tw = W >> 2, th = H >> 2, T = B * th * tw;
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  const int c = blockIdx.y;
-  if (t >= T) return;
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long long)C * T) return;
+  const int c = (int)(e / T), t = (int)(e - (long long)c * T);
   const int b = t / (th * tw), r = t - b * th * tw;
   const int ty = r / tw, tx = r - ty * tw;
   const float* xc = x + ((size_t)b * C + c) * H * W;
@@ -142,10 +144,14 @@ __global__ __launch_bounds__(256) void wino_out_kt_kernel(const float* __restric
                                                           const float* __restrict__ res, float* __restrict__ y,
                                                           float2* __restrict__ gnp) {
   const int tw = W >> 2, th = H >> 2, P = th * tw, T = B * P;
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  const int k = blockIdx.y;
-  const bool live = t < T;
-  const int tt = live ? t : T - 1;
+  // flattened (k, t), k-major: full blocks below 256 tiles per channel; a GroupNorm segment (an
+  // aligned run of min(P, 64) tiles of one plane) stays inside a wave since K·T, T and P are
+  // multiples of it
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = e < (long long)K * T;
+  const long long ee = live ? e : (long long)K * T - 1;
+  const int k = (int)(ee / T);
+  const int tt = (int)(ee - (long long)k * T);
   const int b = tt / P, r = tt - b * P;
   const int ty = r / tw, tx = r - ty * tw;
   const size_t ps = (size_t)K * T;
@@ -225,8 +231,8 @@ extern "C" int skp_wino_in_transform(const float* x, int B, int C, int H, int W,
   SKP_CHECK_ARG(C <= 65535, "C > 65535");
   const long long T = (long long)B * (H / 4) * (W / 4);
   SKP_CHECK_ARG(T * C * 36 < (1LL << 40), "too large");
-  hipLaunchKernelGGL(wino_in_kernel, dim3((unsigned)((T + 255) / 256), C), dim3(256), 0, as_stream(stream), x, B, C, H, W,
-                     V);
+  hipLaunchKernelGGL(wino_in_kernel, dim3((unsigned)((T * C + 255) / 256)), dim3(256), 0, as_stream(stream), x, B, C, H,
+                     W, V);
   SKP_LAUNCH_CHECK();
   return SKP_OK;
 }
@@ -260,7 +266,8 @@ extern "C" int skp_wino_out_transform_kt(const float* M, int B, int K, int H, in
   SKP_CHECK_ARG(T < (1LL << 31), "too many tiles");
   SKP_CHECK_ARG(!gn_part || ((P == 16 || P == 32 || P % 64 == 0) && (reinterpret_cast<uintptr_t>(gn_part) & 7) == 0),
                 "gn_part: tiles per plane must be 16, 32 or a multiple of 64; 8-B aligned");
-  hipLaunchKernelGGL(wino_out_kt_kernel, dim3((unsigned)((T + 255) / 256), K), dim3(256), 0, as_stream(stream), M, B,
+  SKP_CHECK_ARG(T * K < (1LL << 40), "too large");
+  hipLaunchKernelGGL(wino_out_kt_kernel, dim3((unsigned)((T * K + 255) / 256)), dim3(256), 0, as_stream(stream), M, B,
                      K, H, W, bias, residual, y, reinterpret_cast<float2*>(gn_part));
   SKP_LAUNCH_CHECK();
   return SKP_OK;

@@ -690,6 +690,11 @@ def find_top_k_gaussian(maps, top_k, sigma=3, epsilon=1e-5, num_subjects=1, retu
     return (out, kl) if return_kl else out
 
 
+# the A8 top-k fused behind the KL kernel (default) or as its own launch (SKP_TOPK_FUSED=0, A/B;
+# libskp reads the variable per call, tests switch both)
+A8_FUSED = os.environ.get("SKP_TOPK_FUSED", "1") != "0"
+
+
 def find_top_k_gaussian_batch(maps, top_k, sigma=3, epsilon=1e-5, num_subjects=1):
     """find_top_k_gaussian of every image of a (nb, T, h, w) stack in one launch each for the KL
     ranking and the sort: (nb, top_k) int64, row b = find_top_k_gaussian(maps[b], ...)."""
@@ -699,8 +704,14 @@ def find_top_k_gaussian_batch(maps, top_k, sigma=3, epsilon=1e-5, num_subjects=1
     top_k = min(int(top_k), T)
     out = torch.empty(nb, top_k, device=maps.device, dtype=torch.int64)
     kl = torch.empty(nb, T, device=maps.device, dtype=torch.float64)
-    # the KL ranking (algorithmic bytes: every map read once, the keys written) and the top-k of the
-    # keys as two launches, timed apart in the bench's kernels block
+    if A8_FUSED and top_k > 0:
+        # one launch: the KL rows, each image's top-k ranked by its last block (libskp r05)
+        with _timed("skp_topk_gaussian_batch", maps.numel() * 4 + nb * T * 8):
+            call("skp_topk_gaussian_batch", ptr(maps), nb, T, h, w, int(top_k), float(sigma), float(epsilon),
+                 int(num_subjects), ptr(out), ptr(kl), ptr(kl), stream(maps.device))
+        return out
+    # SKP_TOPK_FUSED=0 (A/B): the KL ranking (algorithmic bytes: every map read once, the keys
+    # written) and the top-k of the keys as two launches, timed apart in the bench's kernels block
     with _timed("skp_topk_gaussian_batch", maps.numel() * 4 + nb * T * 8):
         call("skp_topk_gaussian_batch", ptr(maps), nb, T, h, w, 0, float(sigma), float(epsilon),
              int(num_subjects), ptr(out), ptr(kl), ptr(kl), stream(maps.device))
