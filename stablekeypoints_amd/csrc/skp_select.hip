@@ -468,13 +468,24 @@ __global__ __launch_bounds__(BT) void kl_gauss_win_kernel(const float* __restric
   double* kb = kl + (size_t)b * T;
   for (int i = threadIdx.x; i < T; i += BT) ks[i] = __hip_atomic_load(kb + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
+  const int Te = T & ~1;
+  const double2* ks2 = reinterpret_cast<const double2*>(ks);
   for (int i = threadIdx.x; i < T; i += BT) {
     const double ki = ks[i];
     const bool ni = isnan(ki);
     int r = 0;
-    for (int j = 0; j < T; ++j) {   // every lane reads the same ks[j]: LDS broadcast
-      const double kj = ks[j];      // NaN kj compares false: never before a number
-      r += ni ? ((!isnan(kj) || j < i) ? 1 : 0) : ((kj < ki || (kj == ki && j < i)) ? 1 : 0);
+    // every lane reads the same ks[j]: LDS broadcast; 16-B reads, 8 in flight (the loop is
+    // latency-bound otherwise: one block per image does all T² comparisons)
+#pragma unroll 8
+    for (int j2 = 0; j2 < Te / 2; ++j2) {
+      const double2 kk = ks2[j2];
+      const int j = 2 * j2;
+      r += ni ? ((!isnan(kk.x) || j < i) ? 1 : 0) : ((kk.x < ki || (kk.x == ki && j < i)) ? 1 : 0);
+      r += ni ? ((!isnan(kk.y) || j + 1 < i) ? 1 : 0) : ((kk.y < ki || (kk.y == ki && j + 1 < i)) ? 1 : 0);
+    }
+    if (Te < T) {
+      const double kj = ks[T - 1];   // NaN kj compares false: never before a number
+      r += ni ? ((!isnan(kj) || T - 1 < i) ? 1 : 0) : ((kj < ki || (kj == ki && T - 1 < i)) ? 1 : 0);
     }
     if (r < top_k) out[(size_t)b * top_k + r] = i;
   }
@@ -837,11 +848,14 @@ extern "C" int skp_topk_gaussian_batch(const float* maps, int nb, int T, int h, 
       const double r = ceil(sqrt((double)two_sig2 * kk));
       if (r < (double)wr) wr = (int)r;
     }
-    // the top-k fused behind the KL rows (SKP_TOPK_FUSED=0, or SKP_TOPK_SORT=1: separate launch, A/B)
+    // SKP_TOPK_FUSED=1 (A/B, measured slower): the top-k fused behind the KL rows — 111 vs 45 µs
+    // per call at the bench shape (profiles/r05w_a8_fused_ab.txt): the T same-address arrival
+    // atomics per image serialise at the device's coherence point; default: the separate
+    // ranking launch
     const bool fused = top_k > 0 && nb <= kTopkFusedMax && T <= 4096 && [] {
       const char* e = getenv("SKP_TOPK_FUSED");
       const char* f = getenv("SKP_TOPK_SORT");
-      return !(e && atoi(e) == 0) && !(f && atoi(f) == 1);
+      return (e && atoi(e) == 1) && !(f && atoi(f) == 1);
     }();
     const size_t lds = fused ? (size_t)T * sizeof(double) : 0;
     long long* fo = fused ? out : nullptr;

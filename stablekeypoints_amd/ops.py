@@ -690,9 +690,9 @@ def find_top_k_gaussian(maps, top_k, sigma=3, epsilon=1e-5, num_subjects=1, retu
     return (out, kl) if return_kl else out
 
 
-# the A8 top-k fused behind the KL kernel (default) or as its own launch (SKP_TOPK_FUSED=0, A/B;
-# libskp reads the variable per call, tests switch both)
-A8_FUSED = os.environ.get("SKP_TOPK_FUSED", "1") != "0"
+# the A8 top-k as its own ranking launch (default) or fused behind the KL kernel (SKP_TOPK_FUSED=1,
+# A/B, measured slower: profiles/r05w_a8_fused_ab.txt; libskp reads the variable per call)
+A8_FUSED = os.environ.get("SKP_TOPK_FUSED", "0") == "1"
 
 
 def find_top_k_gaussian_batch(maps, top_k, sigma=3, epsilon=1e-5, num_subjects=1):
@@ -704,20 +704,17 @@ def find_top_k_gaussian_batch(maps, top_k, sigma=3, epsilon=1e-5, num_subjects=1
     top_k = min(int(top_k), T)
     out = torch.empty(nb, top_k, device=maps.device, dtype=torch.int64)
     kl = torch.empty(nb, T, device=maps.device, dtype=torch.float64)
-    if A8_FUSED and top_k > 0:
-        # one launch: the KL rows, each image's top-k ranked by its last block (libskp r05)
-        with _timed("skp_topk_gaussian_batch", maps.numel() * 4 + nb * T * 8):
+    # the whole A8 call (algorithmic bytes: every map read once, the keys written) in one timed
+    # scope: the KL ranking launch and the ranking of the keys (or, SKP_TOPK_FUSED=1, one launch)
+    with _timed("skp_topk_gaussian_batch", maps.numel() * 4 + nb * T * 8):
+        if A8_FUSED and top_k > 0:
             call("skp_topk_gaussian_batch", ptr(maps), nb, T, h, w, int(top_k), float(sigma), float(epsilon),
                  int(num_subjects), ptr(out), ptr(kl), ptr(kl), stream(maps.device))
-        return out
-    # SKP_TOPK_FUSED=0 (A/B): the KL ranking (algorithmic bytes: every map read once, the keys
-    # written) and the top-k of the keys as two launches, timed apart in the bench's kernels block
-    with _timed("skp_topk_gaussian_batch", maps.numel() * 4 + nb * T * 8):
-        call("skp_topk_gaussian_batch", ptr(maps), nb, T, h, w, 0, float(sigma), float(epsilon),
-             int(num_subjects), ptr(out), ptr(kl), ptr(kl), stream(maps.device))
-    if top_k > 0:
-        with _timed("skp_topk_keys", nb * T * 8 + nb * top_k * 8):
-            call("skp_topk_keys", ptr(kl), nb, T, int(top_k), ptr(out), stream(maps.device))
+        else:
+            call("skp_topk_gaussian_batch", ptr(maps), nb, T, h, w, 0, float(sigma), float(epsilon),
+                 int(num_subjects), ptr(out), ptr(kl), ptr(kl), stream(maps.device))
+            if top_k > 0:
+                call("skp_topk_keys", ptr(kl), nb, T, int(top_k), ptr(out), stream(maps.device))
     return out
 
 

@@ -250,10 +250,10 @@ def test_topk_keys_rank_kernel_vs_stable_argsort(nb, Tn, top_k):
 
 @pytest.mark.parametrize("nb,Tn,R", [(4, 500, 128), (1, 37, 32), (3, 129, 32)])
 def test_topk_gaussian_fused_equals_separate_launch(monkeypatch, nb, Tn, R):
-    """The A8 call as ONE launch (r05 default: each image's last KL block ranks the image's keys,
-    arrival counters re-armed per launch) selects exactly what the KL launch + skp_topk_keys
-    select, on maps with duplicated rows (equal keys: ties by index) and NaN rows (NaN last), at
-    top_k 1, 25 and T, twice in a row (the counters' re-arming)."""
+    """The A8 call as ONE launch (SKP_TOPK_FUSED=1, A/B option: each image's last KL block ranks the
+    image's keys, arrival counters re-armed per launch) selects exactly what the default KL launch +
+    skp_topk_keys select, on maps with duplicated rows (equal keys: ties by index) and NaN rows
+    (NaN last), at top_k 1, 25 and T, twice in a row (the counters' re-arming)."""
     from stablekeypoints_amd import ops
     maps = np.stack([recipes.attention_like_maps(200 + i, Tn, R) for i in range(nb)]).astype(np.float32)
     maps[:, 3] = maps[:, 1]
@@ -261,9 +261,11 @@ def test_topk_gaussian_fused_equals_separate_launch(monkeypatch, nb, Tn, R):
     mt = T(maps)
     for k in sorted({1, min(25, Tn), Tn}):
         monkeypatch.setattr(ops, "A8_FUSED", True)
+        monkeypatch.setenv("SKP_TOPK_FUSED", "1")   # libskp reads it per call
         a = ops.find_top_k_gaussian_batch(mt, k, sigma=2.0)
         b = ops.find_top_k_gaussian_batch(mt, k, sigma=2.0)
         monkeypatch.setattr(ops, "A8_FUSED", False)
+        monkeypatch.setenv("SKP_TOPK_FUSED", "0")
         c = ops.find_top_k_gaussian_batch(mt, k, sigma=2.0)
         assert torch.equal(a, b) and torch.equal(a, c), k
 
