@@ -1820,7 +1820,7 @@ def conv1x1(x, weight):
 
 # A/B: 0 = the VAE's stride-2 downsampling convolutions run as F.pad + MIOpen (r02)
 WINO_S2 = os.environ.get("SKP_WINO_S2", "1") != "0"
-WINO_S2_MIN_PIXELS = 384 * 384
+WINO_S2_MIN_PIXELS = int(os.environ.get("SKP_WINO_S2_MIN", str(384 * 384)))   # A/B: SKP_WINO_S2_MIN=65536 adds 256²
 
 
 def conv3x3_s2_eligible(x, weight):
