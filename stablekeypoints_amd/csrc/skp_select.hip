@@ -492,6 +492,99 @@ __global__ __launch_bounds__(BT) void kl_gauss_win_kernel(const float* __restric
   if (threadIdx.x == 0) g_topk_arrivals[b] = 0;   // re-armed for the next launch
 }
 
+// r05: kl_gauss_win_kernel's arithmetic streamed instead of held: each thread walks its float4s in
+// chunks of UNR with a running max of fl(v + eps) and Σ exp relative to it (rescaled by one exp2 when
+// a chunk raises the max; threads combine as Σ s_t·exp(m_t − M)), Σ fl(v + eps) for Σu = Σx − HW·M,
+// and the argmax as before.  ≈40 VGPRs instead of 83 (the row in registers), so a 128² row's block
+// of 4 waves fits 8 per CU and a pass's 4 × 500 rows run in one wave of blocks: the maps stream at
+// HBM rate.  Same window terms, same closed form; the sums round differently from the held form
+// (Σu by ≤ HW·ulp ≈ 1e-3 absolute, entering KL scaled by eps/S_t ≈ 4e-7: ≈ 1e-10), indices
+// bit-exact on the goldens (tests/test_gpu_parity.py).
+template <int BT, int UNR>
+__global__ __launch_bounds__(BT) void kl_gauss_stream_kernel(const float* __restrict__ maps, int h, int w,
+                                                            float two_sig2, float eps, int wr,
+                                                            double* __restrict__ kl) {
+  __shared__ float sv[BT / 64];
+  __shared__ int si[BT / 64];
+  __shared__ double sd[6 * (BT / 64)];
+  constexpr float L2E = 1.4426950408889634f;
+  const int HW = h * w, nq = HW >> 2;
+  const float* row = maps + (size_t)blockIdx.x * HW;
+  const float4* m4 = reinterpret_cast<const float4*>(row);
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+  float m = -INFINITY;      // running max of fl(v + eps) over this thread's elements
+  double se = 0.0, sx = 0.0;  // Σ exp(x − m) (relative to the running m), Σ x
+  for (int q0 = threadIdx.x; q0 < nq; q0 += BT * UNR) {
+    float4 v[UNR];
+#pragma unroll
+    for (int k = 0; k < UNR; ++k) {
+      const int q = q0 + k * BT;
+      v[k] = q < nq ? m4[q] : make_float4(NAN, NAN, NAN, NAN);
+    }
+    float cm = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < UNR; ++k) {
+      const int q = q0 + k * BT;
+      if (q < nq) {
+        const float x[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if (x[c] > best || (isnan(x[c]) && !isnan(best))) { best = x[c]; bi = 4 * q + c; }
+          cm = fmaxf(cm, x[c] + eps);
+        }
+      }
+    }
+    if (cm > m) {   // the chunk raised the running max: rescale the sum once
+      se *= (double)__builtin_amdgcn_exp2f((m - cm) * L2E);
+      m = cm;
+    }
+#pragma unroll
+    for (int k = 0; k < UNR; ++k) {
+      const int q = q0 + k * BT;
+      if (q < nq) {
+        const float x0 = v[k].x + eps, x1 = v[k].y + eps, x2 = v[k].z + eps, x3 = v[k].w + eps;
+        const float e0 = __builtin_amdgcn_exp2f((x0 - m) * L2E), e1 = __builtin_amdgcn_exp2f((x1 - m) * L2E);
+        const float e2 = __builtin_amdgcn_exp2f((x2 - m) * L2E), e3 = __builtin_amdgcn_exp2f((x3 - m) * L2E);
+        se += (double)((e0 + e1) + (e2 + e3));
+        sx += (double)((x0 + x1) + (x2 + x3));
+      }
+    }
+  }
+  block_argmax(best, bi, sv, si);
+  // the running maxima's maximum is fl(max v + eps) (rounding is monotonic): the argmax reduction
+  // already carries it (a NaN row: mx is NaN, so is every sum, as in the held form)
+  const float mx = best + eps;
+  se *= (double)__builtin_amdgcn_exp2f((m - mx) * L2E);   // m = −inf (no elements): 0 · 0
+  const float p0 = (((float)(bi / w) + 0.5f) / (float)h) * (float)h;
+  const float p1 = (((float)(bi % w) + 0.5f) / (float)h) * (float)h;
+  const int c0 = (int)floorf(p0), c1 = (int)floorf(p1);
+  const int i0 = max(0, c0 - wr), i1 = min(h - 1, c0 + wr);
+  const int j0 = max(0, c1 - wr), j1 = min(w - 1, c1 + wr);
+  const int ww = j1 - j0 + 1, nW = (i1 - i0 + 1) * ww;
+  double win[4] = {0.0, 0.0, 0.0, 0.0};   // Σ_W t, Σ_W t·log t, Σ_W t·u, Σ_W u
+  for (int k = threadIdx.x; k < nW; k += BT) {
+    const int i = i0 + k / ww, jj = j0 + k % ww;
+    const float di = ((float)i + 0.5f) - p0, dj = ((float)jj + 0.5f) - p1;
+    const float t = expf(-(dj * dj + di * di) / two_sig2) + eps;
+    const float u = (row[i * w + jj] + eps) - mx;
+    win[0] += (double)t;
+    win[1] += (double)t * (double)logf(t);
+    win[2] += (double)t * (double)u;
+    win[3] += (double)u;
+  }
+  double red[6] = {se, sx, win[0], win[1], win[2], win[3]};
+  block_sum_n<6>(red, sd);
+  if (threadIdx.x == 0) {
+    const double e = (double)eps, nO = (double)(HW - nW);
+    const double su = red[1] - (double)HW * (double)mx;   // Σ u over the row
+    const double St = red[2] + nO * e;
+    const double Stl = red[3] + (nO > 0.0 ? nO * e * (double)logf(eps) : 0.0);
+    const double Stu = red[4] + e * (su - red[5]);
+    kl[blockIdx.x] = (Stl - Stu) / St - log(St) + log(red[0]);
+  }
+}
+
 // entropy of softmax(map) (ptp_utils.py:179-182; torch Categorical renormalises and clamps)
 __global__ __launch_bounds__(kRowThreads) void entropy_kernel(const float* __restrict__ maps, int h, int w,
                                                            double* __restrict__ ent) {
@@ -859,7 +952,36 @@ extern "C" int skp_topk_gaussian_batch(const float* maps, int nb, int T, int h, 
     }();
     const size_t lds = fused ? (size_t)T * sizeof(double) : 0;
     long long* fo = fused ? out : nullptr;
-    if (HW <= 4 * 16 * 256)
+    // r05 default for rows up to 128²: the streamed form (SKP_KL_STREAM=0: the held form, A/B)
+    const bool stream = !fused && HW <= 4 * 16 * 256 && [] {
+      const char* e = getenv("SKP_KL_STREAM");
+      return !(e && atoi(e) == 0);
+    }();
+    // float4 per thread per chunk and threads per row (A/B: SKP_KL_UNR = 1 / 2 / 4, SKP_KL_BT = 128 /
+    // 256, read per call); default 1 × 256: kbench kl4 39.4 µs vs 40.0–40.9 (2 × 256), 42.0 (4 × 256),
+    // 44.5–44.9 for the held form (profiles/r05zb_kl_stream_ab.txt)
+    const int unr = [] {
+      const char* e = getenv("SKP_KL_UNR");
+      const int v = e ? atoi(e) : 1;
+      return (v == 2 || v == 4) ? v : 1;
+    }();
+    const int bt = [] {
+      const char* e = getenv("SKP_KL_BT");
+      return (e && atoi(e) == 128) ? 128 : 256;
+    }();
+#define SKP_KL_STREAM_CASE(BT_, U_)                                                                          \
+    else if (stream && bt == BT_ && unr == U_) hipLaunchKernelGGL((kl_gauss_stream_kernel<BT_, U_>), dim3(rows), \
+                                                                  dim3(BT_), 0, st, maps, h, w, two_sig2, epsilon, wr, keys);
+    if (false) {
+    }
+    SKP_KL_STREAM_CASE(256, 2)
+    SKP_KL_STREAM_CASE(256, 1)
+    SKP_KL_STREAM_CASE(256, 4)
+    SKP_KL_STREAM_CASE(128, 2)
+    SKP_KL_STREAM_CASE(128, 1)
+    SKP_KL_STREAM_CASE(128, 4)
+#undef SKP_KL_STREAM_CASE
+    else if (HW <= 4 * 16 * 256)
       hipLaunchKernelGGL((kl_gauss_win_kernel<256, 16>), dim3(rows), dim3(256), lds, st, maps, h, w, two_sig2, epsilon,
                          wr, keys, T, top_k, fo);
     else

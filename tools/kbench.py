@@ -86,10 +86,11 @@ def main():
             res[name] = timed(lambda: torch.autograd.grad(maps, z8, gm, retain_graph=True), args.iters)
             ops.FUSED_MAPS = True
             del z8, maps, gm
-        elif name in ("mapssel8", "mapssel8_dense"):   # sparse backward of 10 selected rows per image, bench shape
-            sizes = (16, 16, 16, 32)
+        elif name in ("mapssel8", "mapssel8_dense", "mapssel8_s16", "mapssel8_s32"):
+            # sparse backward of 10 selected rows per image, bench shape (_s16 / _s32: one layer class)
+            sizes = {"mapssel8_s16": (16, 16, 16), "mapssel8_s32": (32,)}.get(name, (16, 16, 16, 32))
             z8 = [(torch.randn(8 * H, s * s, N, device=dev, generator=g) * 2).requires_grad_(True) for s in sizes]
-            ops.SEL_BWD = name == "mapssel8"
+            ops.SEL_BWD = name != "mapssel8_dense"
             cm = ops.CapturedMaps(z8, sizes, 8, R)
             rows = [torch.randperm(N, device=dev, generator=g)[:10] for _ in range(8)]
             out = cm.select(rows)
