@@ -494,6 +494,9 @@ struct SelLayers {   // up to 4 layers of the same s per launch
 
 // output columns per band and row: 16 where R/s ≥ 8; 8 at R/s = 4 (the s = 32 layers), which keeps
 // the band at 6 low-res columns and the registers under 128 (4 waves per SIMD)
+#ifndef SKP_SEL_LW4
+#define SKP_SEL_LW4 32   // lanes per band at R/s = 4 (A/B build: 64 = whole-wave bands, 16-wave blocks)
+#endif
 template <int RATIO>
 constexpr int sel_pw() { return RATIO >= 8 ? 16 : 8; }
 template <int RATIO>
@@ -502,7 +505,7 @@ constexpr int sel_nc() { return lo_rel(sel_pw<RATIO>() - 1, RATIO) + 6; }   // b
 // holds 2·R/PW bands in R/PW/2 waves (64-token chunks): the s = 32 block then needs 8 waves and
 // 57 KB of LDS like the s = 16 one, two share a CU, and one launch runs both (sel_dense_pair)
 template <int RATIO>
-constexpr int sel_lw() { return RATIO >= 8 ? 64 : 32; }
+constexpr int sel_lw() { return RATIO >= 8 ? 64 : SKP_SEL_LW4; }
 template <int RATIO, int S>
 constexpr int sel_threads() { return (S * RATIO / sel_pw<RATIO>()) * sel_lw<RATIO>(); }
 template <int RATIO, int S>
@@ -808,7 +811,7 @@ bool dense_launch(int R, int S, const SelLayers& sl, int nl, int BH, int H, int 
 // the SD-1.5 capture layers at R = 128 (s = 16 ×3 and s = 32) as one sel_dense_pair launch
 bool dense_pair_launch(int R, int SA, const SelLayers& sa, int na, int SB, const SelLayers& sb, int nb, int BH, int H,
                        int N, int K, const long long* tok, hipStream_t st) {
-  if (!SKP_SEL_PAIR) return false;
+#if SKP_SEL_PAIR && SKP_SEL_LW4 == 32
   if (R == 128 && SA == 16 && SB == 32) {
     launch_dense_pair<128, 16, 128, 32>(sa, na, sb, nb, BH, H, N, K, tok, st);
     return true;
@@ -817,6 +820,7 @@ bool dense_pair_launch(int R, int SA, const SelLayers& sa, int na, int SB, const
     launch_dense_pair<128, 16, 128, 32>(sb, nb, sa, na, BH, H, N, K, tok, st);
     return true;
   }
+#endif
   return false;
 }
 
