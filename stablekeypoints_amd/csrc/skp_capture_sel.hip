@@ -495,7 +495,8 @@ struct SelLayers {   // up to 4 layers of the same s per launch
 // output columns per band and row: 16 where R/s ≥ 8; 8 at R/s = 4 (the s = 32 layers), which keeps
 // the band at 6 low-res columns and the registers under 128 (4 waves per SIMD)
 #ifndef SKP_SEL_LW4
-#define SKP_SEL_LW4 32   // lanes per band at R/s = 4 (A/B build: 64 = whole-wave bands, 16-wave blocks)
+#define SKP_SEL_LW4 32   // lanes per band at R/s = 4 (A/B build: 64 = whole-wave bands in 16-wave blocks, the s = 16
+                         // jobs then two per block in the paired grid: bit-identical, slower, profiles/r05zf_sel_dual_ab.txt)
 #endif
 template <int RATIO>
 constexpr int sel_pw() { return RATIO >= 8 ? 16 : 8; }
@@ -521,7 +522,8 @@ constexpr int sel_lds_z() { return 4 * (S + 4) * sel_lw<RATIO>(); }             
 // (the vertical adjoint of the 4 rows) and the per-row V / Hs stay in registers.
 template <int RATIO, int S>
 __device__ __forceinline__ void sel_dense_body(const SelLayers& sl, int BH, int H, int N, int K,
-                                               const long long* __restrict__ tok, int nchunk, int job, f2* M, f2* Z) {
+                                               const long long* __restrict__ tok, int nchunk, int job, f2* M, f2* Z,
+                                               int tid0) {
   constexpr int PW = sel_pw<RATIO>();
   constexpr int LW = sel_lw<RATIO>();
   constexpr int R = S * RATIO;
@@ -535,7 +537,7 @@ __device__ __forceinline__ void sel_dense_body(const SelLayers& sl, int BH, int 
   const int bh = (job / nchunk) % BH;
   const int l = job / (nchunk * BH);
   const int b = bh / H;
-  const int tid = threadIdx.x, lane = tid & (LW - 1);
+  const int tid = tid0, lane = tid & (LW - 1);   // the thread's index within its job's threads
   // band of this thread: the wave (uniform) or, at LW = 32, the wave's half
   const int bw = LW == WAVE ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid / LW;
   const int n0 = chunk * TPC + 2 * lane;
@@ -737,30 +739,45 @@ void sel_dense_kernel(SelLayers sl, int BH, int H, int N, int K, const long long
   __shared__ __attribute__((aligned(16))) f2 Z[sel_lds_z<RATIO, S>()];   // ring of 4 low-res z rows
   const int job = xcd_job(njobs);
   if (job >= njobs) return;
-  sel_dense_body<RATIO, S>(sl, BH, H, N, K, tok, nchunk, job, M, Z);
+  sel_dense_body<RATIO, S>(sl, BH, H, N, K, tok, nchunk, job, M, Z, threadIdx.x);
 }
 
 // Two layer classes (e.g. SD-1.5's s = 16 layers and its s = 32 layer at R = 128) in ONE grid of
 // equal-size blocks: per XCD, its share of class A's jobs first, then its share of class B's, so
 // the shorter class-B blocks fill the slots class A's last round leaves idle (two launches left
 // half of the CUs idle in the s = 16 launch's last round and ran the s = 32 launch alone).
+// Two layer classes (e.g. SD-1.5's s = 16 layers and its s = 32 layer at R = 128) in ONE grid of
+// equal-size blocks: per XCD, its share of class A's blocks first, then its share of class B's, so
+// the class-B blocks fill the slots class A's last round leaves idle (two launches left half of the
+// CUs idle in the s = 16 launch's last round and ran the s = 32 launch alone).  A class-A job may
+// need fewer threads than a class-B one: a block then runs DA = threads(B) / threads(A) class-A jobs
+// side by side, each on its own slice of the threads and of the LDS (the jobs of one class run the
+// same barrier sequence; a block's surplus slots redo its last job, storing the same values).
 template <int RA, int SA, int RB, int SB>
-__global__ __launch_bounds__((sel_threads<RA, SA>()))
+__global__ __launch_bounds__((sel_threads<RB, SB>()))
 void sel_dense_pair_kernel(SelLayers sa, int nca, int ja, SelLayers sb, int ncb, int jb, int BH, int H, int N, int K,
                            const long long* __restrict__ tok) {
-  static_assert(sel_threads<RA, SA>() == sel_threads<RB, SB>(), "equal block sizes");
+  constexpr int TA = sel_threads<RA, SA>(), TB = sel_threads<RB, SB>();
+  static_assert(TB % TA == 0, "class-A jobs must tile a class-B block");
+  constexpr int DA = TB / TA;
   constexpr int MA = sel_lds_m<RA, SA>(), MB = sel_lds_m<RB, SB>();
   constexpr int ZA = sel_lds_z<RA, SA>(), ZB = sel_lds_z<RB, SB>();
-  __shared__ __attribute__((aligned(16))) f2 M[MA > MB ? MA : MB];
-  __shared__ __attribute__((aligned(16))) f2 Z[ZA > ZB ? ZA : ZB];
-  const int pa = (ja + 7) / 8, pb = (jb + 7) / 8;   // per-XCD shares
+  constexpr int LA = DA * (MA + ZA), LB = MB + ZB;
+  __shared__ __attribute__((aligned(16))) f2 lds[LA > LB ? LA : LB];
+  const int ba = (ja + DA - 1) / DA;                 // class-A blocks
+  const int pa = (ba + 7) / 8, pb = (jb + 7) / 8;   // per-XCD shares
   const int xcd = blockIdx.x & 7, k = blockIdx.x >> 3;
   if (k < pa) {
-    const int job = xcd * pa + k;
-    if (job < ja) sel_dense_body<RA, SA>(sa, BH, H, N, K, tok, nca, job, M, Z);
+    const int blk = xcd * pa + k;
+    if (blk < ba) {
+      const int d = (int)threadIdx.x / TA;
+      const int job = min(blk * DA + d, ja - 1);
+      f2* M = lds + d * (MA + ZA);
+      sel_dense_body<RA, SA>(sa, BH, H, N, K, tok, nca, job, M, M + MA, (int)threadIdx.x - d * TA);
+    }
   } else {
     const int job = xcd * pb + (k - pa);
-    if (job < jb) sel_dense_body<RB, SB>(sb, BH, H, N, K, tok, ncb, job, M, Z);
+    if (job < jb) sel_dense_body<RB, SB>(sb, BH, H, N, K, tok, ncb, job, lds, lds + MB, threadIdx.x);
   }
 }
 
@@ -779,8 +796,10 @@ void launch_dense_pair(const SelLayers& sa, int na, const SelLayers& sb, int nb,
   const int nca = (N + 2 * sel_lw<RA / SA>() - 1) / (2 * sel_lw<RA / SA>());
   const int ncb = (N + 2 * sel_lw<RB / SB>() - 1) / (2 * sel_lw<RB / SB>());
   const int ja = na * BH * nca, jb = nb * BH * ncb;
-  const int grid = 8 * ((ja + 7) / 8 + (jb + 7) / 8);
-  hipLaunchKernelGGL((sel_dense_pair_kernel<RA / SA, SA, RB / SB, SB>), dim3(grid), dim3(sel_threads<RA / SA, SA>()), 0,
+  constexpr int DA = sel_threads<RB / SB, SB>() / sel_threads<RA / SA, SA>();
+  const int ba = (ja + DA - 1) / DA;
+  const int grid = 8 * ((ba + 7) / 8 + (jb + 7) / 8);
+  hipLaunchKernelGGL((sel_dense_pair_kernel<RA / SA, SA, RB / SB, SB>), dim3(grid), dim3(sel_threads<RB / SB, SB>()), 0,
                      st, sa, nca, ja, sb, ncb, jb, BH, H, N, K, tok);
 }
 
@@ -811,7 +830,7 @@ bool dense_launch(int R, int S, const SelLayers& sl, int nl, int BH, int H, int 
 // the SD-1.5 capture layers at R = 128 (s = 16 ×3 and s = 32) as one sel_dense_pair launch
 bool dense_pair_launch(int R, int SA, const SelLayers& sa, int na, int SB, const SelLayers& sb, int nb, int BH, int H,
                        int N, int K, const long long* tok, hipStream_t st) {
-#if SKP_SEL_PAIR && SKP_SEL_LW4 == 32
+#if SKP_SEL_PAIR
   if (R == 128 && SA == 16 && SB == 32) {
     launch_dense_pair<128, 16, 128, 32>(sa, na, sb, nb, BH, H, N, K, tok, st);
     return true;
