@@ -500,7 +500,7 @@ __global__ __launch_bounds__(BT) void kl_gauss_win_kernel(const float* __restric
 // HBM rate.  Same window terms, same closed form; the sums round differently from the held form
 // (Σu by ≤ HW·ulp ≈ 1e-3 absolute, entering KL scaled by eps/S_t ≈ 4e-7: ≈ 1e-10), indices
 // bit-exact on the goldens (tests/test_gpu_parity.py).
-template <int BT, int UNR>
+template <int BT, int UNR, int PROBE = 0>
 __global__ __launch_bounds__(BT) void kl_gauss_stream_kernel(const float* __restrict__ maps, int h, int w,
                                                             float two_sig2, float eps, int wr,
                                                             double* __restrict__ kl) {
@@ -563,15 +563,33 @@ __global__ __launch_bounds__(BT) void kl_gauss_stream_kernel(const float* __rest
   const int j0 = max(0, c1 - wr), j1 = min(w - 1, c1 + wr);
   const int ww = j1 - j0 + 1, nW = (i1 - i0 + 1) * ww;
   double win[4] = {0.0, 0.0, 0.0, 0.0};   // Σ_W t, Σ_W t·log t, Σ_W t·u, Σ_W u
-  for (int k = threadIdx.x; k < nW; k += BT) {
-    const int i = i0 + k / ww, jj = j0 + k % ww;
-    const float di = ((float)i + 0.5f) - p0, dj = ((float)jj + 0.5f) - p1;
-    const float t = expf(-(dj * dj + di * di) / two_sig2) + eps;
-    const float u = (row[i * w + jj] + eps) - mx;
-    win[0] += (double)t;
-    win[1] += (double)t * (double)logf(t);
-    win[2] += (double)t * (double)u;
-    win[3] += (double)u;
+  // the window's row values re-read 4 per thread at a time (loads in flight together), then its terms
+  // in element order per thread (PROBE: timing probes only)
+  for (int k0 = threadIdx.x; k0 < (PROBE >= 1 ? 0 : nW); k0 += 4 * BT) {
+    float rv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int k = k0 + r * BT;
+      rv[r] = k < nW ? row[(i0 + k / ww) * w + j0 + k % ww] : 0.0f;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int k = k0 + r * BT;
+      if (k < nW) {
+        const int i = i0 + k / ww, jj = j0 + k % ww;
+        const float di = ((float)i + 0.5f) - p0, dj = ((float)jj + 0.5f) - p1;
+        const float t = expf(-(dj * dj + di * di) / two_sig2) + eps;
+        const float u = (rv[r] + eps) - mx;
+        win[0] += (double)t;
+        win[1] += (double)t * (double)logf(t);
+        win[2] += (double)t * (double)u;
+        win[3] += (double)u;
+      }
+    }
+  }
+  if (PROBE >= 2) {
+    if (threadIdx.x == 0) kl[blockIdx.x] = se + sx;
+    return;
   }
   double red[6] = {se, sx, win[0], win[1], win[2], win[3]};
   block_sum_n<6>(red, sd);
@@ -974,6 +992,12 @@ extern "C" int skp_topk_gaussian_batch(const float* maps, int nb, int T, int h, 
                                                                   dim3(BT_), 0, st, maps, h, w, two_sig2, epsilon, wr, keys);
     if (false) {
     }
+    else if (stream && getenv("SKP_KL_PROBE") && atoi(getenv("SKP_KL_PROBE")) == 1)   // timing probes (wrong keys)
+      hipLaunchKernelGGL((kl_gauss_stream_kernel<256, 1, 1>), dim3(rows), dim3(256), 0, st, maps, h, w, two_sig2,
+                         epsilon, wr, keys);
+    else if (stream && getenv("SKP_KL_PROBE") && atoi(getenv("SKP_KL_PROBE")) == 2)
+      hipLaunchKernelGGL((kl_gauss_stream_kernel<256, 1, 2>), dim3(rows), dim3(256), 0, st, maps, h, w, two_sig2,
+                         epsilon, wr, keys);
     SKP_KL_STREAM_CASE(256, 2)
     SKP_KL_STREAM_CASE(256, 1)
     SKP_KL_STREAM_CASE(256, 4)
