@@ -352,6 +352,53 @@ __device__ __forceinline__ void block_sum_n(double (&v)[N], double* sd) {
   for (int k = 0; k < N; ++k) v[k] = sd[k * nw];
 }
 
+// Wave sum of doubles on DPP row steps + the gfx950 permlane swaps (both 32-bit halves moved by the
+// same control; every lane ends with the same bits), instead of six LDS-routed shuffles.
+template <int CTRL>
+__device__ __forceinline__ double dpp_read_d(double v) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  v += dpp_read_d<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_read_d<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_read_d<0x141>(v);   // row_half_mirror
+  v += dpp_read_d<0x140>(v);   // row_mirror
+  const long long b = __builtin_bit_cast(long long, v);
+  int lo = (int)b, hi = (int)(b >> 32), wlo = lo, whi = hi;
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\tv_permlane16_swap_b32 %2, %3"
+               : "+v"(lo), "+v"(wlo), "+v"(hi), "+v"(whi));
+  v = __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo) +
+      __builtin_bit_cast(double, ((long long)whi << 32) | (unsigned)wlo);
+  const long long c = __builtin_bit_cast(long long, v);
+  lo = (int)c; hi = (int)(c >> 32); wlo = lo; whi = hi;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\tv_permlane32_swap_b32 %2, %3"
+               : "+v"(lo), "+v"(wlo), "+v"(hi), "+v"(whi));
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo) +
+         __builtin_bit_cast(double, ((long long)whi << 32) | (unsigned)wlo);
+}
+// Block sum of N doubles for thread 0 only (the wave partials added in wave order, one barrier)
+template <int N>
+__device__ __forceinline__ void block_sum_to0(double (&v)[N], double* sd) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    v[k] = wave_sum_dpp(v[k]);
+    if (lane == 0) sd[k * nw + wid] = v[k];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      double x = sd[k * nw];
+      for (int q = 1; q < nw; ++q) x += sd[k * nw + q];
+      v[k] = x;
+    }
+  }
+}
+
 // KL(target ‖ softmax(map + eps)) per token for ONE subject (ptp_utils.py:97-108), one HBM read
 // of the row.  With u = fl(v + eps) − max (the softmax's shifted logit), t = g + eps the target
 // before normalisation and S_t = Σ t, S_e = Σ exp(u):
@@ -592,7 +639,7 @@ __global__ __launch_bounds__(BT) void kl_gauss_stream_kernel(const float* __rest
     return;
   }
   double red[6] = {se, sx, win[0], win[1], win[2], win[3]};
-  block_sum_n<6>(red, sd);
+  block_sum_to0<6>(red, sd);
   if (threadIdx.x == 0) {
     const double e = (double)eps, nO = (double)(HW - nW);
     const double su = red[1] - (double)HW * (double)mx;   // Σ u over the row
