@@ -139,7 +139,7 @@ def _a8_split(dev, T, R, nb=4, reps=20):
             b.synchronize()
             ts.append(a.elapsed_time(b))
         res[name] = float(np.median(ts))
-    res["workload"] = f"{nb} x ({T}, {R}, {R}) synthetic maps, top_k 25, sigma 2; median of {reps}, after the timed region"
+    res["workload"] = f"{nb} x ({T}, {R}, {R}) synthetic maps, top_k 25, sigma 2; median of {reps}, before the warm-up"
     del maps
     return res
 

@@ -770,10 +770,22 @@ void sel_dense_pair_kernel(SelLayers sa, int nca, int ja, SelLayers sb, int ncb,
   if (k < pa) {
     const int blk = xcd * pa + k;
     if (blk < ba) {
-      const int d = (int)threadIdx.x / TA;
-      const int job = min(blk * DA + d, ja - 1);
-      f2* M = lds + d * (MA + ZA);
-      sel_dense_body<RA, SA>(sa, BH, H, N, K, tok, nca, job, M, M + MA, (int)threadIdx.x - d * TA);
+      if constexpr (DA == 1) {   // compile-time LDS bases (a runtime slice offset costs every LDS access)
+        sel_dense_body<RA, SA>(sa, BH, H, N, K, tok, nca, blk, lds, lds + MA, threadIdx.x);
+      } else if constexpr (DA == 2) {   // each half on its own compile-time LDS slice
+        const int d = __builtin_amdgcn_readfirstlane((int)threadIdx.x / TA);
+        const int job = min(blk * 2 + d, ja - 1);
+        if (d == 0)
+          sel_dense_body<RA, SA>(sa, BH, H, N, K, tok, nca, job, lds, lds + MA, threadIdx.x);
+        else
+          sel_dense_body<RA, SA>(sa, BH, H, N, K, tok, nca, job, lds + (MA + ZA), lds + (2 * MA + ZA),
+                                 (int)threadIdx.x - TA);
+      } else {
+        const int d = (int)threadIdx.x / TA;
+        const int job = min(blk * DA + d, ja - 1);
+        f2* M = lds + d * (MA + ZA);
+        sel_dense_body<RA, SA>(sa, BH, H, N, K, tok, nca, job, M, M + MA, (int)threadIdx.x - d * TA);
+      }
     }
   } else {
     const int job = xcd * pb + (k - pa);
