@@ -174,7 +174,7 @@ __global__ __launch_bounds__(256) void sel_dot_kernel(SelSmall t, const float* _
 constexpr int DOTH_PAD = 64;   // zero floats each side of a row's e (≥ 3.5·RATIO at RATIO ≤ 16)
 
 // virtual columns c = cv − 2, cv ∈ [0, S + 4): Vc[cv][k] = Σ_t W[t]·e_k[RATIO·(c − 2) + RATIO/2 + t]
-// (one fixed-length dot product per lane, lanes over k first: rows k sit 2 banks apart)
+// (one fixed-length dot product per lane, lanes over k first: rows k sit 4 banks apart)
 template <int RATIO>
 __device__ __forceinline__ void doth_columns(const float* __restrict__ W, const float* __restrict__ Ep, int EP, int K,
                                              int S, float* __restrict__ Vc) {
@@ -186,8 +186,25 @@ __device__ __forceinline__ void doth_columns(const float* __restrict__ W, const 
     const int k = e % K, cv = e / K;
     const float* src = Ep + k * EP + DOTH_PAD + RATIO / 2 - 4 * RATIO + RATIO * cv;
     float a = 0.0f;
+    if constexpr (RATIO >= 8) {   // 16-B aligned runs (EP, DOTH_PAD and RATIO/2 multiples of 4)
+      const float4* s4 = reinterpret_cast<const float4*>(src);
 #pragma unroll
-    for (int q = 0; q < NT; ++q) a = fmaf(w[q], src[q], a);
+      for (int q = 0; q < NT / 4; ++q) {
+        const float4 v = s4[q];
+        a = fmaf(w[4 * q], v.x, a);
+        a = fmaf(w[4 * q + 1], v.y, a);
+        a = fmaf(w[4 * q + 2], v.z, a);
+        a = fmaf(w[4 * q + 3], v.w, a);
+      }
+    } else {                      // 8-B aligned at RATIO = 4
+      const float2* s2 = reinterpret_cast<const float2*>(src);
+#pragma unroll
+      for (int q = 0; q < NT / 2; ++q) {
+        const float2 v = s2[q];
+        a = fmaf(w[2 * q], v.x, a);
+        a = fmaf(w[2 * q + 1], v.y, a);
+      }
+    }
     Vc[e] = a;
   }
 }
@@ -204,7 +221,7 @@ __global__ __launch_bounds__(256) void sel_doth_kernel(SelSmall t, const float* 
   const int b = bh / H;
   const int S = t.s[l];
   const int ratio = R / S;
-  const int EP = R + 2 * DOTH_PAD + 2;
+  const int EP = R + 2 * DOTH_PAD + 4;   // a multiple of 4 floats: 16-B aligned row runs
   float* W = sm;                        // [64] the column filter
   float* Vs = W + 64;                   // S × K
   float* Ep = Vs + ((S * K + 3) & ~3);  // K × EP, the row's e at [DOTH_PAD, DOTH_PAD + R)
@@ -1053,7 +1070,7 @@ extern "C" int skp_capture_maps_bwd_sel(const float* const* z_low, const int* si
   if (doth) {
     int rmax = 1;
     for (int l = 0; l < L; ++l) rmax = std::max(rmax, R / sizes[l]);
-    const size_t lds = (size_t)(64 + ((smax * K + 3) & ~3) + K * (R + 2 * DOTH_PAD + 2) + K * (R / 4 + 4)) *
+    const size_t lds = (size_t)(64 + ((smax * K + 3) & ~3) + K * (R + 2 * DOTH_PAD + 4) + K * (R / 4 + 4)) *
                        sizeof(float);
     if (rmax <= 8)
       hipLaunchKernelGGL(sel_doth_kernel<8>, dim3((unsigned)(L * BH * R)), dim3(R), lds, st, t, zsel, BH, R, H, K,
