@@ -350,6 +350,31 @@ def test_topk_gaussian_window_kernel_vs_per_pixel(hw):
         assert torch.equal(batch[i], ops.find_top_k_gaussian(a[i], 12, sigma=2.0))
 
 
+@pytest.mark.parametrize("hw", [(128, 128), (64, 64), (96, 80)])
+def test_topk_gaussian_streamed_kernel_vs_held(monkeypatch, hw):
+    """The streamed KL kernel (r05 default for rows up to 128²: running max + rescaled exp sum,
+    Σu as Σx − HW·max) against the held form (SKP_KL_STREAM=0: the row in registers) on the same
+    rows, with a NaN row, an all-equal row (argmax ties) and a row with +inf: identical selections,
+    KL within 1e-6 relative (NaN where the held form gives NaN)."""
+    from stablekeypoints_amd import ops
+    h, w = hw
+    rng = np.random.default_rng(h + w)
+    maps = rng.random((2, 60, h, w), dtype=np.float32) ** 8
+    maps[0, 5, 3, 7] = np.nan
+    maps[0, 6] = 0.25
+    maps[1, 9, h - 1, w - 1] = np.inf
+    a = T(maps)
+    out = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("SKP_KL_STREAM", v)
+        out[v] = [ops.find_top_k_gaussian(a[i], 20, sigma=2.0, return_kl=True) for i in range(2)]
+    for (i1, k1), (i0, k0) in zip(out["1"], out["0"]):
+        assert torch.equal(i1, i0)
+        n1, n0 = torch.isnan(k1), torch.isnan(k0)
+        assert torch.equal(n1, n0)
+        assert torch.allclose(k1[~n1], k0[~n0], rtol=1e-6, atol=0), float((k1[~n1] - k0[~n0]).abs().max())
+
+
 def test_topk_gaussian_window_edges_and_sigma():
     """The window clipped at every border (argmax in corners and on edges), σ large enough that
     the window covers the whole row, and a non-default epsilon: KL within 1e-6 relative of the

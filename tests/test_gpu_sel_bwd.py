@@ -207,3 +207,31 @@ def test_fused_horizontal_adjoint_equals_e_rows(monkeypatch, B, H, sizes, R, Nn,
         out[v] = _sel_abi(zt, list(sizes), B, H, R, T(tok), T(gsel), 0.03125, stats)
     for a, b in zip(out["0"], out["1"]):
         assert torch.equal(a, b), (a - b).abs().max().item()
+
+
+def test_phase_timing_records_each_fast_path_call():
+    """skp_sel_bwd_timing / _read (the bench's `split_ms`): one record per fast-path call while on,
+    four non-negative phase times whose sum is within the call's own event time, none when off."""
+    import ctypes
+    from stablekeypoints_amd._lib import lib
+    L = lib()
+    zs, tok, gsel = _case(3, 2, 4, (8, 16), 64, 64, 5)
+    zt = [T(z) for z in zs]
+    _, stats = _fwd(zt, [8, 16], 2, 4, 64)
+    ms = (ctypes.c_double * 4)()
+    n = ctypes.c_int(-1)
+    assert L.skp_sel_bwd_timing(1) == 0
+    try:
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(2):
+            _sel_abi(zt, [8, 16], 2, 4, 64, T(tok), T(gsel), 0.5, stats)
+        b.record()
+        b.synchronize()
+        assert L.skp_sel_bwd_timing_read(ms, ctypes.byref(n)) == 0
+    finally:
+        L.skp_sel_bwd_timing(0)
+    assert n.value == 2
+    assert all(ms[i] >= 0.0 for i in range(4)) and 0.0 < sum(ms) <= a.elapsed_time(b)
+    _sel_abi(zt, [8, 16], 2, 4, 64, T(tok), T(gsel), 0.5, stats)   # off: nothing recorded
+    assert L.skp_sel_bwd_timing_read(ms, ctypes.byref(n)) == 0 and n.value == 0
