@@ -547,7 +547,7 @@ __global__ __launch_bounds__(BT) void kl_gauss_win_kernel(const float* __restric
 // HBM rate.  Same window terms, same closed form; the sums round differently from the held form
 // (Σu by ≤ HW·ulp ≈ 1e-3 absolute, entering KL scaled by eps/S_t ≈ 4e-7: ≈ 1e-10), indices
 // bit-exact on the goldens (tests/test_gpu_parity.py).
-template <int BT, int UNR, int PROBE = 0>
+template <int BT, int UNR>
 __global__ __launch_bounds__(BT) void kl_gauss_stream_kernel(const float* __restrict__ maps, int h, int w,
                                                             float two_sig2, float eps, int wr,
                                                             double* __restrict__ kl) {
@@ -611,8 +611,9 @@ __global__ __launch_bounds__(BT) void kl_gauss_stream_kernel(const float* __rest
   const int ww = j1 - j0 + 1, nW = (i1 - i0 + 1) * ww;
   double win[4] = {0.0, 0.0, 0.0, 0.0};   // Σ_W t, Σ_W t·log t, Σ_W t·u, Σ_W u
   // the window's row values re-read 4 per thread at a time (loads in flight together), then its terms
-  // in element order per thread (PROBE: timing probes only)
-  for (int k0 = threadIdx.x; k0 < (PROBE >= 1 ? 0 : nW); k0 += 4 * BT) {
+  // in element order per thread (r05 timing probes, profiles/r05zh_kl_probes.txt: the stream alone
+  // 25 µs, + block reductions 4 µs, + this window pass 5 µs)
+  for (int k0 = threadIdx.x; k0 < nW; k0 += 4 * BT) {
     float rv[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -633,10 +634,6 @@ __global__ __launch_bounds__(BT) void kl_gauss_stream_kernel(const float* __rest
         win[3] += (double)u;
       }
     }
-  }
-  if (PROBE >= 2) {
-    if (threadIdx.x == 0) kl[blockIdx.x] = se + sx;
-    return;
   }
   double red[6] = {se, sx, win[0], win[1], win[2], win[3]};
   block_sum_to0<6>(red, sd);
@@ -1039,12 +1036,6 @@ extern "C" int skp_topk_gaussian_batch(const float* maps, int nb, int T, int h, 
                                                                   dim3(BT_), 0, st, maps, h, w, two_sig2, epsilon, wr, keys);
     if (false) {
     }
-    else if (stream && getenv("SKP_KL_PROBE") && atoi(getenv("SKP_KL_PROBE")) == 1)   // timing probes (wrong keys)
-      hipLaunchKernelGGL((kl_gauss_stream_kernel<256, 1, 1>), dim3(rows), dim3(256), 0, st, maps, h, w, two_sig2,
-                         epsilon, wr, keys);
-    else if (stream && getenv("SKP_KL_PROBE") && atoi(getenv("SKP_KL_PROBE")) == 2)
-      hipLaunchKernelGGL((kl_gauss_stream_kernel<256, 1, 2>), dim3(rows), dim3(256), 0, st, maps, h, w, two_sig2,
-                         epsilon, wr, keys);
     SKP_KL_STREAM_CASE(256, 2)
     SKP_KL_STREAM_CASE(256, 1)
     SKP_KL_STREAM_CASE(256, 4)
