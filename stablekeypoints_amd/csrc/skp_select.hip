@@ -612,7 +612,9 @@ __global__ __launch_bounds__(BT) void kl_gauss_stream_kernel(const float* __rest
   double win[4] = {0.0, 0.0, 0.0, 0.0};   // Σ_W t, Σ_W t·log t, Σ_W t·u, Σ_W u
   // the window's row values re-read 4 per thread at a time (loads in flight together), then its terms
   // in element order per thread (r05 timing probes, profiles/r05zh_kl_probes.txt: the stream alone
-  // 25 µs, + block reductions 4 µs, + this window pass 5 µs)
+  // 25 µs, + block reductions 4 µs, + this window pass 5 µs); the Gaussian and its log on the
+  // hardware exp / log (≤ 2 ulp: KL within 1e-6 of the fp64 oracle, indices bit-exact on the
+  // goldens; 34.0 → 33.4 µs)
   for (int k0 = threadIdx.x; k0 < nW; k0 += 4 * BT) {
     float rv[4];
 #pragma unroll
@@ -626,10 +628,10 @@ __global__ __launch_bounds__(BT) void kl_gauss_stream_kernel(const float* __rest
       if (k < nW) {
         const int i = i0 + k / ww, jj = j0 + k % ww;
         const float di = ((float)i + 0.5f) - p0, dj = ((float)jj + 0.5f) - p1;
-        const float t = expf(-(dj * dj + di * di) / two_sig2) + eps;
+        const float t = __expf(-(dj * dj + di * di) / two_sig2) + eps;
         const float u = (rv[r] + eps) - mx;
         win[0] += (double)t;
-        win[1] += (double)t * (double)logf(t);
+        win[1] += (double)t * (double)__logf(t);
         win[2] += (double)t * (double)u;
         win[3] += (double)u;
       }
