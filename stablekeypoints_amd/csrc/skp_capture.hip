@@ -809,19 +809,20 @@ void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nc
   }
 }
 
-// Tiled form of capture_maps_kernel (r05; default where it applies): ONE 16-wave workgroup per CU
+// Tiled form of capture_maps_kernel (r05; A/B only, SKP_MAPS_TILE=2|4 — measured slower than the
+// one-row kernel): ONE 16-wave workgroup per CU
 // owns a TY-row × TX-pixel tile of image b (TY·TX = 16 waves × PXW pixels: 2 × 32 or 4 × 16 at
 // N = 500).  The TY output rows of a tile tap at most TY + 3 consecutive z_low rows (lo(y) rises
 // by ≤ 1 per output row since s ≤ R), so each z_low value a thread loads feeds the vertical pass
 // of every row of the tile: per pixel the z_low load volume is 0.48× (2 × 32) or 0.40× (4 × 16)
 // that of the one-row form, whose per-slab staging was bound by the L2 → CU load rate (9.4 GB per
-// launch at the bench shape, §5).  V is double-buffered and the slab loop has ONE barrier: waves
-// 0-7 stage slab it + 1 before their pixels of slab it, waves 8-15 after them, so on every SIMD
-// two waves wait on their staging loads while the other two compute.  Per pixel the arithmetic is
+// launch at the bench shape, §5).  V is double-buffered and the slab loop has ONE barrier: every
+// wave stages slab it + 1 before its pixels of slab it.  (A staggered form — waves 8-15 staging
+// after their pixels — computed wrong rows on the GPU and was removed)  Per pixel the arithmetic is
 // the one-row kernel's operation for operation (same vertical FMA chain on the same z_low values,
 // same taps, max, exp, sums and accumulation order), so maps and stats are bit-identical to it.
 constexpr int kTileLdsFloats = 160 * 1024 / 4;   // the whole CU's LDS, statically (one workgroup per CU)
-template <int QPL, int TY, bool STAG>
+template <int QPL, int TY>
 __global__ __launch_bounds__(16 * WAVE) __attribute__((amdgpu_waves_per_eu(4)))
 void capture_maps_tile_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nchunks, int vstride, float count,
                               float* __restrict__ maps) {
@@ -848,7 +849,6 @@ void capture_maps_tile_kernel(CapLayers cl, int L, int B, int H, int N, int R, i
   const int row = lane >> 4, li = lane & 15;
   const int ry = wid / WPR;                   // this wave's tile row
   const int nq = N >> 2;
-  const bool late = STAG && wid >= 8;        // stages after its pixels (see above)
   for (int job = jfirst; job < jend; job += nper) {
     const int xc = job % nchunks;
     const int t = (job / nchunks) % nty;
@@ -921,7 +921,7 @@ void capture_maps_tile_kernel(CapLayers cl, int L, int B, int H, int N, int R, i
     __syncthreads();
     const int nslab = L * H;
     for (int it = 0; it < nslab; ++it) {
-      if ((!STAG || !late) && it + 1 < nslab) {
+      if (it + 1 < nslab) {
   #if SKP_MAPS_PRIO
         __builtin_amdgcn_s_setprio(SKP_MAPS_PRIO);
   #endif
@@ -978,15 +978,6 @@ void capture_maps_tile_kernel(CapLayers cl, int L, int B, int H, int N, int R, i
           SKP_MAPS_ST(reinterpret_cast<f2v*>(st)[((size_t)bh * R + yr) * R + x0 + xl], mi);
         }
         __builtin_amdgcn_sched_barrier(0);
-      }
-      if (STAG && late && it + 1 < nslab) {
-  #if SKP_MAPS_PRIO
-        __builtin_amdgcn_s_setprio(SKP_MAPS_PRIO);
-  #endif
-        stage(it + 1);
-  #if SKP_MAPS_PRIO
-        __builtin_amdgcn_s_setprio(0);
-  #endif
       }
       __syncthreads();
     }
@@ -1639,12 +1630,6 @@ int maps_tile_rows() {   // read per call (A/B tests switch it in-process)
   return (v == 2 || v == 4) ? v : 0;
 }
 
-// SKP_MAPS_STAGGER=1: waves 8-15 stage after their pixels (A/B; default off)
-bool maps_tile_stagger() {
-  const char* e = getenv("SKP_MAPS_STAGGER");
-  return e && atoi(e) == 1;
-}
-
 template <int QPL, int TY>
 void launch_maps_tile(const CapLayers& cl, int L, int B, int H, int N, int R, int vstride, size_t lds, float* maps,
                       hipStream_t st) {
@@ -1659,12 +1644,8 @@ void launch_maps_tile(const CapLayers& cl, int L, int B, int H, int N, int R, in
   }();
   const int grid = std::min(8 * ((total + 7) / 8), ncu);   // persistent: one workgroup per CU, multiple of 8
   (void)lds;   // static LDS (kTileLdsFloats); the caller checked lds <= its size
-  if (maps_tile_stagger())
-    hipLaunchKernelGGL((capture_maps_tile_kernel<QPL, TY, true>), dim3(grid), dim3(16 * WAVE), 0, st, cl, L, B, H, N, R,
-                       nchunks, vstride, (float)L * (float)H, maps);
-  else
-    hipLaunchKernelGGL((capture_maps_tile_kernel<QPL, TY, false>), dim3(grid), dim3(16 * WAVE), 0, st, cl, L, B, H, N,
-                       R, nchunks, vstride, (float)L * (float)H, maps);
+  hipLaunchKernelGGL((capture_maps_tile_kernel<QPL, TY>), dim3(grid), dim3(16 * WAVE), 0, st, cl, L, B, H, N, R,
+                     nchunks, vstride, (float)L * (float)H, maps);
 }
 template <int QPL>
 void launch_maps_tile_ty(int ty, const CapLayers& cl, int L, int B, int H, int N, int R, int vstride, size_t lds,
