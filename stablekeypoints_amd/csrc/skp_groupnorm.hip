@@ -24,9 +24,28 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kChunk = 16384;   // floats per block (64 KiB)
 
-__device__ __forceinline__ float silu(float z) { return z / (1.0f + __expf(-z)); }
+#ifndef SKP_GN_FAST
+// 1: σ(z) through v_rcp_f32 (1 ulp) instead of the IEEE division sequence, and the channel of a
+// group offset by a 32-bit division (the 64-bit one is a ≈40-instruction sequence per float4);
+// 0: the r04 forms (A/B build)
+#define SKP_GN_FAST 1
+#endif
+__device__ __forceinline__ float sigmoid_of(float z) {
+#if SKP_GN_FAST
+  return __builtin_amdgcn_rcpf(1.0f + __expf(-z));
+#else
+  return 1.0f / (1.0f + __expf(-z));
+#endif
+}
+__device__ __forceinline__ float silu(float z) {
+#if SKP_GN_FAST
+  return z * sigmoid_of(z);
+#else
+  return z / (1.0f + __expf(-z));
+#endif
+}
 __device__ __forceinline__ float silu_grad(float z) {
-  const float s = 1.0f / (1.0f + __expf(-z));
+  const float s = sigmoid_of(z);
   return s * (1.0f + z * (1.0f - s));
 }
 
@@ -34,6 +53,15 @@ struct GNShape {
   int B, C, G, cpg, nsplit;
   long long HW, len;  // len = cpg * HW (floats per group)
 };
+
+// channel (within its group) of float e of a group: e < len < 2^32 (make_shape)
+__device__ __forceinline__ int chan_of(long long e, const GNShape& sh) {
+#if SKP_GN_FAST
+  return (int)((unsigned)e / (unsigned)sh.HW);
+#else
+  return (int)(e / sh.HW);
+#endif
+}
 
 // shift of channel c of group grp (nullptr: none)
 __device__ __forceinline__ float shift_of(const float* __restrict__ shift, const GNShape& sh, int grp, int c) {
@@ -70,14 +98,14 @@ __global__ __launch_bounds__(kThreads) void gn_stats_kernel(const float* __restr
   if (VEC) {
     for (long long e = lo + 4 * threadIdx.x; e < hi; e += 4 * kThreads) {
       float4 v = *reinterpret_cast<const float4*>(base + e);
-      const float t = shift_of(shift, sh, grp, g * sh.cpg + (int)(e / sh.HW));
+      const float t = shift_of(shift, sh, grp, g * sh.cpg + chan_of(e, sh));
       v.x += t; v.y += t; v.z += t; v.w += t;
       s1 += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
       s2 += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
     }
   } else {
     for (long long e = lo + threadIdx.x; e < hi; e += kThreads) {
-      const double v = base[e] + shift_of(shift, sh, grp, g * sh.cpg + (int)(e / sh.HW));
+      const double v = base[e] + shift_of(shift, sh, grp, g * sh.cpg + chan_of(e, sh));
       s1 += v;
       s2 += v * v;
     }
@@ -164,7 +192,7 @@ __global__ __launch_bounds__(kThreads) void gn_apply_kernel(const float* __restr
   const long long lo = (long long)sp * kChunk, hi = min(sh.len, lo + kChunk);
   if (VEC) {   // HW % 4 == 0: a float4 never straddles two channels
     for (long long e = lo + 4 * threadIdx.x; e < hi; e += 4 * kThreads) {
-      const int c = g * sh.cpg + (int)(e / sh.HW);
+      const int c = g * sh.cpg + chan_of(e, sh);
       const float ga = gamma[c] * rstd, be = beta[c] - mean * gamma[c] * rstd;
       const float t = shift_of(shift, sh, grp, c);
       float4 v = *reinterpret_cast<const float4*>(base + e);
@@ -175,7 +203,7 @@ __global__ __launch_bounds__(kThreads) void gn_apply_kernel(const float* __restr
     }
   } else {
     for (long long e = lo + threadIdx.x; e < hi; e += kThreads) {
-      const int c = g * sh.cpg + (int)(e / sh.HW);
+      const int c = g * sh.cpg + chan_of(e, sh);
       float v = ((base[e] + shift_of(shift, sh, grp, c)) - mean) * rstd * gamma[c] + beta[c];
       out[e] = ACT ? silu(v) : v;
     }
@@ -200,7 +228,7 @@ __global__ __launch_bounds__(kThreads) void gn_bwd_stats_kernel(const float* __r
   double s1 = 0.0, s2 = 0.0;
   const long long step = VEC ? 4 : 1;
   for (long long e0 = lo + step * threadIdx.x; e0 < hi; e0 += step * kThreads) {
-    const int c = g * sh.cpg + (int)(e0 / sh.HW);
+    const int c = g * sh.cpg + chan_of(e0, sh);
     const float ga = gamma[c], be = beta[c], t = shift_of(shift, sh, grp, c);
     float xv[4], dv[4];
     if (VEC) {
@@ -260,7 +288,7 @@ __global__ __launch_bounds__(kThreads) void gn_bwd_apply_kernel(const float* __r
   const long long lo = (long long)sp * kChunk, hi = min(sh.len, lo + kChunk);
   const long long step = VEC ? 4 : 1;
   for (long long e0 = lo + step * threadIdx.x; e0 < hi; e0 += step * kThreads) {
-    const int c = g * sh.cpg + (int)(e0 / sh.HW);
+    const int c = g * sh.cpg + chan_of(e0, sh);
     const float ga = gamma[c], be = beta[c], t = shift_of(shift, sh, grp, c);
     float xv[4], dv[4], r[4], av[4] = {0.f, 0.f, 0.f, 0.f};
     if (VEC) {
@@ -318,7 +346,7 @@ bool make_shape(int B, int C, long long HW, int G, GNShape& sh) {
   sh.B = B; sh.C = C; sh.G = G; sh.cpg = C / G; sh.HW = HW;
   sh.len = (long long)sh.cpg * HW;
   sh.nsplit = (int)((sh.len + kChunk - 1) / kChunk);
-  return true;
+  return sh.len < (1LL << 32);   // chan_of's 32-bit offsets
 }
 
 }  // namespace
