@@ -63,6 +63,40 @@ __device__ __forceinline__ int chan_of(long long e, const GNShape& sh) {
 #endif
 }
 
+#ifndef SKP_GN_BATCH
+#define SKP_GN_BATCH 4   // float4s per thread whose loads are issued together (1: one at a time, A/B)
+#endif
+// This thread's float4s of [lo, hi) (stride 4·kThreads), visited in ascending order (the order the
+// per-thread sums depend on) in batches of SKP_GN_BATCH whose loads ld(e) are issued before any
+// use(e, v): the small 64² / 32² groups are otherwise one load latency per float4.
+template <typename Ld, typename Use>
+__device__ __forceinline__ void for_f4(long long lo, long long hi, Ld ld, Use use) {
+  constexpr int U = SKP_GN_BATCH;
+  constexpr long long S = 4 * kThreads;
+  long long e = lo + 4 * threadIdx.x;
+  for (; e + (U - 1) * S < hi; e += U * S) {
+    decltype(ld(e)) v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = ld(e + u * S);
+#pragma unroll
+    for (int u = 0; u < U; ++u) use(e + u * S, v[u]);
+  }
+  for (; e < hi; e += S) use(e, ld(e));
+}
+
+// a + b rounded on its own (never contracted into the product that made a): the fused residual
+// gradient equals autograd's separate add bit for bit
+__device__ __forceinline__ float add_rn(float a, float b) {
+#pragma clang fp contract(off)
+  return a + b;
+}
+
+// x and dy (and the residual gradient, r) of one float4 position (the backward's loads)
+struct Pair4 {
+  float4 a, b, r;
+};
+__device__ __forceinline__ Pair4 make_pair4(float4 a, float4 b) { return Pair4{a, b, make_float4(0.f, 0.f, 0.f, 0.f)}; }
+
 // shift of channel c of group grp (nullptr: none)
 __device__ __forceinline__ float shift_of(const float* __restrict__ shift, const GNShape& sh, int grp, int c) {
   return shift ? shift[(grp / sh.G) * sh.C + c] : 0.0f;
@@ -96,13 +130,13 @@ __global__ __launch_bounds__(kThreads) void gn_stats_kernel(const float* __restr
   const long long lo = (long long)sp * kChunk, hi = min(sh.len, lo + kChunk);
   double s1 = 0.0, s2 = 0.0;
   if (VEC) {
-    for (long long e = lo + 4 * threadIdx.x; e < hi; e += 4 * kThreads) {
-      float4 v = *reinterpret_cast<const float4*>(base + e);
-      const float t = shift_of(shift, sh, grp, g * sh.cpg + chan_of(e, sh));
-      v.x += t; v.y += t; v.z += t; v.w += t;
-      s1 += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
-      s2 += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
-    }
+    for_f4(lo, hi, [&](long long e) { return *reinterpret_cast<const float4*>(base + e); },
+           [&](long long e, float4 v) {
+             const float t = shift_of(shift, sh, grp, g * sh.cpg + chan_of(e, sh));
+             v.x += t; v.y += t; v.z += t; v.w += t;
+             s1 += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
+             s2 += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+           });
   } else {
     for (long long e = lo + threadIdx.x; e < hi; e += kThreads) {
       const double v = base[e] + shift_of(shift, sh, grp, g * sh.cpg + chan_of(e, sh));
@@ -191,16 +225,16 @@ __global__ __launch_bounds__(kThreads) void gn_apply_kernel(const float* __restr
   float* out = y + (size_t)grp * sh.len;
   const long long lo = (long long)sp * kChunk, hi = min(sh.len, lo + kChunk);
   if (VEC) {   // HW % 4 == 0: a float4 never straddles two channels
-    for (long long e = lo + 4 * threadIdx.x; e < hi; e += 4 * kThreads) {
-      const int c = g * sh.cpg + chan_of(e, sh);
-      const float ga = gamma[c] * rstd, be = beta[c] - mean * gamma[c] * rstd;
-      const float t = shift_of(shift, sh, grp, c);
-      float4 v = *reinterpret_cast<const float4*>(base + e);
-      v.x += t; v.y += t; v.z += t; v.w += t;
-      v.x = v.x * ga + be; v.y = v.y * ga + be; v.z = v.z * ga + be; v.w = v.w * ga + be;
-      if (ACT) { v.x = silu(v.x); v.y = silu(v.y); v.z = silu(v.z); v.w = silu(v.w); }
-      *reinterpret_cast<float4*>(out + e) = v;
-    }
+    for_f4(lo, hi, [&](long long e) { return *reinterpret_cast<const float4*>(base + e); },
+           [&](long long e, float4 v) {
+             const int c = g * sh.cpg + chan_of(e, sh);
+             const float ga = gamma[c] * rstd, be = beta[c] - mean * gamma[c] * rstd;
+             const float t = shift_of(shift, sh, grp, c);
+             v.x += t; v.y += t; v.z += t; v.w += t;
+             v.x = v.x * ga + be; v.y = v.y * ga + be; v.z = v.z * ga + be; v.w = v.w * ga + be;
+             if (ACT) { v.x = silu(v.x); v.y = silu(v.y); v.z = silu(v.z); v.w = silu(v.w); }
+             *reinterpret_cast<float4*>(out + e) = v;
+           });
   } else {
     for (long long e = lo + threadIdx.x; e < hi; e += kThreads) {
       const int c = g * sh.cpg + chan_of(e, sh);
@@ -226,21 +260,13 @@ __global__ __launch_bounds__(kThreads) void gn_bwd_stats_kernel(const float* __r
   const float* db = dy + (size_t)grp * sh.len;
   const long long lo = (long long)sp * kChunk, hi = min(sh.len, lo + kChunk);
   double s1 = 0.0, s2 = 0.0;
-  const long long step = VEC ? 4 : 1;
-  for (long long e0 = lo + step * threadIdx.x; e0 < hi; e0 += step * kThreads) {
+  // the elements of x / dy at e0 (n = 4 or 1 of them), in order
+  auto body = [&](long long e0, const float* xv, const float* dv, int n) {
     const int c = g * sh.cpg + chan_of(e0, sh);
     const float ga = gamma[c], be = beta[c], t = shift_of(shift, sh, grp, c);
-    float xv[4], dv[4];
-    if (VEC) {
-      const float4 a = *reinterpret_cast<const float4*>(xb + e0), b = *reinterpret_cast<const float4*>(db + e0);
-      xv[0] = a.x; xv[1] = a.y; xv[2] = a.z; xv[3] = a.w;
-      dv[0] = b.x; dv[1] = b.y; dv[2] = b.z; dv[3] = b.w;
-    } else {
-      xv[0] = xb[e0];
-      dv[0] = db[e0];
-    }
 #pragma unroll
-    for (int k = 0; k < (VEC ? 4 : 1); ++k) {
+    for (int k = 0; k < 4; ++k) {
+      if (k >= n) break;
       const float xh = ((xv[k] + t) - mean) * rstd;
       float gz = dv[k];
       if (ACT) gz *= silu_grad(xh * ga + be);
@@ -248,6 +274,18 @@ __global__ __launch_bounds__(kThreads) void gn_bwd_stats_kernel(const float* __r
       s1 += (double)gg;
       s2 += (double)gg * (double)xh;
     }
+  };
+  if (VEC) {
+    for_f4(lo, hi,
+           [&](long long e) {
+             return make_pair4(*reinterpret_cast<const float4*>(xb + e), *reinterpret_cast<const float4*>(db + e));
+           },
+           [&](long long e, const Pair4& v) {
+             const float xv[4] = {v.a.x, v.a.y, v.a.z, v.a.w}, dv[4] = {v.b.x, v.b.y, v.b.z, v.b.w};
+             body(e, xv, dv, 4);
+           });
+  } else {
+    for (long long e0 = lo + threadIdx.x; e0 < hi; e0 += kThreads) body(e0, xb + e0, db + e0, 1);
   }
   block_sum2(s1, s2, sd);
   if (threadIdx.x == 0) {
@@ -286,38 +324,41 @@ __global__ __launch_bounds__(kThreads) void gn_bwd_apply_kernel(const float* __r
   float* ob = dx + (size_t)grp * sh.len;
   const float* rb = dres ? dres + (size_t)grp * sh.len : nullptr;
   const long long lo = (long long)sp * kChunk, hi = min(sh.len, lo + kChunk);
-  const long long step = VEC ? 4 : 1;
-  for (long long e0 = lo + step * threadIdx.x; e0 < hi; e0 += step * kThreads) {
+  // dx of the n (4 or 1) elements at e0: xv, dv, av (the residual gradient; 0 without one)
+  auto body = [&](long long e0, const float* xv, const float* dv, const float* av, float* r, int n) {
     const int c = g * sh.cpg + chan_of(e0, sh);
     const float ga = gamma[c], be = beta[c], t = shift_of(shift, sh, grp, c);
-    float xv[4], dv[4], r[4], av[4] = {0.f, 0.f, 0.f, 0.f};
-    if (VEC) {
-      const float4 a = *reinterpret_cast<const float4*>(xb + e0), b = *reinterpret_cast<const float4*>(db + e0);
-      xv[0] = a.x; xv[1] = a.y; xv[2] = a.z; xv[3] = a.w;
-      dv[0] = b.x; dv[1] = b.y; dv[2] = b.z; dv[3] = b.w;
-    } else {
-      xv[0] = xb[e0];
-      dv[0] = db[e0];
-    }
 #pragma unroll
-    for (int k = 0; k < (VEC ? 4 : 1); ++k) {
+    for (int k = 0; k < 4; ++k) {
+      if (k >= n) break;
       const float xh = ((xv[k] + t) - mean) * rstd;
       float gz = dv[k];
       if (ACT) gz *= silu_grad(xh * ga + be);
       r[k] = rstd * (gz * ga - ma - xh * mb);
+      if (rb) r[k] = add_rn(r[k], av[k]);   // + the gradient of x's other consumer (the residual / shortcut)
     }
-    if (rb) {   // + the gradient of x's other consumer (the residual / shortcut), in one pass
-      if (VEC) {
-        const float4 a = *reinterpret_cast<const float4*>(rb + e0);
-        av[0] = a.x; av[1] = a.y; av[2] = a.z; av[3] = a.w;
-      } else {
-        av[0] = rb[e0];
-      }
-#pragma unroll
-      for (int k = 0; k < (VEC ? 4 : 1); ++k) r[k] += av[k];
+  };
+  if (VEC) {
+    for_f4(lo, hi,
+           [&](long long e) {
+             Pair4 v = make_pair4(*reinterpret_cast<const float4*>(xb + e), *reinterpret_cast<const float4*>(db + e));
+             v.r = rb ? *reinterpret_cast<const float4*>(rb + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+             return v;
+           },
+           [&](long long e, const Pair4& v) {
+             const float xv[4] = {v.a.x, v.a.y, v.a.z, v.a.w}, dv[4] = {v.b.x, v.b.y, v.b.z, v.b.w};
+             const float av[4] = {v.r.x, v.r.y, v.r.z, v.r.w};
+             float r[4];
+             body(e, xv, dv, av, r, 4);
+             *reinterpret_cast<float4*>(ob + e) = make_float4(r[0], r[1], r[2], r[3]);
+           });
+  } else {
+    for (long long e0 = lo + threadIdx.x; e0 < hi; e0 += kThreads) {
+      const float av = rb ? rb[e0] : 0.0f;
+      float r;
+      body(e0, xb + e0, db + e0, &av, &r, 1);
+      ob[e0] = r;
     }
-    if (VEC) *reinterpret_cast<float4*>(ob + e0) = make_float4(r[0], r[1], r[2], r[3]);
-    else ob[e0] = r[0];
   }
 }
 
