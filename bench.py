@@ -12,8 +12,9 @@ selection + losses + backward through the UNet into the token embedding, then th
 gradient all-reduce (RCCL) and Adam.  Weak scaling: every rank processes ``accum``
 images per step.  ``value`` = images processed by all ranks ÷ the max-over-ranks time.
 
-Launch: ``python bench.py`` (1 GPU) or ``python -m torch.distributed.run --nproc-per-node N
---master-addr 127.0.0.1 bench.py --gpus N``.  Rank 0 prints ONE JSON line.
+Launch: ``python bench.py`` (1 GPU), ``python bench.py --gpus N`` (starts N ranks itself, one per
+GPU, RCCL), or ``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1
+bench.py --gpus N`` (the launcher's WORLD_SIZE must equal N).  Rank 0 prints ONE JSON line.
 """
 import argparse
 import json
@@ -494,6 +495,23 @@ def stage_main(args, ldm, controllers, context, dev, world, rank, backend):
         dist.destroy_process_group()
 
 
+def dry_run_main(world, rank, local):
+    """--dry-run: the launch path without the GPU.  Every rank joins a gloo group (when world > 1),
+    the ranks all-gather what they saw, and rank 0 prints one JSON line."""
+    seen = {"rank": rank, "world_env": world, "local_rank": local, "device": f"cuda:{local}", "pid": os.getpid()}
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        ranks = [None] * dist.get_world_size()
+        dist.all_gather_object(ranks, seen)
+        n = dist.get_world_size()
+        dist.destroy_process_group()
+    else:
+        ranks, n = [seen], 1
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": n, "ranks": ranks}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -539,21 +557,33 @@ def main():
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
                     help="JSON with PMC-derived HBM bytes per launch of the roofline kernel")
     ap.add_argument("--cpu-leg", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch path only: start the --gpus ranks, join them over gloo, print one JSON line with the "
+                         "world each rank saw and the device it would use; no HIP call anywhere")
     args = ap.parse_args()
     if args.cpu_leg:
         return cpu_leg_main(args)
     if args.graph and args.prefetch < 1:
         args.prefetch = 1   # only prefetched passes replay a graph (TokenOptimizer.micro_steps)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # --gpus N means N ranks.  Without a launcher environment and N > 1, this process starts them
+    # (torch.distributed.run as a child, before any HIP call) and exits with their status; under a
+    # launcher, its world must be the N asked for.
+    from stablekeypoints_amd.launch import launcher_env, spawn_ranks
+    env = launcher_env()
+    if env is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, [os.path.abspath(__file__)], sys.argv[1:]))
+    world, rank, local = env if env is not None else (1, 0, 0)
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     # Rehearsal of the multi-GPU path on a one-GPU box (not the measured configuration):
     # SKP_BENCH_ONE_DEVICE=1 puts every rank on cuda:0, SKP_BENCH_DIST_BACKEND=gloo replaces RCCL
     # (which refuses two ranks on one device).  The driver's N-GPU runs use neither.
     if os.environ.get("SKP_BENCH_ONE_DEVICE") == "1":
         local = 0
     backend = os.environ.get("SKP_BENCH_DIST_BACKEND", "nccl")
+    if args.dry_run:
+        return dry_run_main(world, rank, local)
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
@@ -561,6 +591,8 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        world = dist.get_world_size()
+        backend = dist.get_backend()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 

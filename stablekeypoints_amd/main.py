@@ -4,11 +4,14 @@ optimize (``optimize_embedding`` → ``embedding.pt``) → find_indices (``find_
 ``indices.pt``) → precompute (``precompute_all_keypoints`` → ``source_keypoints.pt``,
 ``target_keypoints.pt``, ``visible.pt``) → regressor (``regressor.pt``) → evaluate
 (``all_errors.pt``).  ``--start_from_stage`` resumes from the saved files.  Visualisation
-(``visualize_attn_maps``) is not built.  Multi-GPU: ``python -m torch.distributed.run
---nproc-per-node N -m stablekeypoints_amd.main ...`` (every rank seeded alike: ``--seed``).
+(``visualize_attn_maps``) is not built.  Multi-GPU: like the reference, one command uses every
+visible GPU — it starts one rank per GPU under ``torch.distributed.run`` (``--num_gpus`` to pick
+fewer); launching it under ``torch.distributed.run`` yourself works too (every rank seeded alike:
+``--seed``).
 """
 import argparse
 import os
+import sys
 
 import torch
 
@@ -56,7 +59,21 @@ def build_parser():
     p.add_argument("--validation", action="store_true")
     p.add_argument("--top_k", type=int, default=10)
     p.add_argument("--seed", type=int, default=0, help="CPU/GPU RNG seed, identical on every rank")
+    p.add_argument("--num_gpus", type=int, default=-1,
+                   help="ranks to start, one per GPU (-1 = every visible GPU, as the reference's DataParallel "
+                        "over torch.cuda.device_count(), optimize_token.py:42-50); ignored under a launcher")
     return p
+
+
+def ranks_to_start(args, visible, env):
+    """How many ranks this command starts: 1 when already running as a rank (``env``) or with at
+    most one GPU, else ``--num_gpus`` (every visible GPU by default)."""
+    if env is not None:
+        return 1
+    n = visible if args.num_gpus < 0 else args.num_gpus
+    if n > max(visible, 1):
+        raise SystemExit(f"--num_gpus {n} but {visible} GPU(s) are visible")
+    return max(n, 1)
 
 
 def _load(folder, name, device=None):
@@ -67,6 +84,11 @@ def _load(folder, name, device=None):
 def main(argv=None):
     import numpy as np
     args = build_parser().parse_args(argv)
+    from .launch import launcher_env, spawn_ranks
+    # torch.cuda.device_count() does not initialise HIP on this image, so the ranks can still start
+    n = ranks_to_start(args, torch.cuda.device_count(), launcher_env())
+    if n > 1:
+        sys.exit(spawn_ranks(n, ["-m", "stablekeypoints_amd.main"], sys.argv[1:] if argv is None else list(argv)))
     from .eval import evaluate
     from .keypoint_regressor import (find_best_indices, precompute_all_keypoints, return_regressor,
                                      return_regressor_human36m, return_regressor_visible)
