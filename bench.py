@@ -699,7 +699,7 @@ def main():
 
     # roofline: the dominant hot-path kernel, skp_capture_maps_fwd (fused capture + per-image
     # aggregate), is VALU-bound (bicubic taps + exp + normalise per (pixel, token, layer, head));
-    # its HBM traffic is reported beside it.  With SKP_FUSED_MAPS=0 the r01 path's HBM-bound
+    # its HBM traffic is reported beside it.  With ops.FUSED_MAPS = False the r01 path's HBM-bound
     # skp_aggregate is reported instead.
     roof = None
     extra = {}

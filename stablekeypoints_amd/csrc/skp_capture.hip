@@ -809,214 +809,6 @@ void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nc
   }
 }
 
-// Tiled form of capture_maps_kernel (r05; A/B only, SKP_MAPS_TILE=2|4 — measured slower than the
-// one-row kernel): ONE 16-wave workgroup per CU
-// owns a TY-row × TX-pixel tile of image b (TY·TX = 16 waves × PXW pixels: 2 × 32 or 4 × 16 at
-// N = 500).  The TY output rows of a tile tap at most TY + 3 consecutive z_low rows (lo(y) rises
-// by ≤ 1 per output row since s ≤ R), so each z_low value a thread loads feeds the vertical pass
-// of every row of the tile: per pixel the z_low load volume is 0.48× (2 × 32) or 0.40× (4 × 16)
-// that of the one-row form, whose per-slab staging was bound by the L2 → CU load rate (9.4 GB per
-// launch at the bench shape, §5).  V is double-buffered and the slab loop has ONE barrier: every
-// wave stages slab it + 1 before its pixels of slab it.  (A staggered form — waves 8-15 staging
-// after their pixels — computed wrong rows on the GPU and was removed)  Per pixel the arithmetic is
-// the one-row kernel's operation for operation (same vertical FMA chain on the same z_low values,
-// same taps, max, exp, sums and accumulation order), so maps and stats are bit-identical to it.
-constexpr int kTileLdsFloats = 160 * 1024 / 4;   // the whole CU's LDS, statically (one workgroup per CU)
-template <int QPL, int TY>
-__global__ __launch_bounds__(16 * WAVE) __attribute__((amdgpu_waves_per_eu(4)))
-void capture_maps_tile_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nchunks, int vstride, float count,
-                              float* __restrict__ maps) {
-  __shared__ __attribute__((aligned(16))) float lds[kTileLdsFloats];
-  constexpr int kT = 16 * WAVE;
-  constexpr int PXW = maps_pxw(QPL);          // pixels per wave (one row of the tile)
-  constexpr int G = PXW / 4;
-  constexpr int WPR = 16 / TY;                // waves per tile row
-  constexpr int TX = WPR * PXW;               // pixels per tile row
-  constexpr int NR = TY + 3;                  // z_low rows one tile can tap
-  constexpr int Np = 64 * QPL;
-  constexpr int Npq = Np / 4;
-  constexpr float L2E = 1.4426950408889634f;
-  float4* TW = reinterpret_cast<float4*>(lds);              // [2][TX] tap weights (by layer parity)
-  int4* TI = reinterpret_cast<int4*>(lds + 8 * TX);          // [2][TX] tap offsets (column − c0) · Npq
-  float* V = lds + 16 * TX;                                  // [2 bufs][TY rows][vstride] (then the store tile)
-
-  const int nty = (R + TY - 1) / TY;
-  const int total = B * nty * nchunks;
-  const int per = (total + 7) / 8;
-  const int xcd = blockIdx.x & 7, nper = gridDim.x >> 3;
-  const int jfirst = xcd * per + (blockIdx.x >> 3), jend = min(total, (xcd + 1) * per);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int row = lane >> 4, li = lane & 15;
-  const int ry = wid / WPR;                   // this wave's tile row
-  const int nq = N >> 2;
-  for (int job = jfirst; job < jend; job += nper) {
-    const int xc = job % nchunks;
-    const int t = (job / nchunks) % nty;
-    const int b = job / (nchunks * nty);
-    const int y0 = TY * t;
-    const int ny = min(TY, R - y0);           // rows past the image redo its last row, stored never
-    const int x0 = xc * TX;
-    const int np = min(TX, R - x0);
-
-    f4 acc[G][QPL];
-  #pragma unroll
-    for (int g = 0; g < G; ++g)
-  #pragma unroll
-      for (int c = 0; c < QPL; ++c) acc[g][c] = (f4)0.0f;
-
-    // tap table (first head of a layer) + the tile rows' vertical passes of slab it into V[it & 1]
-    auto stage = [&](int it) {
-      const int l = it / H, h = it - l * H;
-      const int s = cl.s[l];
-      const int c0 = max(bicubic_taps(x0, s, R).lo, 0);
-      const int nc = min(bicubic_taps(x0 + np - 1, s, R).lo + 3, s - 1) - c0 + 1;
-      if (h == 0) {
-        float4* tw = TW + (l & 1) * TX;
-        int4* tiw = TI + (l & 1) * TX;
-        for (int x = tid; x < TX; x += kT) {
-          const Taps4 tx = bicubic_taps(x0 + min(x, np - 1), s, R);
-          tw[x] = make_float4(tx.w[0], tx.w[1], tx.w[2], tx.w[3]);
-          tiw[x] = make_int4((tx.i[0] - c0) * Npq, (tx.i[1] - c0) * Npq, (tx.i[2] - c0) * Npq, (tx.i[3] - c0) * Npq);
-        }
-      }
-      const int lo0 = bicubic_taps(y0, s, R).lo;
-      const int nraw = bicubic_taps(min(y0 + TY - 1, R - 1), s, R).lo - lo0 + 4;   // ≤ NR
-      const float* zb = cl.z[l] + (size_t)(b * H + h) * s * s * N + (size_t)c0 * N;
-      f4* Vb = reinterpret_cast<f4*>(V + (it & 1) * TY * vstride);
-      const int tot = nc * Npq;
-  #pragma unroll 1
-      for (int e = tid; e < tot; e += kT) {
-        const int jj = e / Npq, q = e - jj * Npq;
-        const bool ok = q < nq;
-        const int o = jj * nq + q;
-        f4 a[NR];
-  #pragma unroll
-        for (int m = 0; m < NR; ++m) {
-          const int zr = min(max(lo0 + m, 0), s - 1);
-          a[m] = (ok && m < nraw) ? reinterpret_cast<const f4*>(zb + (size_t)zr * s * N)[o] : (f4)0.0f;
-        }
-  #pragma unroll
-        for (int r = 0; r < TY; ++r) {
-          const Taps4 ty = bicubic_taps(min(y0 + r, R - 1), s, R);
-          const int d = ty.lo - lo0;            // uniform: this row's taps are a[d .. d + 3]
-          f4 v = (f4)kPadLogit;
-          if (ok) {
-  #pragma unroll
-            for (int dd = 0; dd <= (TY - 1 < 3 ? TY - 1 : 3); ++dd) {
-              if (dd == d) {   // uniform branch: fixed register indices per case
-                v = a[dd] * ty.w[0];
-                v = __builtin_elementwise_fma(a[dd + 1], (f4)ty.w[1], v);
-                v = __builtin_elementwise_fma(a[dd + 2], (f4)ty.w[2], v);
-                v = __builtin_elementwise_fma(a[dd + 3], (f4)ty.w[3], v);
-              }
-            }
-          }
-          Vb[r * (vstride / 4) + e] = v;
-        }
-      }
-    };
-
-    if (job != jfirst) __syncthreads();   // the previous job's store tile (in V) fully read
-    stage(0);
-    __syncthreads();
-    const int nslab = L * H;
-    for (int it = 0; it < nslab; ++it) {
-      if (it + 1 < nslab) {
-  #if SKP_MAPS_PRIO
-        __builtin_amdgcn_s_setprio(SKP_MAPS_PRIO);
-  #endif
-        stage(it + 1);
-  #if SKP_MAPS_PRIO
-        __builtin_amdgcn_s_setprio(0);
-  #endif
-      }
-      const int l = it / H, bh = b * H + (it - l * H);
-      const f4* V4 = reinterpret_cast<const f4*>(V + ((it & 1) * TY + ry) * vstride) + li;
-      const float4* tw = TW + (l & 1) * TX;
-      const int4* tiw = TI + (l & 1) * TX;
-      float2* st = cl.stats[l];
-      const int yr = y0 + ry;
-  #pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const int xl = (wid - ry * WPR) * PXW + 4 * g + row;   // pixel of this 16-lane row
-        const int xr = min(xl, np - 1);
-        const float4 w = tw[xr];
-        const int4 ti = tiw[xr];
-        f4 zc[QPL];
-        float m = kPadLogit;
-  #pragma unroll
-        for (int c = 0; c < QPL; ++c) {
-          const f4 a0 = V4[ti.x + 16 * c], a1 = V4[ti.y + 16 * c];
-          const f4 a2 = V4[ti.z + 16 * c], a3 = V4[ti.w + 16 * c];
-          f4 v = a0 * w.x;
-          v = __builtin_elementwise_fma(a1, (f4)w.y, v);
-          v = __builtin_elementwise_fma(a2, (f4)w.z, v);
-          v = __builtin_elementwise_fma(a3, (f4)w.w, v);
-          zc[c] = v;
-          m = __builtin_fmaxf(__builtin_fmaxf(m, v.x), v.y);
-          m = __builtin_fmaxf(__builtin_fmaxf(m, v.z), v.w);
-          if (QPL > 4 || (c & 1)) __builtin_amdgcn_sched_barrier(0);
-        }
-        m = row16_max(m);
-        const f4 mb = (f4)(-m * L2E);
-        f4 sv = (f4)0.0f;
-  #pragma unroll
-        for (int c = 0; c < QPL; ++c) {
-          f4 ex = __builtin_elementwise_fma(zc[c], (f4)L2E, mb);
-          ex.x = __builtin_amdgcn_exp2f(ex.x);
-          ex.y = __builtin_amdgcn_exp2f(ex.y);
-          ex.z = __builtin_amdgcn_exp2f(ex.z);
-          ex.w = __builtin_amdgcn_exp2f(ex.w);
-          zc[c] = ex;
-          sv += ex;
-        }
-        const float inv = __builtin_amdgcn_rcpf(row16_sum((sv.x + sv.y) + (sv.z + sv.w)));
-  #pragma unroll
-        for (int c = 0; c < QPL; ++c) acc[g][c] = __builtin_elementwise_fma(zc[c], (f4)inv, acc[g][c]);
-        if (st && li == 0 && xl < np && ry < ny) {
-          const f2v mi = {m, inv};
-          SKP_MAPS_ST(reinterpret_cast<f2v*>(st)[((size_t)bh * R + yr) * R + x0 + xl], mi);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      __syncthreads();
-    }
-    // token-major store: tile row p = ry·TX + xl; round rd stages tokens [128 rd, 128 rd + 128)
-    constexpr int TS = 128 + 4;
-    constexpr int P = TY * TX;
-    float* tile = V;
-    float* ob = maps + (size_t)b * N * R * R + (size_t)y0 * R + x0;
-    const float rc = 1.0f / count;
-  #pragma unroll
-    for (int rd = 0; rd < (QPL + 1) / 2; ++rd) {
-      if (rd > 0) __syncthreads();
-  #pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const int p = ry * TX + (wid - ry * WPR) * PXW + 4 * g + row;
-  #pragma unroll
-        for (int h2 = 0; h2 < 2; ++h2) {
-          const int c = 2 * rd + h2;
-          if (c < QPL) *reinterpret_cast<f4*>(tile + p * TS + 4 * (li + 16 * h2)) = acc[g][c] * rc;
-        }
-      }
-      __syncthreads();
-      const int nr = min(128, Np - 128 * rd) / 4;
-      for (int e = tid; e < P * nr; e += kT) {
-        const int p = e % P, jq = e / P;
-        const int r = p / TX, xl = p - r * TX;
-        if (xl >= np || r >= ny) continue;
-        const f4 v = *reinterpret_cast<const f4*>(tile + p * TS + 4 * jq);
-        const int n = 128 * rd + 4 * jq;
-        float* o = ob + (size_t)r * R + xl;
-        if (n < N) SKP_MAPS_ST(o[(size_t)n * R * R], v.x);
-        if (n + 1 < N) SKP_MAPS_ST(o[(size_t)(n + 1) * R * R], v.y);
-        if (n + 2 < N) SKP_MAPS_ST(o[(size_t)(n + 2) * R * R], v.z);
-        if (n + 3 < N) SKP_MAPS_ST(o[(size_t)(n + 3) * R * R], v.w);
-      }
-    }
-  }
-}
-
 // ------------------------------------------------------------------------------------ fused bwd
 // Backward of skp_capture_maps_fwd, one (layer, b·H + h, output row y) per WAVE, no LDS and no
 // barriers.  The per-image map gradient is first transposed to pixel-major gT (B, R², N)
@@ -1566,92 +1358,28 @@ size_t maps_lds(int vstride, int qpl, int waves) {   // [2][P] taps ×2 + [2][vs
   return (16 * (size_t)waves * maps_pxw(qpl) + 2 * (size_t)vstride) * sizeof(float);
 }
 
-// workgroup size: 8 waves (two workgroups per CU) unless SKP_MAPS_WAVES=16 (one per CU) or 4 (four
-// per CU) (A/B switch, read per call)
-int maps_waves() {
-  const char* e = getenv("SKP_MAPS_WAVES");
-  const int v = e ? atoi(e) : 8;
-  return (v == 16 || v == 4) ? v : 8;
-}
+// 8-wave workgroups, a persistent grid of two per CU walking their XCD's rows in step (1003 vs
+// 1013 µs and FETCH_SIZE 955 vs 1070 MB against one job per workgroup,
+// profiles/r03ad_maps_persist_ab.txt; 4- and 16-wave workgroups measured slower,
+// profiles/r05w_maps_waves_ab.txt)
+constexpr int kMapWaves = 8;
 
-template <int QPL, int WAVES>
+template <int QPL>
 void launch_maps(const CapLayers& cl, int L, int B, int H, int N, int R, int vstride, size_t lds, float* maps,
                  hipStream_t st) {
+  constexpr int WAVES = kMapWaves;
   const int P = WAVES * maps_pxw(QPL);
   const int nchunks = (R + P - 1) / P;
   const int total = B * R * nchunks;
-  int grid = 8 * ((total + 7) / 8);
-  // persistent grid (default; SKP_MAPS_PERSIST=0: one job per workgroup, read per call): 2
-  // workgroups per CU walk their XCD's rows in step — 1003 vs 1013 µs, FETCH_SIZE 955 vs 1070 MB
-  // at the bench shape (profiles/r03ad_maps_persist_ab.txt)
-  const char* env = getenv("SKP_MAPS_PERSIST");
-  if (!(env && atoi(env) == 0)) {
-    static const int ncu = [] {
-      int dev = 0, n = 0;
-      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        n = 256;
-      return std::max(8, n / 8 * 8);
-    }();
-    grid = std::min(grid, (16 / WAVES) * ncu);   // multiple of 8
-  }
-  hipLaunchKernelGGL((capture_maps_kernel<QPL, WAVES>), dim3(grid), dim3(WAVES * WAVE), lds, st, cl, L, B, H, N, R,
-                     nchunks, vstride, (float)L * (float)H, maps);
-}
-
-template <int QPL>
-void launch_maps_w(int waves, const CapLayers& cl, int L, int B, int H, int N, int R, int vstride, size_t lds,
-                   float* maps, hipStream_t st) {
-  if (waves == 16) launch_maps<QPL, 16>(cl, L, B, H, N, R, vstride, lds, maps, st);
-  else if (waves == 4) launch_maps<QPL, 4>(cl, L, B, H, N, R, vstride, lds, maps, st);
-  else launch_maps<QPL, 8>(cl, L, B, H, N, R, vstride, lds, maps, st);
-}
-
-// tiled form (capture_maps_tile_kernel): one 16-wave workgroup per CU, TY-row × TX-pixel tiles
-constexpr int maps_tile_tx(int qpl, int ty) { return (16 / ty) * maps_pxw(qpl); }
-int maps_tile_vstride(const int* sizes, int L, int R, int qpl, int ty) {   // floats per V row buffer
-  const int TX = maps_tile_tx(qpl, ty), Np = 64 * qpl;
-  int ncmax = 1;
-  for (int l = 0; l < L; ++l) {
-    const int s = sizes[l];
-    ncmax = std::max(ncmax, std::min(s, (int)(((long long)TX * s + R - 1) / R) + 4));
-  }
-  const int tile = ty * TX * (128 + 4);   // the store tile fits in the 2 · TY row buffers
-  return (std::max(ncmax * Np, (tile + 2 * ty - 1) / (2 * ty)) + 3) & ~3;
-}
-size_t maps_tile_lds(int vstride, int qpl, int ty) {
-  return (16 * (size_t)maps_tile_tx(qpl, ty) + 2 * (size_t)ty * vstride) * sizeof(float);
-}
-
-// SKP_MAPS_TILE: rows per tile of the tiled kernel (2 or 4), 0 (default) = the one-row kernel
-int maps_tile_rows() {   // read per call (A/B tests switch it in-process)
-  const char* e = getenv("SKP_MAPS_TILE");
-  if (!e) return 0;
-  const int v = atoi(e);
-  return (v == 2 || v == 4) ? v : 0;
-}
-
-template <int QPL, int TY>
-void launch_maps_tile(const CapLayers& cl, int L, int B, int H, int N, int R, int vstride, size_t lds, float* maps,
-                      hipStream_t st) {
-  constexpr int TX = maps_tile_tx(QPL, TY);
-  const int nchunks = (R + TX - 1) / TX;
-  const int total = B * ((R + TY - 1) / TY) * nchunks;
   static const int ncu = [] {
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       n = 256;
     return std::max(8, n / 8 * 8);
   }();
-  const int grid = std::min(8 * ((total + 7) / 8), ncu);   // persistent: one workgroup per CU, multiple of 8
-  (void)lds;   // static LDS (kTileLdsFloats); the caller checked lds <= its size
-  hipLaunchKernelGGL((capture_maps_tile_kernel<QPL, TY>), dim3(grid), dim3(16 * WAVE), 0, st, cl, L, B, H, N, R,
+  const int grid = std::min(8 * ((total + 7) / 8), (16 / WAVES) * ncu);   // multiple of 8
+  hipLaunchKernelGGL((capture_maps_kernel<QPL, WAVES>), dim3(grid), dim3(WAVES * WAVE), lds, st, cl, L, B, H, N, R,
                      nchunks, vstride, (float)L * (float)H, maps);
-}
-template <int QPL>
-void launch_maps_tile_ty(int ty, const CapLayers& cl, int L, int B, int H, int N, int R, int vstride, size_t lds,
-                         float* maps, hipStream_t st) {
-  if (ty == 4) launch_maps_tile<QPL, 4>(cl, L, B, H, N, R, vstride, lds, maps, st);
-  else launch_maps_tile<QPL, 2>(cl, L, B, H, N, R, vstride, lds, maps, st);
 }
 }  // namespace
 
@@ -1676,27 +1404,15 @@ extern "C" int skp_capture_maps_fwd(const float* const* z_low, const int* sizes,
   }
   SKP_CHECK_ARG(aligned || (N % 4) != 0, "z_low pointers must be 16-B aligned");
   hipStream_t st = as_stream(stream);
-  const int ty = maps_tile_rows();
-  if (ty > 0 && (N % 4) == 0 && qpl >= 4 && qpl <= 8) {
-    const int vstride = maps_tile_vstride(sizes, L, R, qpl, ty);
-    const size_t lds = maps_tile_lds(vstride, qpl, ty);
-    if (lds <= sizeof(float) * kTileLdsFloats) {
-      if (qpl == 4) launch_maps_tile_ty<4>(ty, cl, L, B, H, N, R, vstride, lds, maps, st);
-      else launch_maps_tile_ty<8>(ty, cl, L, B, H, N, R, vstride, lds, maps, st);
-      SKP_LAUNCH_CHECK();
-      return SKP_OK;
-    }
-  }
-  const int waves = maps_waves();
-  const int vstride = maps_vstride(sizes, L, R, qpl, waves);
-  const size_t lds = maps_lds(vstride, qpl, waves);
+  const int vstride = maps_vstride(sizes, L, R, qpl, kMapWaves);
+  const size_t lds = maps_lds(vstride, qpl, kMapWaves);
   SKP_CHECK_ARG(lds <= 160 * 1024, "s*N too large for LDS");
   switch (qpl) {
-    case 1: launch_maps_w<1>(waves, cl, L, B, H, N, R, vstride, lds, maps, st); break;
-    case 2: launch_maps_w<2>(waves, cl, L, B, H, N, R, vstride, lds, maps, st); break;
-    case 4: launch_maps_w<4>(waves, cl, L, B, H, N, R, vstride, lds, maps, st); break;
-    case 8: launch_maps_w<8>(waves, cl, L, B, H, N, R, vstride, lds, maps, st); break;
-    default: launch_maps_w<16>(waves, cl, L, B, H, N, R, vstride, lds, maps, st); break;
+    case 1: launch_maps<1>(cl, L, B, H, N, R, vstride, lds, maps, st); break;
+    case 2: launch_maps<2>(cl, L, B, H, N, R, vstride, lds, maps, st); break;
+    case 4: launch_maps<4>(cl, L, B, H, N, R, vstride, lds, maps, st); break;
+    case 8: launch_maps<8>(cl, L, B, H, N, R, vstride, lds, maps, st); break;
+    default: launch_maps<16>(cl, L, B, H, N, R, vstride, lds, maps, st); break;
   }
   SKP_LAUNCH_CHECK();
   return SKP_OK;

@@ -15,12 +15,11 @@
 //
 // Kernels (per layer):
 //   sel_gather   zsel[bh][q][k] = z_low[bh][q][tok_k]                         (the selected logits)
-//   sel_dot      per (bh, row y): a_k, e_k = a_k·g_k, dot → E[bh][k][p] = e_k, pix[bh][p] = (mb, −dot)
-//                with mb = log2(1/Σ) − max·log2e, so a = exp2(z·log2e + mb)
-//   sel_adj      per (bh, k): es[bh][k] = bicubicᵀ(E[bh][k])  (R² → s², separable through an LDS table
-//                of the adjoint weights, deterministic)
-//   (r05 default: sel_doth = sel_dot + the horizontal half of sel_adj, E never leaves LDS, and
-//    sel_adjv = the vertical half on the R × s rows sel_doth wrote)
+//   sel_doth     per (bh, row y): a_k, e_k = a_k·g_k and dot → pix[bh][p] = (mb, −dot) with
+//                mb = log2(1/Σ) − max·log2e, so a = exp2(z·log2e + mb); the row's e_k stay in LDS and
+//                leave as the horizontal half of bicubicᵀ, Hs[bh][k][y][j] (R·s floats, not R²)
+//   sel_adjv     per (bh, k): es[bh][k] = the vertical half of bicubicᵀ over Hs (R × s → s²),
+//                deterministic
 //   sel_dense    per (bh, 128-token chunk): the dense part's adjoint, plus es at the selected tokens
 // sel_dense is the hot kernel.  One workgroup = R/PW bands of 64 (or, at R/s = 4, 32) lanes; band
 // w owns output columns [PW·w, PW·w + PW) of every row and lanes own token pairs (packed f32:
@@ -106,59 +105,6 @@ __device__ __forceinline__ void adj_range(int j, int S, int R, int& lo, int& hi)
   if (j == S - 1) hi = R - 1;
 }
 
-// ------------------------------------------------------------------------------ sel_dot
-// one block per (bh, y); threads over x.  Per pixel: a_k, e_k = a_k·g_k (E[bh][k][p]) and dot →
-// pix[bh][p] = (mb, −dot) with mb = log2(1/Σ) − max·log2e, so a = exp2(z·log2e + mb).
-// LDS: the vertical pass Vs[S][K] of the selected logits.
-__global__ __launch_bounds__(256) void sel_dot_kernel(SelSmall t, const float* __restrict__ zsel, int BH, int R,
-                                                      int H, int K, const long long* __restrict__ tok,
-                                                      const float* __restrict__ gsel, float gscale,
-                                                      float* __restrict__ E, float2* __restrict__ pix) {
-  extern __shared__ float Vs[];   // S × K
-  const int l = blockIdx.x / (BH * R);
-  const int rem = blockIdx.x - l * (BH * R);
-  const int bh = rem / R, y = rem % R;
-  const int b = bh / H;
-  const int S = t.s[l];
-  const size_t RRl = (size_t)R * R;
-  E += (size_t)l * BH * K * RRl;
-  pix += (size_t)l * BH * RRl;
-  const float2* stats = t.stats[l];
-  const Taps4 ty = bicubic_taps(y, S, R);
-  const float* zb = zsel + t.zoff[l] + (size_t)bh * S * S * K;
-  for (int e = threadIdx.x; e < S * K; e += blockDim.x) {
-    const int j = e / K, k = e - j * K;
-    float v = ty.w[0] * zb[((size_t)ty.i[0] * S + j) * K + k];
-    v = fmaf(ty.w[1], zb[((size_t)ty.i[1] * S + j) * K + k], v);
-    v = fmaf(ty.w[2], zb[((size_t)ty.i[2] * S + j) * K + k], v);
-    v = fmaf(ty.w[3], zb[((size_t)ty.i[3] * S + j) * K + k], v);
-    Vs[e] = v;
-  }
-  __syncthreads();
-  const size_t RR = (size_t)R * R;
-  for (int x = threadIdx.x; x < R; x += blockDim.x) {
-    const Taps4 tx = bicubic_taps(x, S, R);
-    const size_t p = (size_t)y * R + x;
-    const float2 st = stats[(size_t)bh * RR + p];
-    const float mb = __builtin_amdgcn_logf(st.y) - st.x * L2E;   // v_log_f32 = log2
-    float dot = 0.0f;
-    for (int k = 0; k < K; ++k) {
-      float e = 0.0f;
-      if (tok[(size_t)b * K + k] >= 0) {
-        float z = tx.w[0] * Vs[tx.i[0] * K + k];
-        z = fmaf(tx.w[1], Vs[tx.i[1] * K + k], z);
-        z = fmaf(tx.w[2], Vs[tx.i[2] * K + k], z);
-        z = fmaf(tx.w[3], Vs[tx.i[3] * K + k], z);
-        const float a = __builtin_amdgcn_exp2f(fmaf(z, L2E, mb));
-        e = a * (gsel[((size_t)b * K + k) * RR + p] * gscale);
-      }
-      dot += e;
-      E[((size_t)bh * K + k) * RR + p] = e;
-    }
-    pix[(size_t)bh * RR + p] = sel_pix(mb, dot);
-  }
-}
-
 // ------------------------------------------------------------------------------ sel_doth
 // sel_dot with the horizontal half of the sparse part's bicubicᵀ fused in (r05): the row's e_k stay
 // in LDS and leave as Hs[l][bh][k][y][j] = Σ_x A[j][x]·e_k[y][x] (R·s floats per (bh, k) instead
@@ -169,8 +115,8 @@ __global__ __launch_bounds__(256) void sel_dot_kernel(SelSmall t, const float* _
 // phase (RATIO/2 + t) mod RATIO: one fixed filter for every column, so column c is a 4·RATIO-tap dot
 // product against the row's e (zero-padded past both edges), and the clamped edge columns add their
 // virtual columns −2, −1, 0 / S − 1, S, S + 1 in that order.  Per column the terms run x ascending
-// from 0 — exactly sel_adjw's rolling-window sums and its edge order, so Hs (and es) are
-// bit-identical to the E path's.
+// from 0 — the summation order of a rolling window over the row (r04's sel_adjw, which took E
+// through HBM; r05 measured Hs and es bit-identical to it before it was removed in r06).
 constexpr int DOTH_PAD = 64;   // zero floats each side of a row's e (≥ 3.5·RATIO at RATIO ≤ 16)
 
 // virtual columns c = cv − 2, cv ∈ [0, S + 4): Vc[cv][k] = Σ_t W[t]·e_k[RATIO·(c − 2) + RATIO/2 + t]
@@ -274,7 +220,7 @@ __global__ __launch_bounds__(256) void sel_doth_kernel(SelSmall t, const float* 
   else if (ratio == 8) doth_columns<8>(W, Ep, EP, K, S, Vc);
   else doth_columns<4>(W, Ep, EP, K, S, Vc);
   __syncthreads();
-  // clamped edge columns: their virtual columns in sel_adjw's order (−2, −1, 0 / S − 1, S, S + 1)
+  // clamped edge columns: their virtual columns in order (−2, −1, 0 / S − 1, S, S + 1)
   for (int e = threadIdx.x; e < K * S; e += blockDim.x) {
     const int j = e % S, k = e / S;   // lanes over j: each k's row of s columns leaves contiguous
     float s;
@@ -293,179 +239,8 @@ __global__ __launch_bounds__(256) void sel_doth_kernel(SelSmall t, const float* 
   }
 }
 
-// ------------------------------------------------------------------------------ sel_adj
-// es[bh][k] = bicubicᵀ(E[bh][k]) (R² → s²), separable, through LDS: A[S][R + 1] (the adjoint matrix,
-// built once; rows padded so the lanes' different j hit different banks), the horizontal pass
-// Hs[y][j] = Σ_x A[j][x]·E[y][x] over 32-row tiles of E staged in LDS (rows padded to R + 1; lanes
-// take consecutive rows of the tile, so one wave reads 32 different banks), then
-// es[i][j] = Σ_y A[i][y]·Hs[y][j].  Fixed summation order (x, then y ascending).
-constexpr int SEL_ADJ_TILE = 32;
-constexpr int SEL_ADJ_PF = 8;   // float4 of the next tile each thread holds in registers
-// rows per E tile: 32, fewer where R > 256 so a tile fits the register prefetch (256 threads)
-inline int sel_adj_tile(int R) { return std::min(SEL_ADJ_TILE, std::max(1, SEL_ADJ_PF * 256 * 4 / R)); }
-__global__ __launch_bounds__(256) void sel_adj_kernel(SelSmall t, const float* __restrict__ E, int BHK, int smax,
-                                                      int R, int TR, float* __restrict__ es) {
-  extern __shared__ float sh[];
-  const int RP = R + 1;
-  const int l = blockIdx.x / BHK;
-  const int S = t.s[l];
-  float* A = sh;                 // S × (R + 1)
-  float* Hs = A + S * RP;        // R × S
-  float* Et = Hs + R * S;        // TR × (R + 1)
-  const size_t bk = blockIdx.x - (size_t)l * BHK;  // bh·K + k
-  const float* Eb = E + ((size_t)l * BHK + bk) * (size_t)R * R;
-  es += (size_t)l * BHK * smax * smax;
-  // the next tile of E in flight in registers while the current one is reduced (the map is read
-  // exactly once, 16 B per lane, coalesced)
-  float4 pf[SEL_ADJ_PF];
-  auto fetch = [&](int y0) {
-    const int n4 = min(TR, R - y0) * R / 4;
-    const float4* src = reinterpret_cast<const float4*>(Eb + (size_t)y0 * R);
-#pragma unroll
-    for (int m = 0; m < SEL_ADJ_PF; ++m) {
-      const int e = m * 256 + (int)threadIdx.x;
-      if (e < n4) pf[m] = src[e];
-    }
-  };
-  fetch(0);
-  for (int e = threadIdx.x; e < S * RP; e += blockDim.x) A[e] = 0.0f;
-  __syncthreads();
-  for (int x = threadIdx.x; x < R; x += blockDim.x) {
-    const Taps4 t = bicubic_taps(x, S, R);
-#pragma unroll
-    for (int m = 0; m < 4; ++m) A[t.i[m] * RP + x] += t.w[m];
-  }
-  for (int y0 = 0; y0 < R; y0 += TR) {
-    const int ny = min(TR, R - y0);
-#pragma unroll
-    for (int m = 0; m < SEL_ADJ_PF; ++m) {
-      const int e = m * 256 + (int)threadIdx.x;
-      if (e < ny * R / 4) {
-        const int yy = (4 * e) / R, x = 4 * e - yy * R;
-        float* d = Et + yy * RP + x;
-        d[0] = pf[m].x; d[1] = pf[m].y; d[2] = pf[m].z; d[3] = pf[m].w;
-      }
-    }
-    if (y0 + TR < R) fetch(y0 + TR);
-    __syncthreads();   // (the first pass also publishes A)
-    for (int e = threadIdx.x; e < ny * S; e += blockDim.x) {
-      const int yy = e % ny, j = e / ny;   // lanes over rows: distinct banks
-      int x0, x1;
-      adj_range(j, S, R, x0, x1);
-      const float* Aj = A + j * RP;
-      const float* Ey = Et + yy * RP;
-      float acc = 0.0f;
-      for (int x = x0; x <= x1; ++x) acc = fmaf(Aj[x], Ey[x], acc);
-      Hs[(y0 + yy) * S + j] = acc;
-    }
-    __syncthreads();
-  }
-  for (int e = threadIdx.x; e < S * S; e += blockDim.x) {
-    const int i = e / S, j = e - i * S;
-    int y0, y1;
-    adj_range(i, S, R, y0, y1);
-    const float* Ai = A + i * RP;
-    float acc = 0.0f;
-    for (int y = y0; y <= y1; ++y) acc = fmaf(Ai[y], Hs[y * S + j], acc);
-    es[bk * (size_t)S * S + e] = acc;
-  }
-}
-
-// sel_adj with the horizontal pass as a rolling window (the capture backward's column trick): one
-// thread per E row streams its R pixels once (16-B loads), keeping the adjoint of the 4 low-res
-// columns lo(x) … lo(x) + 3 its taps reach in registers; a column is complete once lo passes it
-// (lo never decreases) and leaves for Hs in LDS, virtual columns −2, −1 / S, S + 1 folding into 0 /
-// S − 1 as torch's clamped taps.  4 FMAs per pixel and no LDS reads of E or of an adjoint matrix
-// (the per-(row, column) dot products of sel_adj re-read a ≈35-wide band of both per output).
-// The vertical pass is sel_adj's.  Block = (layer, bh, k), R threads (R ≤ 256, a multiple of 16).
-__global__ __launch_bounds__(256) void sel_adjw_kernel(SelSmall t, const float* __restrict__ E, int BHK, int smax,
-                                                       int R, float* __restrict__ es) {
-  extern __shared__ float sh[];
-  const int RP = R + 1;
-  const int l = blockIdx.x / BHK;
-  const int S = t.s[l];
-  float* A = sh;                                   // S × (R + 1), the vertical pass's adjoint matrix
-  float* Hs = A + S * RP;                          // R × S
-  // [R] tap weights, 16-B aligned whatever S is (the launch sizes the LDS for the rounding)
-  float4* TW = reinterpret_cast<float4*>(Hs + ((R * S + S * RP + 3) & ~3) - S * RP);
-  int* TL = reinterpret_cast<int*>(TW + R);             // [R] first tap (unclamped)
-  const size_t bk = blockIdx.x - (size_t)l * BHK;  // bh·K + k
-  const float* Eb = E + ((size_t)l * BHK + bk) * (size_t)R * R;
-  es += (size_t)l * BHK * smax * smax;
-  const int y = threadIdx.x;
-  for (int e = y; e < S * RP; e += blockDim.x) A[e] = 0.0f;
-  __syncthreads();
-  if (y < R) {
-    const Taps4 tx = bicubic_taps(y, S, R);
-#pragma unroll
-    for (int m = 0; m < 4; ++m) A[tx.i[m] * RP + y] += tx.w[m];
-    TW[y] = make_float4(tx.w[0], tx.w[1], tx.w[2], tx.w[3]);
-    TL[y] = tx.lo;
-  }
-  __syncthreads();
-  if (y < R) {
-    const float4* row = reinterpret_cast<const float4*>(Eb + (size_t)y * R);
-    float* hrow = Hs + y * S;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f, pend = 0.f;
-    int base = -2, pt = 0;
-    auto emit = [&](int c, float v) {   // virtual column c complete; clamped columns accumulate in order
-      const int tt = min(max(c, 0), S - 1);
-      if (tt != pt) {
-        hrow[pt] = pend;
-        pt = tt;
-        pend = v;
-      } else {
-        pend += v;
-      }
-    };
-    // groups of 4 float4 (16 pixels), the next group's loads in flight while this one is reduced
-    float4 cur[4], nxt[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) cur[q] = q < R / 4 ? row[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int g0 = 0; g0 < R / 4; g0 += 4) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) nxt[q] = g0 + 4 + q < R / 4 ? row[g0 + 4 + q] : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int x = 4 * g0 + u;   // R is a multiple of 16 on this path
-        const float4 ev = cur[u >> 2];
-        const float e1 = (u & 3) == 0 ? ev.x : (u & 3) == 1 ? ev.y : (u & 3) == 2 ? ev.z : ev.w;
-        const int lo = TL[x];
-        while (base < lo) {
-          emit(base, a0);
-          a0 = a1; a1 = a2; a2 = a3; a3 = 0.0f;
-          ++base;
-        }
-        const float4 w = TW[x];
-        a0 = fmaf(w.x, e1, a0);
-        a1 = fmaf(w.y, e1, a1);
-        a2 = fmaf(w.z, e1, a2);
-        a3 = fmaf(w.w, e1, a3);
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
-    }
-    emit(base, a0);
-    emit(base + 1, a1);
-    emit(base + 2, a2);
-    emit(base + 3, a3);
-    hrow[pt] = pend;
-    for (int j = pt + 1; j < S; ++j) hrow[j] = 0.0f;   // columns no pixel reaches (none at R ≥ S)
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < S * S; e += blockDim.x) {
-    const int i = e / S, j = e - i * S;
-    int y0, y1;
-    adj_range(i, S, R, y0, y1);
-    const float* Ai = A + i * RP;
-    float acc = 0.0f;
-    for (int yy = y0; yy <= y1; ++yy) acc = fmaf(Ai[yy], Hs[yy * S + j], acc);
-    es[bk * (size_t)S * S + e] = acc;
-  }
-}
-
 // The vertical half of the sparse part's bicubicᵀ after sel_doth: es[i][j] = Σ_y A[i][y]·Hs[y][j]
-// (sel_adjw's final pass, y ascending) on the R × s rows sel_doth left in HBM.  Block = (layer,
+// (y ascending) on the R × s rows sel_doth left in HBM.  Block = (layer,
 // bh, k), 256 threads; LDS: the adjoint matrix A[S][R + 1] and the block's Hs rows [R][S].
 __global__ __launch_bounds__(256) void sel_adjv_kernel(SelSmall t, const float* __restrict__ Hsg, int BH, int BHK,
                                                        int smax, int R, float* __restrict__ es) {
@@ -511,10 +286,6 @@ struct SelLayers {   // up to 4 layers of the same s per launch
 
 // output columns per band and row: 16 where R/s ≥ 8; 8 at R/s = 4 (the s = 32 layers), which keeps
 // the band at 6 low-res columns and the registers under 128 (4 waves per SIMD)
-#ifndef SKP_SEL_LW4
-#define SKP_SEL_LW4 32   // lanes per band at R/s = 4 (A/B build: 64 = whole-wave bands in 16-wave blocks, the s = 16
-                         // jobs then two per block in the paired grid: bit-identical, slower, profiles/r05zf_sel_dual_ab.txt)
-#endif
 template <int RATIO>
 constexpr int sel_pw() { return RATIO >= 8 ? 16 : 8; }
 template <int RATIO>
@@ -523,7 +294,7 @@ constexpr int sel_nc() { return lo_rel(sel_pw<RATIO>() - 1, RATIO) + 6; }   // b
 // holds 2·R/PW bands in R/PW/2 waves (64-token chunks): the s = 32 block then needs 8 waves and
 // 57 KB of LDS like the s = 16 one, two share a CU, and one launch runs both (sel_dense_pair)
 template <int RATIO>
-constexpr int sel_lw() { return RATIO >= 8 ? 64 : SKP_SEL_LW4; }
+constexpr int sel_lw() { return RATIO >= 8 ? 64 : 32; }
 template <int RATIO, int S>
 constexpr int sel_threads() { return (S * RATIO / sel_pw<RATIO>()) * sel_lw<RATIO>(); }
 template <int RATIO, int S>
@@ -640,7 +411,7 @@ __device__ __forceinline__ void sel_dense_body(const SelLayers& sl, int BH, int 
         for (int w2 = wlo; w2 <= whi; ++w2) s += M[(w2 * NC + j + 2 - w2 * CS) * LW + lane];
       }
       if (n < N) {
-        if (esl) {   // es added here (single-stream order); else by sel_es_add_kernel after this launch
+        if (esl) {   // the sparse part es at the selected tokens, k order
           for (unsigned m = mx; m; m &= m - 1) s.x += esl[((size_t)__builtin_ctz(m) * S + r) * S + j];   // k order
           for (unsigned m = my; m; m &= m - 1) s.y += esl[((size_t)__builtin_ctz(m) * S + r) * S + j];
         }
@@ -760,50 +531,25 @@ void sel_dense_kernel(SelLayers sl, int BH, int H, int N, int K, const long long
 }
 
 // Two layer classes (e.g. SD-1.5's s = 16 layers and its s = 32 layer at R = 128) in ONE grid of
-// equal-size blocks: per XCD, its share of class A's jobs first, then its share of class B's, so
-// the shorter class-B blocks fill the slots class A's last round leaves idle (two launches left
-// half of the CUs idle in the s = 16 launch's last round and ran the s = 32 launch alone).
-// Two layer classes (e.g. SD-1.5's s = 16 layers and its s = 32 layer at R = 128) in ONE grid of
 // equal-size blocks: per XCD, its share of class A's blocks first, then its share of class B's, so
 // the class-B blocks fill the slots class A's last round leaves idle (two launches left half of the
-// CUs idle in the s = 16 launch's last round and ran the s = 32 launch alone).  A class-A job may
-// need fewer threads than a class-B one: a block then runs DA = threads(B) / threads(A) class-A jobs
-// side by side, each on its own slice of the threads and of the LDS (the jobs of one class run the
-// same barrier sequence; a block's surplus slots redo its last job, storing the same values).
+// CUs idle in the s = 16 launch's last round and ran the s = 32 launch alone).  (r05 measured a
+// 16-wave form with two class-A jobs per block side by side — bit-identical, 5% slower,
+// profiles/r05zf_sel_dual_ab.txt — removed in r06.)
 template <int RA, int SA, int RB, int SB>
 __global__ __launch_bounds__((sel_threads<RB, SB>()))
 void sel_dense_pair_kernel(SelLayers sa, int nca, int ja, SelLayers sb, int ncb, int jb, int BH, int H, int N, int K,
                            const long long* __restrict__ tok) {
-  constexpr int TA = sel_threads<RA, SA>(), TB = sel_threads<RB, SB>();
-  static_assert(TB % TA == 0, "class-A jobs must tile a class-B block");
-  constexpr int DA = TB / TA;
+  static_assert(sel_threads<RA, SA>() == sel_threads<RB, SB>(), "the two classes' blocks must be equal");
   constexpr int MA = sel_lds_m<RA, SA>(), MB = sel_lds_m<RB, SB>();
   constexpr int ZA = sel_lds_z<RA, SA>(), ZB = sel_lds_z<RB, SB>();
-  constexpr int LA = DA * (MA + ZA), LB = MB + ZB;
+  constexpr int LA = MA + ZA, LB = MB + ZB;
   __shared__ __attribute__((aligned(16))) f2 lds[LA > LB ? LA : LB];
-  const int ba = (ja + DA - 1) / DA;                 // class-A blocks
-  const int pa = (ba + 7) / 8, pb = (jb + 7) / 8;   // per-XCD shares
+  const int pa = (ja + 7) / 8, pb = (jb + 7) / 8;   // per-XCD shares
   const int xcd = blockIdx.x & 7, k = blockIdx.x >> 3;
   if (k < pa) {
-    const int blk = xcd * pa + k;
-    if (blk < ba) {
-      if constexpr (DA == 1) {   // compile-time LDS bases (a runtime slice offset costs every LDS access)
-        sel_dense_body<RA, SA>(sa, BH, H, N, K, tok, nca, blk, lds, lds + MA, threadIdx.x);
-      } else if constexpr (DA == 2) {   // each half on its own compile-time LDS slice
-        const int d = __builtin_amdgcn_readfirstlane((int)threadIdx.x / TA);
-        const int job = min(blk * 2 + d, ja - 1);
-        if (d == 0)
-          sel_dense_body<RA, SA>(sa, BH, H, N, K, tok, nca, job, lds, lds + MA, threadIdx.x);
-        else
-          sel_dense_body<RA, SA>(sa, BH, H, N, K, tok, nca, job, lds + (MA + ZA), lds + (2 * MA + ZA),
-                                 (int)threadIdx.x - TA);
-      } else {
-        const int d = (int)threadIdx.x / TA;
-        const int job = min(blk * DA + d, ja - 1);
-        f2* M = lds + d * (MA + ZA);
-        sel_dense_body<RA, SA>(sa, BH, H, N, K, tok, nca, job, M, M + MA, (int)threadIdx.x - d * TA);
-      }
-    }
+    const int job = xcd * pa + k;
+    if (job < ja) sel_dense_body<RA, SA>(sa, BH, H, N, K, tok, nca, job, lds, lds + MA, threadIdx.x);
   } else {
     const int job = xcd * pb + (k - pa);
     if (job < jb) sel_dense_body<RB, SB>(sb, BH, H, N, K, tok, ncb, job, lds, lds + MB, threadIdx.x);
@@ -825,9 +571,7 @@ void launch_dense_pair(const SelLayers& sa, int na, const SelLayers& sb, int nb,
   const int nca = (N + 2 * sel_lw<RA / SA>() - 1) / (2 * sel_lw<RA / SA>());
   const int ncb = (N + 2 * sel_lw<RB / SB>() - 1) / (2 * sel_lw<RB / SB>());
   const int ja = na * BH * nca, jb = nb * BH * ncb;
-  constexpr int DA = sel_threads<RB / SB, SB>() / sel_threads<RA / SA, SA>();
-  const int ba = (ja + DA - 1) / DA;
-  const int grid = 8 * ((ba + 7) / 8 + (jb + 7) / 8);
+  const int grid = 8 * ((ja + 7) / 8 + (jb + 7) / 8);
   hipLaunchKernelGGL((sel_dense_pair_kernel<RA / SA, SA, RB / SB, SB>), dim3(grid), dim3(sel_threads<RB / SB, SB>()), 0,
                      st, sa, nca, ja, sb, ncb, jb, BH, H, N, K, tok);
 }
@@ -879,56 +623,6 @@ bool dense_supported(int R, int S) {
   return false;
 }
 
-// The sparse part's final pass (r05: sel_adjw runs on a second stream beside sel_dense, so sel_dense
-// stores the dense part alone and the selected tokens get their es here): one thread per (layer,
-// head, low-res pixel q) adds es[l][bh][k][q] to dz[l][bh][q][tok_k] in k order — the order sel_dense's
-// emit used, so the result is bit-identical to adding them there.
-struct SelEs {
-  float* dz[SKP_MAX_LAYERS];
-  const float* es[SKP_MAX_LAYERS];
-  int s[SKP_MAX_LAYERS];
-  long long qoff[SKP_MAX_LAYERS + 1];   // prefix of BH·s² over layers
-};
-__global__ void sel_es_add_kernel(SelEs t, int L, int BH, int H, int N, int K, const long long* __restrict__ tok) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= t.qoff[L]) return;
-  int l = 0;
-  while (l + 1 < L && e >= t.qoff[l + 1]) ++l;
-  const long long le = e - t.qoff[l];
-  const int SS = t.s[l] * t.s[l];
-  const int bh = (int)(le / SS), q = (int)(le % SS);
-  const int b = bh / H;
-  float* dz = t.dz[l] + ((size_t)bh * SS + q) * N;
-  const float* es = t.es[l] + (size_t)bh * K * SS;   // [bh][k][S][S] at the layer's s (sel_adjw's layout)
-  for (int k = 0; k < K; ++k) {
-    const long long tk = tok[(size_t)b * K + k];
-    if (tk >= 0 && tk < N) dz[tk] += es[(size_t)k * SS + q];
-  }
-}
-
-// per-thread auxiliary stream + fork/join events of the current device (created once per thread and
-// device; a caller's stream is never shared across threads through them)
-struct AuxStream {
-  int dev = -1;
-  hipStream_t st = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-};
-AuxStream* aux_stream() {
-  static thread_local AuxStream a[16];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
-  AuxStream& x = a[dev];
-  if (x.dev != dev) {
-    int least = 0, greatest = 0;   // the auxiliary work yields the CUs to the caller's stream
-    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = 0;
-    if (hipStreamCreateWithPriority(&x.st, hipStreamNonBlocking, least) != hipSuccess) return nullptr;
-    if (hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) != hipSuccess) return nullptr;
-    if (hipEventCreateWithFlags(&x.join, hipEventDisableTiming) != hipSuccess) return nullptr;
-    x.dev = dev;
-  }
-  return &x;
-}
-
 // dense gradient from the sparse one (fallback): g[b][tok_k][p] = Σ_k gsel[b][k][p] (k order)
 __global__ void sel_scatter_kernel(const long long* __restrict__ tok, const float* __restrict__ gsel, int B, int K,
                                    int N, long long RR, float* __restrict__ g) {
@@ -943,7 +637,7 @@ __global__ void sel_scatter_kernel(const long long* __restrict__ tok, const floa
 }
 
 struct SelWs {   // workspace carve-up (floats)
-  size_t zsel, E, pix, es, total;
+  size_t zsel, hs, pix, es, total;
 };
 SelWs sel_ws(const int* sizes, int L, int B, int H, int R, int K) {
   SelWs w{};
@@ -954,32 +648,29 @@ SelWs sel_ws(const int* sizes, int L, int B, int H, int R, int K) {
   size_t zs = 0;
   for (int l = 0; l < L; ++l) zs += BH * (size_t)sizes[l] * sizes[l] * K;
   w.zsel = 0;
-  w.E = w.zsel + ((zs + 3) & ~(size_t)3);
-  w.pix = w.E + (size_t)L * BH * K * RR;
+  w.hs = w.zsel + ((zs + 3) & ~(size_t)3);                // sel_doth's Hs rows [l][bh][k][R][smax]
+  w.pix = w.hs + (((size_t)L * BH * K * R * smax + 3) & ~(size_t)3);
   w.es = w.pix + (size_t)L * BH * RR * 2;
   w.total = w.es + (size_t)L * BH * K * smax2;
   return w;
 }
 
-// Per-phase timing of the fast path (skp_sel_bwd_timing*): when enabled, each single-stream call
-// records 5 events on its stream — before sel_gather, after sel_gather, after sel_dot(h), after
-// the adjoint (sel_adjv / sel_adjw / sel_adj), after sel_dense — into a pool read back by
-// skp_sel_bwd_timing_read.  Off by default (no events recorded).
+// Per-phase timing of the fast path (skp_sel_bwd_timing*): when enabled, each call records 5 events
+// on its stream — before sel_gather, after sel_gather, after sel_doth, after sel_adjv, after
+// sel_dense — into a pool read back by skp_sel_bwd_timing_read.  A call's slot counts only once its
+// last event is recorded, so a call that returns early leaves no half-recorded slot behind.  Off by
+// default (no events recorded); one caller thread at a time (the bench).
 struct SelTiming {
   bool on = false;
-  int n = 0;                       // calls recorded since the last read
+  int n = 0;                       // complete calls recorded since the last read
   std::vector<hipEvent_t> ev;      // 5 per call
 };
 SelTiming& sel_timing() {
   static SelTiming t;
   return t;
 }
-bool getenv_fork_off() {
-  const char* e = getenv("SKP_SEL_FORK");
-  return !(e && atoi(e) == 1);
-}
 constexpr int SEL_TIMING_MAX_CALLS = 256;
-hipEvent_t* sel_timing_slot() {   // this call's 5 events, or null (off / pool full)
+hipEvent_t* sel_timing_slot() {   // the next call's 5 events (committed by sel_timing_commit), or null
   SelTiming& t = sel_timing();
   if (!t.on || t.n >= SEL_TIMING_MAX_CALLS) return nullptr;
   while ((int)t.ev.size() < 5 * (t.n + 1)) {
@@ -987,13 +678,19 @@ hipEvent_t* sel_timing_slot() {   // this call's 5 events, or null (off / pool f
     if (hipEventCreate(&e) != hipSuccess) return nullptr;
     t.ev.push_back(e);
   }
-  return &t.ev[5 * t.n++];
+  return &t.ev[5 * t.n];
 }
+void sel_timing_commit() { ++sel_timing().n; }
 
+// (R, s) pairs of the fast path: a compiled sel_dense kernel, and R/s ∈ {4, 8, 16} — the column
+// filters sel_doth instantiates (its W table holds 4·RATIO ≤ 64 taps)
 bool fast_path(const int* sizes, int L, int R, int N) {
-  if (N % 2 != 0 || N < 2) return false;
-  for (int l = 0; l < L; ++l)
+  if (N % 2 != 0 || N < 2 || R > 256) return false;
+  for (int l = 0; l < L; ++l) {
     if (!dense_supported(R, sizes[l])) return false;
+    const int ratio = R / sizes[l];
+    if (R % sizes[l] != 0 || (ratio != 4 && ratio != 8 && ratio != 16)) return false;
+  }
   return true;
 }
 
@@ -1042,11 +739,14 @@ extern "C" int skp_capture_maps_bwd_sel(const float* const* z_low, const int* si
   }
   const SelWs wsz = sel_ws(sizes, L, B, H, R, K);
   float* zsel = workspace + wsz.zsel;
-  float* E = workspace + wsz.E;
+  float* hs = workspace + wsz.hs;
   float2* pix = reinterpret_cast<float2*>(workspace + wsz.pix);
   float* es = workspace + wsz.es;
-  int smax = 1;
-  for (int l = 0; l < L; ++l) smax = std::max(smax, sizes[l]);
+  int smax = 1, rmax = 1;
+  for (int l = 0; l < L; ++l) {
+    smax = std::max(smax, sizes[l]);
+    rmax = std::max(rmax, R / sizes[l]);
+  }
   SelSmall t{};
   t.zoff[0] = 0;
   for (int l = 0; l < L; ++l) {
@@ -1055,99 +755,28 @@ extern "C" int skp_capture_maps_bwd_sel(const float* const* z_low, const int* si
     t.s[l] = sizes[l];
     t.zoff[l + 1] = t.zoff[l] + (long long)BH * sizes[l] * sizes[l] * K;
   }
-  // r05 default: sel_doth + sel_adjv (the horizontal half of bicubicᵀ in the dot kernel, no R² E
-  // rows in HBM); SKP_SEL_DOTH=0: sel_dot + sel_adjw / sel_adj through E (A/B), read per call
-  const bool doth = [] {
-    const char* e = getenv("SKP_SEL_DOTH");
-    return !(e && atoi(e) == 0);
-  }() && R <= 256;
-  hipEvent_t* tev = getenv_fork_off() ? sel_timing_slot() : nullptr;
+  hipEvent_t* tev = sel_timing_slot();
   if (tev) (void)hipEventRecord(tev[0], st);
   hipLaunchKernelGGL(sel_gather_kernel, dim3((unsigned)((t.zoff[L] + 255) / 256)), dim3(256), 0, st, t, L, BH, N, H,
                      sel_tok, K, zsel);
   SKP_LAUNCH_CHECK();
   if (tev) (void)hipEventRecord(tev[1], st);
-  if (doth) {
-    int rmax = 1;
-    for (int l = 0; l < L; ++l) rmax = std::max(rmax, R / sizes[l]);
-    const size_t lds = (size_t)(64 + ((smax * K + 3) & ~3) + K * (R + 2 * DOTH_PAD + 4) + K * (R / 4 + 4)) *
-                       sizeof(float);
-    if (rmax <= 8)
-      hipLaunchKernelGGL(sel_doth_kernel<8>, dim3((unsigned)(L * BH * R)), dim3(R), lds, st, t, zsel, BH, R, H, K,
-                         sel_tok, gsel, gscale, smax, E, pix);
-    else
-      hipLaunchKernelGGL(sel_doth_kernel<16>, dim3((unsigned)(L * BH * R)), dim3(R), lds, st, t, zsel, BH, R, H, K,
-                         sel_tok, gsel, gscale, smax, E, pix);
-  } else {
-    hipLaunchKernelGGL(sel_dot_kernel, dim3((unsigned)(L * BH * R)), dim3(std::min(R, 256)),
-                       (size_t)smax * K * sizeof(float), st, t, zsel, BH, R, H, K, sel_tok, gsel, gscale, E, pix);
-  }
+  // sel_doth: per (layer, bh, row) a_k, e_k = a_k·g_k and dot, with the horizontal half of the
+  // sparse part's bicubicᵀ applied in LDS (Hs rows; the R² e rows never reach HBM)
+  const size_t lds = (size_t)(64 + ((smax * K + 3) & ~3) + K * (R + 2 * DOTH_PAD + 4) + K * (R / 4 + 4)) * sizeof(float);
+  if (rmax <= 8)
+    hipLaunchKernelGGL(sel_doth_kernel<8>, dim3((unsigned)(L * BH * R)), dim3(R), lds, st, t, zsel, BH, R, H, K, sel_tok,
+                       gsel, gscale, smax, hs, pix);
+  else
+    hipLaunchKernelGGL(sel_doth_kernel<16>, dim3((unsigned)(L * BH * R)), dim3(R), lds, st, t, zsel, BH, R, H, K,
+                       sel_tok, gsel, gscale, smax, hs, pix);
   SKP_LAUNCH_CHECK();
   if (tev) (void)hipEventRecord(tev[2], st);
-  // SKP_SEL_FORK=1: the sparse part es = bicubicᵀ(E) (sel_adjw / sel_adj), which needs only E, on a
-  // low-priority auxiliary stream concurrently with sel_dense, whose emits then leave es out;
-  // sel_es_add_kernel adds it once both are done (bit-identical).  Measured SLOWER at the bench shape
-  // (mapssel8 1223-1237 vs 1145-1161 us, profiles/r05g_sel_fork_ab.txt: the small blocks take CU
-  // slots from sel_dense's last round), so the default (0) keeps one stream, es added in the emits.
-  const bool fork_env = [] {   // read per call (the A/B test switches it in-process)
-    const char* e = getenv("SKP_SEL_FORK");
-    return e && atoi(e) == 1;
-  }();
-  AuxStream* aux = fork_env ? aux_stream() : nullptr;
-  hipStream_t adj_st = st;
-  if (aux) {   // E is complete here; the auxiliary stream's sel_adjw is enqueued after sel_dense
-    SKP_CHECK_ARG(hipEventRecord(aux->fork, st) == hipSuccess && hipStreamWaitEvent(aux->st, aux->fork, 0) == hipSuccess,
-                  "fork event failed");
-    adj_st = aux->st;
-  }
-  auto launch_adj = [&]() -> int {
-  // the rolling-window horizontal pass (sel_adjw_kernel: 78 vs 104 us at the bench shape,
-  // profiles/r04aa_sel_adj_ab.txt); SKP_SEL_ADJ=0: sel_adj's per-output banded dot products (A/B)
-  static const bool adj_win = [] {
-    const char* e = getenv("SKP_SEL_ADJ");
-    return !(e && atoi(e) == 0);
-  }();
-  if (doth) {   // E holds sel_doth's Hs rows [l][bh][k][R][smax]
-    hipLaunchKernelGGL(sel_adjv_kernel, dim3((unsigned)(L * BH * K)), dim3(256),
-                       (size_t)(smax * (R + 1) + R * smax) * sizeof(float), adj_st, t, E, BH, BH * K, smax, R, es);
-  } else if (adj_win && R <= 256 && R % 16 == 0) {
-    hipLaunchKernelGGL(sel_adjw_kernel, dim3((unsigned)(L * BH * K)), dim3(R),
-                       (size_t)(smax * (R + 1) + R * smax + 3 + 5 * R) * sizeof(float), adj_st, t, E, BH * K, smax, R,
-                       es);
-  } else {
-    const int tr = sel_adj_tile(R);
-    hipLaunchKernelGGL(sel_adj_kernel, dim3((unsigned)(L * BH * K)), dim3(256),
-                       (size_t)(smax * (R + 1) + R * smax + tr * (R + 1)) * sizeof(float), adj_st, t, E, BH * K, smax, R,
-                       tr, es);
-  }
+  // sel_adjv: the vertical half → es[l][bh][k] (s × s per selected row)
+  hipLaunchKernelGGL(sel_adjv_kernel, dim3((unsigned)(L * BH * K)), dim3(256),
+                     (size_t)(smax * (R + 1) + R * smax) * sizeof(float), st, t, hs, BH, BH * K, smax, R, es);
   SKP_LAUNCH_CHECK();
-  if (aux) SKP_CHECK_ARG(hipEventRecord(aux->join, aux->st) == hipSuccess, "join event failed");
-  return SKP_OK;
-  };
-  if (!aux) {   // single stream: es before sel_dense, which adds it in its emits
-    const int rc = launch_adj();
-    if (rc != SKP_OK) return rc;
-    if (tev) (void)hipEventRecord(tev[3], st);
-  }
-  auto finish = [&]() -> int {   // launch the auxiliary sel_adjw, join it, add es at the selected tokens
-    if (tev) (void)hipEventRecord(tev[4], st);
-    if (!aux) return SKP_OK;
-    const int rc = launch_adj();
-    if (rc != SKP_OK) return rc;
-    SKP_CHECK_ARG(hipStreamWaitEvent(st, aux->join, 0) == hipSuccess, "join wait failed");
-    SelEs te{};
-    te.qoff[0] = 0;
-    for (int l = 0; l < L; ++l) {
-      te.dz[l] = dz_low[l];
-      te.es[l] = es + (size_t)l * BH * K * smax * smax;
-      te.s[l] = sizes[l];
-      te.qoff[l + 1] = te.qoff[l] + (long long)BH * sizes[l] * sizes[l];
-    }
-    hipLaunchKernelGGL(sel_es_add_kernel, dim3((unsigned)((te.qoff[L] + 255) / 256)), dim3(256), 0, st, te, L, BH, H, N,
-                       K, sel_tok);
-    SKP_LAUNCH_CHECK();
-    return SKP_OK;
-  };
+  if (tev) (void)hipEventRecord(tev[3], st);
   // the dense part: layers of equal s share a class (up to 4 per launch); two classes that have
   // a paired kernel (SD-1.5: s = 16 and 32 at R = 128) run as one launch
   SelLayers cls[SKP_MAX_LAYERS];
@@ -1161,7 +790,7 @@ extern "C" int skp_capture_maps_bwd_sel(const float* const* z_low, const int* si
       if (done[m] || sizes[m] != sizes[l]) continue;
       sl.z[nl] = z_low[m];
       sl.pix[nl] = pix + (size_t)m * BH * RR;
-      sl.es[nl] = aux ? nullptr : es + (size_t)m * BH * K * smax * smax;
+      sl.es[nl] = es + (size_t)m * BH * K * smax * smax;
       sl.dz[nl] = dz_low[m];
       done[m] = true;
       ++nl;
@@ -1171,18 +800,18 @@ extern "C" int skp_capture_maps_bwd_sel(const float* const* z_low, const int* si
     cls_n[ncls] = nl;
     ++ncls;
   }
-  if (ncls == 2 && dense_pair_launch(R, cls_s[0], cls[0], cls_n[0], cls_s[1], cls[1], cls_n[1], BH, H, N, K, sel_tok,
-                                     st)) {
-    SKP_LAUNCH_CHECK();
-    return finish();
+  if (!(ncls == 2 && dense_pair_launch(R, cls_s[0], cls[0], cls_n[0], cls_s[1], cls[1], cls_n[1], BH, H, N, K, sel_tok,
+                                       st))) {
+    for (int c = 0; c < ncls; ++c)
+      SKP_CHECK_ARG(dense_launch(R, cls_s[c], cls[c], cls_n[c], BH, H, N, K, sel_tok, st),
+                    "internal: no sel_dense kernel for this shape");
   }
-  for (int c = 0; c < ncls; ++c) {
-    if (!dense_launch(R, cls_s[c], cls[c], cls_n[c], BH, H, N, K, sel_tok, st)) {
-      SKP_CHECK_ARG(false, "internal: no sel_dense kernel for this shape");
-    }
-    SKP_LAUNCH_CHECK();
+  SKP_LAUNCH_CHECK();
+  if (tev) {
+    (void)hipEventRecord(tev[4], st);
+    sel_timing_commit();
   }
-  return finish();
+  return SKP_OK;
 }
 
 extern "C" int skp_sel_bwd_timing(int enable) {

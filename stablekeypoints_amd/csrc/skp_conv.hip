@@ -40,6 +40,17 @@
 
 using namespace skp;
 
+// Timing-probe builds only (tools/build_variant.sh, e.g. EXTRA=-DSKP_WINO2_DEBUG=8); the shipped
+// library is built with 0.  wino_f4_kernel: 1 drop x loads, 2 drop U loads, 4 skip transforms,
+// 8 skip MFMAs.  wino2_kernel: 1 skip transforms, 2 skip MFMAs, 4 skip input DMA, 8 skip weight
+// DMA, 16 skip the stage loop, 32 skip the epilogue, 64 skip its global stores.
+#ifndef SKP_WINO_DEBUG
+#define SKP_WINO_DEBUG 0
+#endif
+#ifndef SKP_WINO2_DEBUG
+#define SKP_WINO2_DEBUG 0
+#endif
+
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -428,9 +439,9 @@ extern "C" int skp_conv3x3_wino(const float* x, const float* U, const float* bia
   const long long ntiles = (long long)B * tpi;
   SKP_CHECK_ARG(ntiles <= 0x7fffffffLL - kMT, "too many tiles");
   SKP_CHECK_ARG((long long)B * C * H * W * 4 < 0x7fffffffLL, "input larger than 2 GiB (32-bit buffer offsets)");
-  // at most 32 tiles (8² at batch 8): 32-tile × 64-channel workgroups (SKP_WINO_WIDE=0: off)
-  static const bool wide_ok = !getenv("SKP_WINO_WIDE") || atoi(getenv("SKP_WINO_WIDE")) != 0;
-  const bool wide = wide_ok && ntiles <= 32 && K % 64 == 0;
+  // at most 32 tiles (8² at batch 8): 32-tile × 64-channel workgroups (ops.wino_conv's planner
+  // mirrors this rule)
+  const bool wide = ntiles <= 32 && K % 64 == 0;
   const int mt = wide ? 32 : kMT;
   const int ntb = (int)((ntiles + mt - 1) / mt), nkb = K / (wide ? 64 : kNC);
   SKP_CHECK_ARG((long long)ntb * nkb * nsplit <= 0x7fffffffLL, "grid too large");
@@ -439,7 +450,7 @@ extern "C" int skp_conv3x3_wino(const float* x, const float* U, const float* bia
   const int kb_major = ubytes > (2LL << 20);
   const int epi = nsplit > 1 ? 0 : (bias ? 1 : 0) | (residual ? 2 : 0);
   float* out = nsplit > 1 ? ws : y;
-  static const int dbg = getenv("SKP_WINO_DEBUG") ? atoi(getenv("SKP_WINO_DEBUG")) : 0;   // dev: 1 drop x loads, 2 drop U loads, 4 skip transforms, 8 skip MFMAs
+  const int dbg = SKP_WINO_DEBUG;
   hipStream_t st = as_stream(stream);
   const dim3 grid((unsigned)(ntb * nkb * nsplit));
 #define SKP_WG(E)                                                                                                    \
@@ -531,7 +542,6 @@ struct GeoT : GeoN<TXB, NW> {
 constexpr int kUP = 40;                    // floats per (input, output channel) U row
 constexpr int kUF = kCK * kNC * kUP;       // 5120 floats = 20 KB per U slot
 constexpr int kUInstr = kUF / 256;         // 20
-constexpr int kThreads = 512;
 constexpr unsigned kOOB = 0x80000000u;     // buffer offset past any num_records (< 2 GiB): loads 0
 static_assert(kUF % 256 == 0, "whole 1-KB chunks");
 static_assert((4 * GeoT<8>::RAWF + 3 * kUF) * 4 <= 160 * 1024 && 3 * (GeoT<4>::RAWF + kUF) * 4 <= 160 * 1024, "LDS");
@@ -1148,17 +1158,12 @@ extern "C" int skp_wino2_weights(const float* w, int K, int C, int flip, float* 
 // the odd positions (2oy + 1, 2ox + 1).  The Winograd kernel computes the 32×32 blocks and its epilogue
 // stores only the odd rows / columns (+ bias): no padded copy, no NCHW↔NHWC transposes, no bias pass.
 namespace {
-// flag 128 of the kernels' dbg word: non-temporal output stores, for outputs larger than the
-// Infinity Cache (the next layer re-reads them from HBM either way; the stream then does not
-// evict the input regions / weights the other workgroups re-read from L2).  SKP_WINO_NT: 0 off,
-// 2 always, default 1 = outputs ≥ SKP_WINO_NT_MB (256) MB; read per call.
+// flag 128 of the kernels' flag word: non-temporal output stores, for outputs of at least 256 MB
+// (larger than the Infinity Cache: the next layer re-reads them from HBM either way, and the stream
+// then does not evict the input regions / weights the other workgroups re-read from L2)
 int wino_nt_flag(long long out_bytes, int nsplit) {
   if (nsplit > 1) return 0;   // split-K partials are re-read by the reduction
-  const char* e = getenv("SKP_WINO_NT");
-  const int mode = e ? atoi(e) : 1;
-  const char* m = getenv("SKP_WINO_NT_MB");
-  const long long thr = (m ? atoll(m) : 256) << 20;
-  return (mode == 2 || (mode == 1 && out_bytes >= thr)) ? 128 : 0;
+  return out_bytes >= (256LL << 20) ? 128 : 0;
 }
 }  // namespace
 
@@ -1173,28 +1178,20 @@ extern "C" int skp_conv3x3s2_wino2(const float* x, const float* U, const float* 
   SKP_CHECK_ARG(nsplit == 1 || ws, "split-K needs a workspace of nsplit·B·K·(H/2)·(W/2) floats");
   SKP_CHECK_ARG(aligned16(x) && aligned16(U) && aligned16(y) && (!ws || aligned16(ws)), "tensors must be 16-byte aligned");
   SKP_CHECK_ARG((long long)B * C * H * W * 4 < 0x7fffffffLL, "input larger than 2 GiB (32-bit buffer offsets)");
-  const char* he = getenv("SKP_WINO2_HALF");   // half-height blocks (see skp_conv3x3_wino2)
-  const bool half = !(he && atoi(he) == 0);
-  const int bw = W / 32, bpi = (H / (half ? 16 : 32)) * bw;
+  // half-height blocks (see skp_conv3x3_wino2)
+  const int bw = W / 32, bpi = (H / 16) * bw;
   const long long nblk = (long long)B * bpi;
   const int nkb = K / w2::kNC;
   SKP_CHECK_ARG(nblk * nkb * nsplit <= 0x7fffffffLL, "grid too large");
-  static const int dbg = getenv("SKP_WINO2_DEBUG") ? atoi(getenv("SKP_WINO2_DEBUG")) : 0;
   float* out = nsplit > 1 ? ws : y;
   hipStream_t st = as_stream(stream);
   const dim3 grid((unsigned)(nblk * nkb * nsplit));
-  const int fl = dbg | wino_nt_flag((long long)B * K * (H / 2) * (W / 2) * 4, nsplit);
-  if (half && nsplit == 1 && bias)
+  const int fl = SKP_WINO2_DEBUG | wino_nt_flag((long long)B * K * (H / 2) * (W / 2) * 4, nsplit);
+  if (nsplit == 1 && bias)
     hipLaunchKernelGGL((wino2_kernel<5, 8, 4>), grid, dim3(4 * WAVE), 0, st, x, U, bias, nullptr, out, B, C, K, H, W,
                        bw, bpi, (int)nblk, nkb, 0, C / nsplit, fl, nullptr);
-  else if (half)
-    hipLaunchKernelGGL((wino2_kernel<4, 8, 4>), grid, dim3(4 * WAVE), 0, st, x, U, nullptr, nullptr, out, B, C, K, H,
-                       W, bw, bpi, (int)nblk, nkb, 0, C / nsplit, fl, nullptr);
-  else if (nsplit == 1 && bias)
-    hipLaunchKernelGGL((wino2_kernel<5, 8>), grid, dim3(w2::kThreads), 0, st, x, U, bias, nullptr, out, B, C, K, H, W,
-                       bw, bpi, (int)nblk, nkb, 0, C / nsplit, fl, nullptr);
   else
-    hipLaunchKernelGGL((wino2_kernel<4, 8>), grid, dim3(w2::kThreads), 0, st, x, U, nullptr, nullptr, out, B, C, K, H,
+    hipLaunchKernelGGL((wino2_kernel<4, 8, 4>), grid, dim3(4 * WAVE), 0, st, x, U, nullptr, nullptr, out, B, C, K, H,
                        W, bw, bpi, (int)nblk, nkb, 0, C / nsplit, fl, nullptr);
   SKP_LAUNCH_CHECK();
   if (nsplit > 1) return splitk_reduce(ws, nsplit, B, K, (H / 2) * (W / 2), bias, nullptr, y, st);
@@ -1220,26 +1217,17 @@ extern "C" int skp_conv3x3_wino2_gn(const float* x, const float* U, const float*
                 "tensors must be 16-byte aligned");
   SKP_CHECK_ARG((long long)B * C * H * W * 4 < 0x7fffffffLL, "input larger than 2 GiB (32-bit buffer offsets)");
   // half-height blocks (32 × 16 pixels, 4 waves, two workgroups per CU: one's prologue / epilogue
-  // overlaps the other's stage loop): the default, 5-11% faster at every VAE / UNet shape
-  // (profiles/r03al_wino_half_ab.txt); SKP_WINO2_HALF=0 = the 32 × 32 single-workgroup form
-  const char* he = getenv("SKP_WINO2_HALF");
-  const bool half = !(he && atoi(he) == 0);
-  // the 16×16 geometry's 4-wave form (two images per workgroup, two workgroups per CU; 2-slot
-  // raw and weight rings): the default, SKP_WINO2_HALF16=0 = four images per workgroup
-  // (profiles/r03ap_wino_half16_ab.txt)
-  const char* h16 = getenv("SKP_WINO2_HALF16");
-  const bool half16 = g16 && !(h16 && atoi(h16) == 0);
-  const int bw = W / 32, bpi = (H / (half ? 16 : 32)) * bw;
-  const long long nblk = g16 ? B / (half16 ? 2 : 4) : (long long)B * bpi;
+  // overlaps the other's stage loop), 5-11% faster than the 32 × 32 one-workgroup-per-CU form at
+  // every VAE / UNet shape (profiles/r03al_wino_half_ab.txt); the 16×16 geometry as two images per
+  // 4-wave workgroup, two workgroups per CU (profiles/r03ap_wino_half16_ab.txt)
+  const int bw = W / 32, bpi = (H / 16) * bw;
+  const long long nblk = g16 ? B / 2 : (long long)B * bpi;
   const int nkb = K / w2::kNC;
   SKP_CHECK_ARG(nblk * nkb * nsplit <= 0x7fffffffLL, "grid too large");
-  // dev switches (SKP_WINO2_DEBUG): 1 skip transforms, 2 skip MFMAs, 4 skip input DMA, 8 skip weight DMA,
-  // 16 skip the stage loop, 32 skip the epilogue, 64 skip its global stores; SKP_WINO2_ORDER 1 tile-major, 2 channel-block-major
-  static const int dbg = getenv("SKP_WINO2_DEBUG") ? atoi(getenv("SKP_WINO2_DEBUG")) : 0;
-  static const int order = getenv("SKP_WINO2_ORDER") ? atoi(getenv("SKP_WINO2_ORDER")) : 0;
+  const int dbg = SKP_WINO2_DEBUG;
   // tile-major (the channel blocks of one pixel block back to back, sharing its input region in
   // L2) measured 1-2% ahead of channel-block-major at every VAE / UNet shape, U size regardless
-  const int kb_major = order == 2;
+  const int kb_major = 0;
   const int epi = nsplit > 1 ? 0 : (bias ? 1 : 0) | (residual ? 2 : 0);
   float* out = nsplit > 1 ? ws : y;
   hipStream_t st = as_stream(stream);
@@ -1247,17 +1235,11 @@ extern "C" int skp_conv3x3_wino2_gn(const float* x, const float* U, const float*
   const int fl = dbg | wino_nt_flag((long long)B * K * H * W * 4, nsplit);
   float2* gnp = reinterpret_cast<float2*>(gn_part);
 #define SKP_WG2(E)                                                                                            \
-  if (half16)                                                                                                 \
+  if (g16)                                                                                                    \
     hipLaunchKernelGGL((wino2_kernel<E, 4, 4>), grid, dim3(4 * WAVE), 0, st, x, U, bias, residual, out, B, C, K,  \
                        H, W, bw, bpi, (int)nblk, nkb, kb_major, C / nsplit, fl, nullptr);                              \
-  else if (g16)                                                                                               \
-    hipLaunchKernelGGL((wino2_kernel<E, 4>), grid, dim3(w2::kThreads), 0, st, x, U, bias, residual, out, B, C, K, \
-                       H, W, bw, bpi, (int)nblk, nkb, kb_major, C / nsplit, fl, nullptr);                              \
-  else if (half)                                                                                              \
-    hipLaunchKernelGGL((wino2_kernel<E, 8, 4>), grid, dim3(4 * WAVE), 0, st, x, U, bias, residual, out, B, C, K,  \
-                       H, W, bw, bpi, (int)nblk, nkb, kb_major, C / nsplit, fl, gnp);                              \
   else                                                                                                        \
-    hipLaunchKernelGGL((wino2_kernel<E, 8>), grid, dim3(w2::kThreads), 0, st, x, U, bias, residual, out, B, C, K, \
+    hipLaunchKernelGGL((wino2_kernel<E, 8, 4>), grid, dim3(4 * WAVE), 0, st, x, U, bias, residual, out, B, C, K,  \
                        H, W, bw, bpi, (int)nblk, nkb, kb_major, C / nsplit, fl, gnp)
   switch (epi) {
     case 0: SKP_WG2(0); break;

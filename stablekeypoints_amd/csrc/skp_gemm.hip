@@ -271,22 +271,14 @@ extern "C" int skp_bgemm_f32_2b(const float* A, long long sAo, long long sAb, lo
     return (w128 - n) <= (w64 - n) + n / 16 ? 128 : 64;
   };
   int bm = pick(M), bn = pick(N);
-  static const bool small_only = [] {   // SKP_BGEMM_TILE=64: A/B switch to the 64×64 tile only
-    const char* e = getenv("SKP_BGEMM_TILE");
-    return e && atoi(e) == 64;
-  }();
-  if (fa == 2 || fb == 2 || small_only) bm = bn = 64;
+  if (fa == 2 || fb == 2) bm = bn = 64;
   const long long tiles128 = (long long)batch * ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   if (tiles128 < 512) bm = bn = 64;   // too few tiles to fill 256 CUs twice: keep the small tile
   const int tiles_m = (M + bm - 1) / bm, tiles_n = (N + bn - 1) / bn;
   const long long tiles = (long long)batch * tiles_m * tiles_n;
   SKP_CHECK_ARG(tiles < (1LL << 31), "too many tiles");
-  const int occ_def = (bm == 128 && bn == 128) ? 2 : (bm == 128 || bn == 128) ? 3 : kOcc;
-  static const int occ_env = [] {
-    const char* e = getenv("SKP_BGEMM_OCC");
-    return e ? std::max(1, atoi(e)) : 0;
-  }();
-  const int occ = occ_env ? occ_env : occ_def;
+  // workgroups per CU (occupancy at 1, 2 or 3 per CU measured the same on q·kᵀ)
+  const int occ = (bm == 128 && bn == 128) ? 2 : (bm == 128 || bn == 128) ? 3 : kOcc;
   const int grid = (int)std::min<long long>(8 * ((tiles + 7) / 8), 256LL * occ) & ~7;
   hipStream_t st = as_stream(stream);
 #define SKP_BG3(X, Y, TM, TN, WM, WN)                                                                           \
@@ -298,17 +290,12 @@ extern "C" int skp_bgemm_f32_2b(const float* A, long long sAo, long long sAb, lo
     hipLaunchKernelGGL((bgemm_kernel<X, Y, false, TM, TN, WM, WN>), dim3(grid), dim3(WM * WN * WAVE), 0, st, A, \
                        sAb, sAm, sAk, B, sBb, sBk, sBn, C, sCb, sCm, sCn, M, N, K, alpha, tiles_m, tiles_n,     \
                        (int)tiles, hb, sAo, sBo, sCo)
-  // 128-edge tiles run 8 waves (4 per SIMD at two workgroups per CU) unless SKP_BGEMM_WAVES=4
-  static const bool four_waves = [] {
-    const char* e = getenv("SKP_BGEMM_WAVES");
-    return e && atoi(e) == 4;
-  }();
+  // 128-edge tiles run 8 waves (4 per SIMD at two workgroups per CU)
 #define SKP_BG(X, Y)                                                         \
   if (X == 2 || Y == 2 || (bm == 64 && bn == 64)) {                          \
     SKP_BG3(X, Y, 64, 64, 2, 2);                                             \
   } else if (bm == 128 && bn == 128) {                                       \
-    if (four_waves) SKP_BG3((X < 2 ? X : 0), (Y < 2 ? Y : 0), 128, 128, 2, 2); \
-    else SKP_BG3((X < 2 ? X : 0), (Y < 2 ? Y : 0), 128, 128, 4, 2);          \
+    SKP_BG3((X < 2 ? X : 0), (Y < 2 ? Y : 0), 128, 128, 4, 2);               \
   } else if (bm == 128) {                                                    \
     SKP_BG3((X < 2 ? X : 0), (Y < 2 ? Y : 0), 128, 64, 2, 2);                \
   } else {                                                                   \

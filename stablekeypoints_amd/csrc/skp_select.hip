@@ -410,19 +410,9 @@ __device__ __forceinline__ void block_sum_to0(double (&v)[N], double* sd) {
 // window only (≈33² pixels at σ = 2, re-read from L2).  Agrees with the per-pixel kernel above to
 // fp32 rounding (≈3e-7 absolute on KL ≈ 5, tests/test_gpu_parity.py); rows of HW ≤ 4·NV·BT
 // floats, 16-B aligned, HW % 4 == 0 (the launcher checks); blockIdx.x = row of a (rows, HW) stack.
-// r05: with `out` set, the top_k of each image's keys is fused behind the rows (one launch for the
-// A8 call): every block bumps its image's arrival counter (device-scope atomic) once its key is
-// stored at the coherence point; the image's LAST block reads the T keys from there into LDS and ranks
-// them as rank_topk_kernel does (same strict order: NaN last, ties by index, so the same indices),
-// then re-arms the counter for the next launch.  Counters: kTopkFusedMax per library, zero at load;
-// one fused launch at a time per device (the callers' single compute stream).
-constexpr int kTopkFusedMax = 1024;
-__device__ int g_topk_arrivals[kTopkFusedMax];
-
 template <int BT, int NV>
 __global__ __launch_bounds__(BT) void kl_gauss_win_kernel(const float* __restrict__ maps, int h, int w, float two_sig2,
-                                                         float eps, int wr, double* __restrict__ kl, int T = 0,
-                                                         int top_k = 0, long long* __restrict__ out = nullptr) {
+                                                         float eps, int wr, double* __restrict__ kl) {
   __shared__ float sv[BT / 64];
   __shared__ int si[BT / 64];
   __shared__ double sd[6 * (BT / 64)];
@@ -494,49 +484,8 @@ __global__ __launch_bounds__(BT) void kl_gauss_win_kernel(const float* __restric
     const double St = red[2] + nO * e;
     const double Stl = red[3] + (nO > 0.0 ? nO * e * (double)logf(eps) : 0.0);
     const double Stu = red[4] + e * (red[1] - red[5]);
-    const double key = (Stl - Stu) / St - log(St) + log(red[0]);
-    if (out == nullptr) {
-      kl[blockIdx.x] = key;
-    } else {
-      // the key goes to the device's coherence point (agent-scope atomic store) and is acknowledged
-      // before the arrival is counted, so the image's last block — on any XCD — reads it there; no
-      // L2-wide release fence per block (measured: one per block made the launch 4x longer)
-      __hip_atomic_store(kl + blockIdx.x, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_s_waitcnt(0);
-    }
+    kl[blockIdx.x] = (Stl - Stu) / St - log(St) + log(red[0]);
   }
-  if (out == nullptr) return;   // uniform
-  __shared__ int last;
-  const int b = blockIdx.x / T;
-  if (threadIdx.x == 0) last = atomicAdd(&g_topk_arrivals[b], 1) == T - 1;   // device scope
-  __syncthreads();
-  if (!last) return;
-  extern __shared__ __attribute__((aligned(16))) double ks[];   // T keys
-  double* kb = kl + (size_t)b * T;
-  for (int i = threadIdx.x; i < T; i += BT) ks[i] = __hip_atomic_load(kb + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  const int Te = T & ~1;
-  const double2* ks2 = reinterpret_cast<const double2*>(ks);
-  for (int i = threadIdx.x; i < T; i += BT) {
-    const double ki = ks[i];
-    const bool ni = isnan(ki);
-    int r = 0;
-    // every lane reads the same ks[j]: LDS broadcast; 16-B reads, 8 in flight (the loop is
-    // latency-bound otherwise: one block per image does all T² comparisons)
-#pragma unroll 8
-    for (int j2 = 0; j2 < Te / 2; ++j2) {
-      const double2 kk = ks2[j2];
-      const int j = 2 * j2;
-      r += ni ? ((!isnan(kk.x) || j < i) ? 1 : 0) : ((kk.x < ki || (kk.x == ki && j < i)) ? 1 : 0);
-      r += ni ? ((!isnan(kk.y) || j + 1 < i) ? 1 : 0) : ((kk.y < ki || (kk.y == ki && j + 1 < i)) ? 1 : 0);
-    }
-    if (Te < T) {
-      const double kj = ks[T - 1];   // NaN kj compares false: never before a number
-      r += ni ? ((!isnan(kj) || T - 1 < i) ? 1 : 0) : ((kj < ki || (kj == ki && T - 1 < i)) ? 1 : 0);
-    }
-    if (r < top_k) out[(size_t)b * top_k + r] = i;
-  }
-  if (threadIdx.x == 0) g_topk_arrivals[b] = 0;   // re-armed for the next launch
 }
 
 // r05: kl_gauss_win_kernel's arithmetic streamed instead of held: each thread walks its float4s in
@@ -678,50 +627,10 @@ __global__ __launch_bounds__(kRowThreads) void entropy_kernel(const float* __res
   if (threadIdx.x == 0) ent[blockIdx.x] = -acc;
 }
 
-// Ascending sort of T double keys (NaN last, ties by index) -> first top_k indices.
-__device__ __forceinline__ bool key_less(double a, int ia, double b, int ib) {
-  const bool na = isnan(a), nb = isnan(b);
-  if (na || nb) return (!na && nb) || (na && nb && ia < ib);
-  return a < b || (a == b && ia < ib);
-}
-
-// blockIdx.x = segment: keys[b·T …], out[b·top_k …] (one launch sorts every image's keys)
-__global__ __launch_bounds__(1024) void sort_topk_kernel(const double* __restrict__ keys, int T, int n2, int top_k,
-                                                         long long* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  double* k = reinterpret_cast<double*>(smem);
-  int* id = reinterpret_cast<int*>(k + n2);
-  keys += (size_t)blockIdx.x * T;
-  out += (size_t)blockIdx.x * top_k;
-  for (int i = threadIdx.x; i < n2; i += blockDim.x) {
-    k[i] = i < T ? keys[i] : INFINITY;
-    id[i] = i < T ? i : 0x7fffffff;
-  }
-  __syncthreads();
-  for (int size = 2; size <= n2; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = threadIdx.x; i < n2; i += blockDim.x) {
-        const int l = i ^ stride;
-        if (l > i) {
-          const bool up = (i & size) == 0;
-          const bool lt = key_less(k[l], id[l], k[i], id[i]);
-          if (up == lt) {
-            const double tk = k[i]; k[i] = k[l]; k[l] = tk;
-            const int ti = id[i]; id[i] = id[l]; id[l] = ti;
-          }
-        }
-      }
-      __syncthreads();
-    }
-  }
-  for (int i = threadIdx.x; i < top_k; i += blockDim.x) out[i] = id[i];
-}
-
-// r05: the first top_k of that order by ranking instead of sorting: key i's position in the ascending
-// order is rank_i = #{j : key_less(k_j, j, k_i, i)} (a strict total order: NaN last, ties by index),
-// so out[rank_i] = i for rank_i < top_k — the sort's first top_k exactly, with one barrier instead of
-// the bitonic network's log²(n) (at T = 500: 45 barrier-separated stages of one 1024-thread block per
-// image).  A 16-lane row of a wave counts for one key (each lane over every 16th key, then one DPP
+// The first top_k of the ascending order of T double keys (NaN last, ties by index) by ranking: key
+// i's position is rank_i = #{j : k_j before k_i} (a strict total order), so out[rank_i] = i for
+// rank_i < top_k — a sort's first top_k exactly, with one barrier (r05; the r04 bitonic sort ran
+// log²(n) barrier-separated stages of one 1024-thread block per image: 15.9 vs 4.8 µs).  A 16-lane row of a wave counts for one key (each lane over every 16th key, then one DPP
 // row sum), so a 256-thread block ranks 16 keys; grid = (images, ⌈T / 16⌉).  The block stages its
 // image's T keys (≤ 8192) in LDS.
 __global__ __launch_bounds__(256) void rank_topk_kernel(const double* __restrict__ keys, int T, int top_k,
@@ -956,21 +865,9 @@ extern "C" int skp_gaussian_target(const float* pos, int num, int T, int size, f
 }
 
 static int launch_sort(const double* keys, int T, int top_k, long long* out, hipStream_t st, int nb = 1) {
-  SKP_CHECK_ARG(T <= 8192, "T > 8192 tokens is not supported by the selection sort");
-  // SKP_TOPK_SORT=1: the r04 bitonic sort (A/B); default: the ranking kernel (same indices)
-  static const bool bitonic = [] {
-    const char* e = getenv("SKP_TOPK_SORT");
-    return e && atoi(e) == 1;
-  }();
-  if (bitonic) {
-    int n2 = 1;
-    while (n2 < T) n2 <<= 1;
-    const size_t lds = (size_t)n2 * (sizeof(double) + sizeof(int));
-    hipLaunchKernelGGL(sort_topk_kernel, dim3(nb), dim3(1024), lds, st, keys, T, n2, top_k, out);
-  } else {
-    hipLaunchKernelGGL(rank_topk_kernel, dim3((T + 15) / 16, nb), dim3(256), (size_t)T * sizeof(double), st, keys, T,
-                       top_k, out);
-  }
+  SKP_CHECK_ARG(T <= 8192, "T > 8192 tokens is not supported by the selection ranking");
+  hipLaunchKernelGGL(rank_topk_kernel, dim3((T + 15) / 16, nb), dim3(256), (size_t)T * sizeof(double), st, keys, T,
+                     top_k, out);
   SKP_LAUNCH_CHECK();
   return SKP_OK;
 }
@@ -1005,54 +902,18 @@ extern "C" int skp_topk_gaussian_batch(const float* maps, int nb, int T, int h, 
       const double r = ceil(sqrt((double)two_sig2 * kk));
       if (r < (double)wr) wr = (int)r;
     }
-    // SKP_TOPK_FUSED=1 (A/B, measured slower): the top-k fused behind the KL rows — 111 vs 45 µs
-    // per call at the bench shape (profiles/r05w_a8_fused_ab.txt): the T same-address arrival
-    // atomics per image serialise at the device's coherence point; default: the separate
-    // ranking launch
-    const bool fused = top_k > 0 && nb <= kTopkFusedMax && T <= 4096 && [] {
-      const char* e = getenv("SKP_TOPK_FUSED");
-      const char* f = getenv("SKP_TOPK_SORT");
-      return (e && atoi(e) == 1) && !(f && atoi(f) == 1);
-    }();
-    const size_t lds = fused ? (size_t)T * sizeof(double) : 0;
-    long long* fo = fused ? out : nullptr;
-    // r05 default for rows up to 128²: the streamed form (SKP_KL_STREAM=0: the held form, A/B)
-    const bool stream = !fused && HW <= 4 * 16 * 256 && [] {
-      const char* e = getenv("SKP_KL_STREAM");
-      return !(e && atoi(e) == 0);
-    }();
-    // float4 per thread per chunk and threads per row (A/B: SKP_KL_UNR = 1 / 2 / 4, SKP_KL_BT = 128 /
-    // 256, read per call); default 1 × 256: kbench kl4 39.4 µs vs 40.0–40.9 (2 × 256), 42.0 (4 × 256),
-    // 44.5–44.9 for the held form (profiles/r05zb_kl_stream_ab.txt)
-    const int unr = [] {
-      const char* e = getenv("SKP_KL_UNR");
-      const int v = e ? atoi(e) : 1;
-      return (v == 2 || v == 4) ? v : 1;
-    }();
-    const int bt = [] {
-      const char* e = getenv("SKP_KL_BT");
-      return (e && atoi(e) == 128) ? 128 : 256;
-    }();
-#define SKP_KL_STREAM_CASE(BT_, U_)                                                                          \
-    else if (stream && bt == BT_ && unr == U_) hipLaunchKernelGGL((kl_gauss_stream_kernel<BT_, U_>), dim3(rows), \
-                                                                  dim3(BT_), 0, st, maps, h, w, two_sig2, epsilon, wr, keys);
-    if (false) {
-    }
-    SKP_KL_STREAM_CASE(256, 2)
-    SKP_KL_STREAM_CASE(256, 1)
-    SKP_KL_STREAM_CASE(256, 4)
-    SKP_KL_STREAM_CASE(128, 2)
-    SKP_KL_STREAM_CASE(128, 1)
-    SKP_KL_STREAM_CASE(128, 4)
-#undef SKP_KL_STREAM_CASE
-    else if (HW <= 4 * 16 * 256)
-      hipLaunchKernelGGL((kl_gauss_win_kernel<256, 16>), dim3(rows), dim3(256), lds, st, maps, h, w, two_sig2, epsilon,
-                         wr, keys, T, top_k, fo);
+    // rows up to 128²: the streamed form, 256 threads, one float4 per thread per chunk (kbench kl4
+    // 39.4 µs vs 40.0–40.9 at two, 42.0 at four, 44.5–44.9 for the held form,
+    // profiles/r05zb_kl_stream_ab.txt); larger rows (find_best_indices at 256²): the held form.
+    // (Fusing the ranking behind the KL rows — each image's last block ranks — measured 2.5× slower,
+    // profiles/r05w_a8_fused_ab.txt, and was removed in r06.)
+    if (HW <= 4 * 16 * 256)
+      hipLaunchKernelGGL((kl_gauss_stream_kernel<256, 1>), dim3(rows), dim3(256), 0, st, maps, h, w, two_sig2, epsilon, wr,
+                         keys);
     else
-      hipLaunchKernelGGL((kl_gauss_win_kernel<1024, 16>), dim3(rows), dim3(1024), lds, st, maps, h, w, two_sig2,
-                         epsilon, wr, keys, T, top_k, fo);
+      hipLaunchKernelGGL((kl_gauss_win_kernel<1024, 16>), dim3(rows), dim3(1024), 0, st, maps, h, w, two_sig2, epsilon,
+                         wr, keys);
     SKP_LAUNCH_CHECK();
-    if (fused) return SKP_OK;
     if (top_k == 0) return SKP_OK;
     return launch_sort(keys, T, top_k, out, st, nb);
   } else if (reg && HW <= 4 * 1 * kRowThreads)

@@ -298,7 +298,7 @@ def aggregate(layers, indices=None, upsample_res=-1):
     return _Aggregate.apply(indices, int(upsample_res), *layers)
 
 
-FUSED_MAPS = os.environ.get("SKP_FUSED_MAPS", "1") != "0"   # A/B: 0 = skp_capture_fwd + skp_aggregate
+FUSED_MAPS = True   # tests switch it: False = skp_capture_fwd + skp_aggregate (the AttentionStore path)
 
 
 def capture_maps_bytes(B, H, N, R, sizes):
@@ -437,7 +437,7 @@ def capture_maps(zs, sizes, B, R):
 
 # A/B: 0 = the selected rows' gradient goes through the dense (B, N, R²) map gradient and
 # skp_capture_maps_bwd, as in r02
-SEL_BWD = os.environ.get("SKP_SEL_BWD", "1") != "0"
+SEL_BWD = True   # tests switch it: False = the dense map gradient + skp_capture_maps_bwd
 # skp_capture_maps_bwd_sel's per-image row limit (32-bit lane masks in csrc/skp_capture_sel.hip);
 # more selected rows per image (a user --top_k > 32) take the dense backward
 SEL_MAXK = 32
@@ -690,11 +690,8 @@ def find_top_k_gaussian(maps, top_k, sigma=3, epsilon=1e-5, num_subjects=1, retu
     return (out, kl) if return_kl else out
 
 
-# the A8 top-k as its own ranking launch (default) or fused behind the KL kernel (SKP_TOPK_FUSED=1,
-# A/B, measured slower: profiles/r05w_a8_fused_ab.txt; libskp reads the variable per call)
-A8_FUSED = os.environ.get("SKP_TOPK_FUSED", "0") == "1"
-
-
+# the A8 top-k as its own ranking launch behind the KL kernel (the fused one-launch form measured
+# 2.5× slower, profiles/r05w_a8_fused_ab.txt, and was removed in r06)
 def find_top_k_gaussian_batch(maps, top_k, sigma=3, epsilon=1e-5, num_subjects=1):
     """find_top_k_gaussian of every image of a (nb, T, h, w) stack in one launch each for the KL
     ranking and the sort: (nb, top_k) int64, row b = find_top_k_gaussian(maps[b], ...)."""
@@ -705,16 +702,11 @@ def find_top_k_gaussian_batch(maps, top_k, sigma=3, epsilon=1e-5, num_subjects=1
     out = torch.empty(nb, top_k, device=maps.device, dtype=torch.int64)
     kl = torch.empty(nb, T, device=maps.device, dtype=torch.float64)
     # the whole A8 call (algorithmic bytes: every map read once, the keys written) in one timed
-    # scope: the KL ranking launch and the ranking of the keys (or, SKP_TOPK_FUSED=1, one launch)
+    # scope: the KL ranking launch and the ranking of the keys
     with _timed("skp_topk_gaussian_batch", maps.numel() * 4 + nb * T * 8):
-        if A8_FUSED and top_k > 0:
-            call("skp_topk_gaussian_batch", ptr(maps), nb, T, h, w, int(top_k), float(sigma), float(epsilon),
-                 int(num_subjects), ptr(out), ptr(kl), ptr(kl), stream(maps.device))
-        else:
-            call("skp_topk_gaussian_batch", ptr(maps), nb, T, h, w, 0, float(sigma), float(epsilon),
-                 int(num_subjects), ptr(out), ptr(kl), ptr(kl), stream(maps.device))
-            if top_k > 0:
-                call("skp_topk_keys", ptr(kl), nb, T, int(top_k), ptr(out), stream(maps.device))
+        # the KL ranking launch, then (top_k > 0) the ranking of its keys, both on this stream
+        call("skp_topk_gaussian_batch", ptr(maps), nb, T, h, w, int(top_k), float(sigma), float(epsilon),
+             int(num_subjects), ptr(out), ptr(kl), ptr(kl), stream(maps.device))
     return out
 
 
@@ -937,10 +929,10 @@ def equivariance_loss_batch(A, At, theta_inv, nb):
 
 
 # --------------------------------------------------------------------------- UNet-side GroupNorm(+SiLU)
-# A/B switch (SKP_GN_EPI=0 off): the Winograd convolution's epilogue writes per-segment (mean, M2) of
+# GN_EPI (tests set False to compare): the Winograd convolution's epilogue writes per-segment (mean, M2) of
 # its output (skp_conv3x3_wino2_gn) and a GroupNorm reading that output takes its statistics from
 # them (skp_groupnorm_fwd_part) instead of a pass over the activation.
-GN_EPI = os.environ.get("SKP_GN_EPI", "1") != "0"
+GN_EPI = True   # tests switch it: False = GroupNorm computes its own statistics
 
 
 def _gn_parts_of(x):
@@ -1108,8 +1100,8 @@ def attention_nograd(q, k, v, scale):
 
 # head dims routed to skp_attn_bwd_kv: d = 40 measured faster end to end (2 waves per SIMD fit);
 # d = 64 / 80 run at one wave per SIMD and measured slower than the unfused path.
-# SKP_ATTN_FUSED_KV=0 disables it, =all routes every supported head dim.
-ATTN_FUSED_KV = {"0": (), "all": (40, 64, 80)}.get(os.environ.get("SKP_ATTN_FUSED_KV", ""), (40,))
+# (tests route every supported head dim through it, or none)
+ATTN_FUSED_KV = (40,)
 
 
 class MathAttention(torch.autograd.Function):
@@ -1277,8 +1269,8 @@ def geglu(h):
 
 
 # head dims whose grad-needing attention keeps no probability tensor (FlashAttention below);
-# SKP_ATTN_FLASH=0 disables it, =all routes every supported head dim
-ATTN_FLASH = {"0": (), "all": (40, 64, 80)}.get(os.environ.get("SKP_ATTN_FLASH", ""), (40, 64))
+# (tests route every supported head dim through it, or none)
+ATTN_FLASH = (40, 64)
 
 
 class FlashAttention(torch.autograd.Function):
@@ -1329,7 +1321,7 @@ def math_attention(q, k, v, scale):
 
 # --------------------------------------------------------------------------- attention on (B, S, H·d) projections
 # A/B: 0 = permute q / k / v / out between (B, S, H·d) and (B·H, S, d) around the attention kernels (r02)
-ATTN_BSHD = os.environ.get("SKP_ATTN_BSHD", "1") != "0"
+ATTN_BSHD = True
 
 
 def _lay(t):
@@ -1469,8 +1461,8 @@ class QKVProjection(torch.autograd.Function):
         return dx.view(ctx.x_shape), None, None
 
 
-# A/B (SKP_QKV=0: three nn.Linear calls and autograd's gradient sum)
-QKV_FUSED = os.environ.get("SKP_QKV", "1") != "0"
+# (QKV_FUSED = False: three nn.Linear calls and autograd's gradient sum)
+QKV_FUSED = True
 
 
 def qkv_projection(x, *ws):
@@ -1544,15 +1536,11 @@ WINO_MIN_WORKGROUPS = 128
 # Which kernel takes an eligible shape: "auto" = skp_conv3x3_wino2 where H and W are multiples
 # of 32 (every VAE-encoder layer, the UNet's 64² and 32² layers) or 16×16 with the batch a
 # multiple of 4 (the UNet's 16² layers), skp_conv3x3_wino elsewhere (8²);
-# "v1" forces the first kernel (A/B runs: SKP_WINO=v1).  SKP_WINO_SPLIT=0 disables split-K.
-WINO_KERNEL = os.environ.get("SKP_WINO", "auto")
-WINO_SPLIT = os.environ.get("SKP_WINO_SPLIT", "1") != "0"
-WINO_WIDE = os.environ.get("SKP_WINO_WIDE", "1") != "0"   # must match skp_conv3x3_wino's rule
-# half-height Winograd blocks (libskp's default for H, W multiples of 32; SKP_WINO2_HALF=0 off):
-# the split-K planner models two co-resident workgroups per CU for them
-WINO2_HALF = os.environ.get("SKP_WINO2_HALF", "1") != "0"
-WINO2_HALF16 = os.environ.get("SKP_WINO2_HALF16", "1") != "0"   # the 16×16 geometry's 4-wave form
-WINO_PLAN_HALF = os.environ.get("SKP_WINO_PLAN_HALF", "1") != "0"   # 0: the one-workgroup-per-CU cost model (A/B)
+# "v1" forces the first kernel (tests).  WINO_SPLIT = False disables split-K; WINO_NSPLIT_FORCE
+# (tests, tools/wino_time.py) measures one given split.
+WINO_KERNEL = "auto"
+WINO_SPLIT = True
+WINO_NSPLIT_FORCE = 0
 
 
 def _wino_v2(H, W, B=None):
@@ -1591,12 +1579,12 @@ def _wino_plan_uncached(B, C, K, H, W, force):
     v2 = _wino_v2(H, W, B)
     if v2:
         wgs = (B // 4 if H == 16 else B * (H // 32) * (W // 32)) * (K // 32)
-    elif WINO_WIDE and B * (H // 4) * (W // 4) <= 32 and K % 64 == 0:
+    elif B * (H // 4) * (W // 4) <= 32 and K % 64 == 0:
         wgs = K // 64   # one 32-tile × 64-channel block per channel block (libskp's rule, skp_conv.hip)
     else:
         wgs = -(-(B * (H // 4) * (W // 4)) // 64) * (K // 32)
     out_bytes = B * K * H * W * 4
-    half = v2 and (WINO2_HALF16 if H == 16 else WINO2_HALF) and WINO_PLAN_HALF
+    half = v2   # libskp's half-height blocks: two co-resident workgroups per CU
 
     def cost(s):
         if half:
@@ -1613,7 +1601,7 @@ def _wino_plan_uncached(B, C, K, H, W, force):
     if WINO_SPLIT:
         cands = [s for s in range(1, 33) if C % (4 * s) == 0 and (s == 1 or C // s >= 32)]
         nsplit = min(cands, key=cost)
-        if force and C % (4 * force) == 0:   # dev: SKP_WINO_NSPLIT measures a given split
+        if force and C % (4 * force) == 0:   # dev: WINO_NSPLIT_FORCE measures a given split
             nsplit = force
     return v2, nsplit, wgs * nsplit
 
@@ -1624,8 +1612,8 @@ _WINO_PLANS = {}
 def _wino_plan(B, C, K, H, W):
     """_wino_plan_uncached, memoised per shape (and the module switches it reads): the planner's
     32-candidate cost loop ran in Python on every convolution call, ~1500 launches per step."""
-    force = int(os.environ.get("SKP_WINO_NSPLIT", "0"))
-    key = (B, C, K, H, W, force, WINO_KERNEL, WINO_SPLIT, WINO_WIDE, WINO2_HALF, WINO2_HALF16, WINO_PLAN_HALF)
+    force = int(WINO_NSPLIT_FORCE)
+    key = (B, C, K, H, W, force, WINO_KERNEL, WINO_SPLIT)
     plan = _WINO_PLANS.get(key)
     if plan is None:
         plan = _WINO_PLANS[key] = _wino_plan_uncached(B, C, K, H, W, force)
@@ -1643,8 +1631,8 @@ def wino_eligible(B, C, K, H, W, min_workgroups=None):
 # Small-image, many-channel convolutions (the UNet's 8²-32² layers) as Winograd transforms + 36
 # batched library GEMMs (skp_wino_in_transform → torch.bmm → skp_wino_out_transform) instead of the
 # fused kernels: at these sizes the fused grids are a few hundred latency-bound workgroups.
-# SKP_WINO_GEMM_MAX_HW = the largest H·W that takes it (0 = off; A/B).
-WINO_GEMM_MAX_HW = int(os.environ.get("SKP_WINO_GEMM_MAX_HW", "1024"))
+# WINO_GEMM_MAX_HW = the largest H·W that takes it (tests set 0 to cover the fused kernels).
+WINO_GEMM_MAX_HW = 1024
 WINO_GEMM_MIN_CH = 256
 # G of F(4×4, 3×3) at the points (0, 1, −1, 1/2, −2, ∞) (skp_conv.hip wino_weights_kernel's Gm)
 _WINO_G = ((1.0, 0.0, 0.0), (1 / 3, 1 / 3, 1 / 3), (-1 / 3, 1 / 3, -1 / 3), (-16 / 15, -8 / 15, -4 / 15),
@@ -1676,10 +1664,10 @@ def _wino_u_gemm(weight, flip):
     return U
 
 
-# A/B (SKP_WINO_KT=0: the (36, T, K) product and its per-lane scattered tile stores): the product
-# as (36, K, T), so the output transform reads it and writes the tiles coalesced (and leaves the
-# next GroupNorm's statistics partials, as the fused kernel does)
-WINO_KT = os.environ.get("SKP_WINO_KT", "1") != "0"
+# The product as (36, K, T), so the output transform reads it and writes the tiles coalesced (and
+# leaves the next GroupNorm's statistics partials, as the fused kernel does); r04 measured it ahead
+# of the (36, T, K) product with per-lane scattered tile stores (skp_wino_out_transform, kept in
+# the ABI).
 
 
 def _wino_gemm_conv(x, weight, flip, bias, residual, K, gn=False):
@@ -1690,10 +1678,6 @@ def _wino_gemm_conv(x, weight, flip, bias, residual, K, gn=False):
     call("skp_wino_in_transform", ptr(x), B, C, H, W, ptr(V), stream(x.device))
     y = torch.empty(B, K, H, W, device=x.device, dtype=F32)
     bp, rp = ptr(bias) if bias is not None else None, ptr(residual) if residual is not None else None
-    if not WINO_KT:
-        M = torch.bmm(V.transpose(1, 2), U)                          # (36, T, K)
-        call("skp_wino_out_transform", ptr(M), B, K, H, W, bp, rp, ptr(y), stream(x.device))
-        return y
     M = torch.bmm(U.transpose(1, 2), V)                              # (36, K, T)
     P = (H // 4) * (W // 4)
     gnp = None
@@ -1804,7 +1788,7 @@ class Conv1x1(torch.autograd.Function):
 # bench's shortcut shapes (tools/conv1x1_time.py, batch 8, fwd + input grad): within ±3% of MIOpen's
 # 1×1 kernels at 8², 16² and 32² (2560→1280 @16²: 274 vs 272 us; 960→640 @32²: 186 vs 201 us;
 # 1280→640 @32²: 290 vs 249 us), the VAE's 128→256 @256² 318 vs 343 us — no net gain, so MIOpen stays
-CONV1X1_GEMM = os.environ.get("SKP_CONV1X1_GEMM", "0") == "1"
+CONV1X1_GEMM = False   # tests switch it: True = 1×1 shortcuts as one GEMM (measured neutral)
 
 
 def conv1x1(x, weight):
@@ -1819,8 +1803,8 @@ def conv1x1(x, weight):
 
 
 # A/B: 0 = the VAE's stride-2 downsampling convolutions run as F.pad + MIOpen (r02)
-WINO_S2 = os.environ.get("SKP_WINO_S2", "1") != "0"
-WINO_S2_MIN_PIXELS = int(os.environ.get("SKP_WINO_S2_MIN", str(384 * 384)))   # A/B: SKP_WINO_S2_MIN=65536 adds 256²
+WINO_S2 = True
+WINO_S2_MIN_PIXELS = 384 * 384   # 256² / 128² measured neutral on the copy-free kernel (profiles/r05y_s2_wino_ab.txt)
 
 
 def conv3x3_s2_eligible(x, weight):

@@ -19,7 +19,7 @@ from . import eval as skp_eval
 from .invertable_transform import RandomAffineWithInverse
 
 # A/B: 0 = select per image (one top-k / FPS launch chain per image, r03ao and before)
-SEL_BATCH = os.environ.get("SKP_SEL_BATCH", "1") != "0"
+SEL_BATCH = True
 
 
 def _upload(t, device):

@@ -126,7 +126,7 @@ class LogitStore(AttentionStore):
 
 # A/B: 0 = run_and_find_attn fills an AttentionStore with the materialised (B·H, R², N)
 # attention of every captured layer, as in r02
-EVAL_LOGITS = os.environ.get("SKP_EVAL_LOGITS", "1") != "0"
+EVAL_LOGITS = True   # tests switch it: False = the AttentionStore capture path
 
 
 @contextlib.contextmanager

@@ -38,7 +38,7 @@ class CaptureComplete(Exception):
 # fused softmax backward run on libskp when True (HIP tensors, frozen parameters); False is the
 # plain-torch model (the tests compare the two).
 USE_FUSED_GROUPNORM = True
-USE_SKP_LAYERNORM = os.environ.get("SKP_LN", "1") != "0"   # A/B switch for the LayerNorm kernel
+USE_SKP_LAYERNORM = True   # tests switch it: False = ATen LayerNorm
 
 
 def _fused(x, *modules):
@@ -65,7 +65,7 @@ def _ln(norm, x):
 
 
 # A/B switch: 0 = the residual consumers of a norm's input get their gradient summed by autograd
-NORM_RES = os.environ.get("SKP_NORM_RES", "1") != "0"
+NORM_RES = True
 
 
 def _ln_res(norm, x):
@@ -162,9 +162,9 @@ class CrossAttention(nn.Module):
         return self.to_out[1](self.to_out[0](out))
 
 
-SHARED_KV = os.environ.get("SKP_SHARED_KV", "1") != "0"   # A/B switch for kv_projection
+SHARED_KV = True
 # A/B switch: 0 = a batch-shared context's k / v are expanded to the batch and head-permuted with it
-SHARED_HEAD_MAJOR = os.environ.get("SKP_SHARED_HEAD_MAJOR", "1") != "0"
+SHARED_HEAD_MAJOR = True
 
 
 def _shared_context(context):

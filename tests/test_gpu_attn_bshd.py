@@ -92,7 +92,7 @@ def test_attention_heads_nograd_and_fallbacks():
 
 
 def test_unet_cross_attention_module_uses_bshd_and_matches_permuting_path(monkeypatch):
-    """CrossAttention.forward through the BSHD path equals the r02 permuting path (SKP_ATTN_BSHD=0)."""
+    """CrossAttention.forward through the BSHD path equals the r02 permuting path (ops.ATTN_BSHD = False)."""
     from stablekeypoints_amd import ops
     from stablekeypoints_amd.sd.unet import CrossAttention
     torch.manual_seed(0)

@@ -251,7 +251,7 @@ def test_conv3x3_stride2_downsample_vs_fp64(all_shapes, monkeypatch, B, C, K, H,
     ops = all_shapes
     monkeypatch.setattr(ops, "WINO_S2_MIN_PIXELS", 1)
     if nsplit:
-        monkeypatch.setenv("SKP_WINO_NSPLIT", str(nsplit))
+        monkeypatch.setattr(ops, "WINO_NSPLIT_FORCE", nsplit)
     g = torch.Generator().manual_seed(B * 1000 + C + K + H)
     x = torch.randn(B, C, H, W, generator=g)
     w = torch.randn(K, C, 3, 3, generator=g) / (3 * C ** 0.5)
@@ -310,7 +310,7 @@ def test_conv1x1_gemm_vs_fp64(B, C, K, H, W):
 
 def test_resnet_block_shortcut_gemm_matches_miopen_form(monkeypatch):
     """ResnetBlock2D with a 1×1 shortcut: the fused form (shortcut GEMM, its bias folded into conv2's
-    epilogue) equals the MIOpen shortcut form (SKP_CONV1X1_GEMM=0), forward and input gradient."""
+    epilogue) equals the MIOpen shortcut form (ops.CONV1X1_GEMM = False), forward and input gradient."""
     from stablekeypoints_amd import ops
     from stablekeypoints_amd.sd.unet import ResnetBlock2D
     torch.manual_seed(1)

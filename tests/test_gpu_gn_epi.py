@@ -6,7 +6,7 @@ Checks: the per-segment (mean, M2) partials (r05: accumulated around a pivot ins
 then Chan's combination) against fp64 segment means (1e-5 of the segment's mean |y|) and centred
 second moments (1e-5 relative, plus a floor); the GroupNorm output against fp64 torch GroupNorm of the same conv output
 (2e-5 of max |y|, the same bound the plain statistics pass meets) and against the statistics-pass
-path (SKP_GN_EPI=0); an in-place write to the conv output drops the partials."""
+path (ops.GN_EPI = False); an in-place write to the conv output drops the partials."""
 import pytest
 import torch
 

@@ -166,49 +166,6 @@ def test_select_more_rows_than_the_sparse_kernel_takes():
         assert err < 2e-5, err
 
 
-@pytest.mark.parametrize("B,H,sizes,R,Nn,K,dup,ragged", [
-    (8, 8, (16, 16, 16, 32), 128, 500, 10, False, False),  # the bench shape (the paired sel_dense launch)
-    (2, 4, (4, 8), 32, 64, 5, True, True),                # duplicated token, ragged rows
-    (2, 2, (4, 8, 16), 64, 64, 32, True, False),          # K = 32, three sizes
-])
-def test_forked_sparse_part_equals_single_stream(monkeypatch, B, H, sizes, R, Nn, K, dup, ragged):
-    """SKP_SEL_FORK=1 (A/B option, measured slower: sel_adjw on a second stream beside sel_dense, the selected tokens'
-    es added by a final pass in k order) is bit-identical to SKP_SEL_FORK=0 (default: es added inside
-    sel_dense's emit, one stream): the same additions in the same order."""
-    from stablekeypoints_amd import ops
-    zs, tok, gsel = _case(77 + K, B, H, sizes, R, Nn, K, dup, ragged)
-    zt = [T(z) for z in zs]
-    _, stats = _fwd(zt, list(sizes), B, H, R)
-    out = {}
-    for fork in ("0", "1"):
-        monkeypatch.setenv("SKP_SEL_FORK", fork)
-        out[fork] = _sel_abi(zt, list(sizes), B, H, R, T(tok), T(gsel), 0.03125, stats)
-    for a, b in zip(out["0"], out["1"]):
-        assert torch.equal(a, b), (a - b).abs().max().item()
-
-
-@pytest.mark.parametrize("B,H,sizes,R,Nn,K,dup,ragged", [
-    (8, 8, (16, 16, 16, 32), 128, 500, 10, False, False),  # the bench shape
-    (2, 4, (4, 8), 32, 64, 5, True, True),                # R/s = 8 and 4, duplicated token, ragged rows
-    (2, 2, (4, 8, 16), 64, 64, 32, True, False),          # R/s = 16, 8, 4, K = 32
-    (1, 3, (16, 8, 16, 32), 128, 8, 1, False, False),     # K = 1, mixed sizes
-])
-def test_fused_horizontal_adjoint_equals_e_rows(monkeypatch, B, H, sizes, R, Nn, K, dup, ragged):
-    """SKP_SEL_DOTH=1 (default: sel_doth keeps a row's e in LDS and applies the horizontal half of
-    bicubicᵀ as one 4·RATIO-tap filter per column, sel_adjv the vertical half) is bit-identical to
-    SKP_SEL_DOTH=0 (sel_dot writes the R² E rows, sel_adjw's rolling window reduces them): the same
-    products summed in the same order, edge columns included."""
-    zs, tok, gsel = _case(91 + K, B, H, sizes, R, Nn, K, dup, ragged)
-    zt = [T(z) for z in zs]
-    _, stats = _fwd(zt, list(sizes), B, H, R)
-    out = {}
-    for v in ("0", "1"):
-        monkeypatch.setenv("SKP_SEL_DOTH", v)
-        out[v] = _sel_abi(zt, list(sizes), B, H, R, T(tok), T(gsel), 0.03125, stats)
-    for a, b in zip(out["0"], out["1"]):
-        assert torch.equal(a, b), (a - b).abs().max().item()
-
-
 def test_phase_timing_records_each_fast_path_call():
     """skp_sel_bwd_timing / _read (the bench's `split_ms`): one record per fast-path call while on,
     four non-negative phase times whose sum is within the call's own event time, none when off."""

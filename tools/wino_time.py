@@ -1,6 +1,6 @@
 """Dev tool: time skp_conv3x3_wino forward on a few shapes (TF/s-equivalent of the direct conv).
 
-usage: python tools/wino_time.py [--shapes B,C,K,HW;...]  (SKP_WINO=v1: first kernel; SKP_WINO_DEBUG: its load/compute switches)
+usage: python tools/wino_time.py [--shapes B,C,K,HW;...]  (timing-probe builds: tools/build_variant.sh with -DSKP_WINO_DEBUG=… / -DSKP_WINO2_DEBUG=…)
 """
 import argparse
 import os
