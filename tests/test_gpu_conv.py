@@ -265,7 +265,7 @@ def test_conv3x3_stride2_downsample_vs_fp64(all_shapes, monkeypatch, B, C, K, H,
 
 def test_vae_downsample_uses_stride2_winograd_and_matches_miopen(monkeypatch):
     """The VAE's Downsample2D takes the stride-2 Winograd path under no_grad and equals the
-    F.pad + MIOpen path (the SKP_WINO_S2=0 form) at 128 channels, batch 2."""
+    F.pad + MIOpen path (the ops.WINO_S2 = False form) at 128 channels, batch 2."""
     from stablekeypoints_amd import ops
     from stablekeypoints_amd.sd.unet import Downsample2D
     torch.manual_seed(0)

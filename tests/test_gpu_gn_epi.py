@@ -130,7 +130,7 @@ def test_resnet_block_with_epilogue_statistics_matches_plain(monkeypatch):
                                            (4, 256, 256, 16, 32, False), (2, 256, 320, 32, 64, True)])
 def test_wino_gemm_groupnorm_statistics(monkeypatch, B, C, K, H, W, res):
     """The Winograd-GEMM form (skp_wino_out_transform_kt): the same partials per segment of
-    min(P, 64) tiles, output equal to the (36, T, K) form's within fp32 GEMM rounding."""
+    min(P, 64) tiles, output within 3e-5 of the fp64 convolution."""
     from stablekeypoints_amd import ops
     g = torch.Generator(device=DEV).manual_seed(B + C + K + H + W)
     x = torch.randn(B, C, H, W, device=DEV, generator=g)
@@ -147,10 +147,6 @@ def test_wino_gemm_groupnorm_statistics(monkeypatch, B, C, K, H, W, res):
     assert nseg == P // seg
     tiles = y.double().reshape(B, K, th, 4, tw, 4).permute(0, 1, 2, 4, 3, 5).reshape(B, K, P, 16)
     _check_parts(gp, tiles.reshape(B, K, nseg, seg * 16))
-    monkeypatch.setattr(ops, "WINO_KT", False)
-    y0 = ops.conv3x3(x, w, bias, r)
-    assert ops._gn_parts_of(y0) is None
-    assert float((y - y0).abs().max()) <= 2e-5 * float(y0.abs().max())
     ref = torch.nn.functional.conv2d(x.double(), w.double(), bias.double(), padding=1)
     if r is not None:
         ref = ref + r.double()
