@@ -9,9 +9,11 @@ bicubic and to_q are linear and commute with ·kᵀ, so this equals
 ``softmax(bicubic(q kᵀ·scale))`` where ``q kᵀ·scale`` is the layer's own
 normal-path logit matrix at s×s.  The patched forward therefore computes the
 logits once on the matrix cores (``skp_bgemm_f32``), feeds them to the normal
-softmax·V path, and hands them to ``skp_capture_fwd`` for the R×R capture:
-≈248 GFLOP of dense work per capture in the reference becomes ≈1.6 GFLOP plus
-an HBM-bound upsample/softmax kernel.
+softmax·V path, and hands them to the capture kernels: ≈248 GFLOP of dense work per
+capture in the reference becomes ≈1.6 GFLOP of MFMA plus the upsample/softmax/aggregate
+kernel ``skp_capture_maps_fwd`` (VALU-bound: 4 taps, an exp and the normalised
+accumulate per (pixel, token, layer, head)), or ``skp_capture_fwd`` for
+a plain ``AttentionStore``.
 """
 import abc
 import contextlib

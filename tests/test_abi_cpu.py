@@ -29,6 +29,18 @@ def test_library_exports_every_symbol():
     assert _lib.lib().skp_version() == 1
 
 
+def test_library_reads_no_environment():
+    """r06: every A/B switch left the shipped library: no libc
+    getenv import and no SKP_* variable name in its strings; variants are build options
+    (tools/build_variant.sh), not runtime paths."""
+    from stablekeypoints_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libskp.so not built")
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"getenv" not in blob
+    assert re.search(rb"SKP_[A-Z0-9_]{3,}", blob) is None
+
+
 def test_bad_arguments_rejected_without_gpu():
     from stablekeypoints_amd import _lib
     if not os.path.exists(_lib.LIB_PATH):

@@ -6,8 +6,10 @@ to this package's modules so reference callers run unchanged:
     python -m unsupervised_keypoints.main --dataset_loc ... --model_type <weights dir>
 
 Each submodule IS the ``stablekeypoints_amd`` module of the same name (``sys.modules`` alias: the
-same objects, so monkey-patching one patches the other).  ``sdxl_monkey_patch`` maps to the SDXL
-capture path (the reference's patch is inert).  Not built: ``visualize``
+same objects, so monkey-patching one patches the other).  ``sdxl_monkey_patch`` is the restated
+SDXL store API (``AttentionControl`` / ``AttentionStore``, pinned by a fixture recorded from the
+reference's classes) with ``register_attention_control`` on this package's SDXL UNet (the
+reference's own patch patches nothing).  Not built: ``visualize``
 (matplotlib figures), ``generate_image`` (text-to-image), ``cub`` (h5py): importing them raises
 ImportError.
 """
