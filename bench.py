@@ -128,8 +128,20 @@ def _a8_split(dev, T, R, nb=4, reps=20):
     def whole():
         ops.find_top_k_gaussian_batch(maps, 25, sigma=2.0)
 
+    maps_t = torch.rand(nb, T, R, R, device=dev, generator=g) ** 8   # the warps' maps the FPS reads
+
+    def chain_r05():   # KL → rank (skp_topk_gaussian_batch) → argmax + FPS (skp_fps_batch): 4 launches
+        c = ops.find_top_k_gaussian_batch(maps, 25, sigma=2.0)
+        return ops.furthest_point_sampling_batch(maps_t, 10, c)[0]
+
+    def chain_r06():   # KL → rank + argmax → FPS (ops.gaussian_fps_batch): 3 launches
+        return ops.gaussian_fps_batch(maps, maps_t, 25, 10, sigma=2.0)[0]
+
+    if not torch.equal(chain_r05(), chain_r06()):
+        raise SystemExit("bench: gaussian_fps_batch differs from the two-call selection")
     res = {}
-    for name, fn in (("kl_ms", kl_only), ("topk_ms", topk_only), ("call_ms", whole)):
+    for name, fn in (("kl_ms", kl_only), ("topk_ms", topk_only), ("call_ms", whole),
+                     ("select_chain_r05_ms", chain_r05), ("select_chain_ms", chain_r06)):
         fn()
         ts = []
         for _ in range(reps):
@@ -140,8 +152,11 @@ def _a8_split(dev, T, R, nb=4, reps=20):
             b.synchronize()
             ts.append(a.elapsed_time(b))
         res[name] = float(np.median(ts))
-    res["workload"] = f"{nb} x ({T}, {R}, {R}) synthetic maps, top_k 25, sigma 2; median of {reps}, before the warm-up"
-    del maps
+    res["workload"] = (f"{nb} x ({T}, {R}, {R}) synthetic maps (+ as many warp maps for the FPS), top_k 25, sigma 2, "
+                       f"FPS 10; median of {reps}, before the warm-up; select_chain_r05_ms = KL + rank launch + "
+                       "argmax + FPS launches (the r05 chain), select_chain_ms = KL + rank/argmax + FPS (r06), "
+                       "outputs checked equal")
+    del maps, maps_t
     return res
 
 
@@ -626,7 +641,7 @@ def main():
     imgs = [data[i]["img"][None].to(dev) for i in range(len(data))]
     timer = KernelTimer(["skp_aggregate", "skp_capture_fwd", "skp_capture_bwd", "skp_capture_maps_fwd",
                          "skp_capture_maps_bwd", "skp_capture_maps_bwd_sel", "skp_topk_gaussian_batch",
-                         "skp_topk_keys"])
+                         "skp_topk_keys", "skp_selection"])
     ops.set_kernel_timer(timer)
 
     counter = [0]
@@ -769,10 +784,15 @@ def main():
             "bound": "hbm", "avg_ms": sel["avg_ms"], "launches": sel["launches"], "timing_source": timing_src,
             "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,
             "algorithmic_bytes_per_launch": sel["bytes_per_launch"], "traffic": traffic, "traffic_source": traffic_src,
-            "note": "the whole A8 call of a pass (every image): the KL ranking launch (kl_gauss_win_kernel) and the "
-                    "ranking of its keys (rank_topk_kernel), one timed scope"}
+            "note": "the KL keys of a pass's images (kl_gauss_stream_kernel), one launch; r06: the ranking of the "
+                    "keys moved into the candidates' argmax launch (skp_fps_keys_batch), timed in `selection`"}
         extra["a8_call_ms"] = sel["avg_ms"]
         extra["a8_split_isolated"] = a8_split
+    chain = timer.summary("skp_selection")
+    if chain:
+        extra["selection"] = {"avg_ms": chain["avg_ms"], "launches": chain["launches"], "timing_source": timing_src,
+                              "note": "a pass's whole selection, one timed scope: KL keys → ranking + the 25 candidates' "
+                                      "argmax on the warps' maps → FPS (3 launches; r05: 4)"}
     for k in ("skp_capture_fwd", "skp_capture_bwd"):
         s_ = timer.summary(k)
         if s_:

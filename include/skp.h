@@ -173,6 +173,14 @@ int skp_fps(const float* maps, int T, int h, int w, const long long* cand, int n
  * workspace >= 8 * nb * n_cand bytes.                                                        */
 int skp_fps_batch(const float* maps, int nb, int T, int h, int w, const long long* cand, int n_cand, int top_k,
                   long long* out, int* n_out, void* workspace, void* stream);
+/* The ranking of skp_topk_keys and the candidates' argmax of skp_fps_batch in one launch, then the
+   FPS launch: per image b, cand[b] = the n_cand tokens of smallest keys[b] (ascending; NaN last,
+   ties by index — torch.argsort(keys)[:n_cand] of find_top_k_gaussian, ptp_utils.py:110-112), and
+   out[b] / n_out[b] = furthest_point_sampling(maps[b], top_k, cand[b]) (ptp_utils.py:115-159) on the
+   (nb, T, h, w) maps the FPS reads (the warped image's, optimize.py:403-410).  workspace: 2·nb·n_cand
+   floats. */
+int skp_fps_keys_batch(const double* keys, const float* maps, int nb, int T, int h, int w, int n_cand, int top_k,
+                       long long* cand, long long* out, int* n_out, void* workspace, void* stream);
 
 /* ---------------------------------------------------------------- A11 sharpening
  * optimize.sharpening_loss (optimize.py:166-206): pos = k-max of A / w,

@@ -43,6 +43,7 @@ _SIGS = {
     "skp_entropy_sort": [_p, _c_int, _c_int, _c_int, _c_int, _p, _p, _p, _p],
     "skp_fps": [_p, _c_int, _c_int, _c_int, _p, _c_int, _c_int, _p, _p, _p, _p],
     "skp_fps_batch": [_p, _c_int, _c_int, _c_int, _c_int, _p, _c_int, _c_int, _p, _p, _p, _p],
+    "skp_fps_keys_batch": [_p, _p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _p, _p, _p, _p, _p],
     "skp_sharpen_fwd": [_p, _c_int, _c_int, _c_int, _c_float, _c_int, _p, _p, _p, _p],
     "skp_sharpen_bwd": [_p, _c_int, _c_int, _c_int, _c_float, _c_int, _p, _p, _p, _p],
     "skp_wino_in_transform": [_p, _c_int, _c_int, _c_int, _c_int, _p, _p],

@@ -660,6 +660,56 @@ __global__ __launch_bounds__(256) void rank_topk_kernel(const double* __restrict
   if (li == 0 && i < T && r < top_k) out[r] = i;
 }
 
+// r06: the ranking of the KL keys and the candidates' argmax in ONE launch (skp_fps_keys_batch): block
+// (b, i) finds the token of rank i among image b's T keys — rank_topk_kernel's strict order (NaN
+// last, ties by index), 16 lanes per key — and then takes the argmax of that token's row of the
+// FPS maps (argmax_kernel's torch order and position convention), so the selection chain of a
+// pass is KL → (rank + argmax) → FPS.  Every block ranks its image's keys again (T ≤ 8192 doubles
+// from L2); that redundant work replaces a dependent launch.
+__global__ __launch_bounds__(kRowThreads) void rank_argmax_kernel(const double* __restrict__ keys, int T, int C,
+                                                               const float* __restrict__ maps, int h, int w,
+                                                               long long* __restrict__ cand,
+                                                               float* __restrict__ pos) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* k = reinterpret_cast<double*>(smem);
+  __shared__ float sv[kRowThreads / 64];
+  __shared__ int si[kRowThreads / 64];
+  __shared__ int tok;
+  const int b = blockIdx.y, want = blockIdx.x;   // image, rank
+  keys += (size_t)b * T;
+  for (int i = threadIdx.x; i < T; i += blockDim.x) k[i] = keys[i];
+  if (threadIdx.x == 0) tok = -1;
+  __syncthreads();
+  const int li = threadIdx.x & 15;
+  for (int i0 = 0; i0 < T; i0 += kRowThreads / 16) {
+    const int i = i0 + (threadIdx.x >> 4);
+    const int ii = min(i, T - 1);
+    const double ki = k[ii];
+    const bool ni = isnan(ki);
+    int r = 0;
+    for (int j = li; j < T; j += 16) {
+      const double kj = k[j];   // NaN kj compares false: never before a number
+      r += ni ? ((!isnan(kj) || j < ii) ? 1 : 0) : ((kj < ki || (kj == ki && j < ii)) ? 1 : 0);
+    }
+    r += __shfl_xor(r, 1, 16);
+    r += __shfl_xor(r, 2, 16);
+    r += __shfl_xor(r, 4, 16);
+    r += __shfl_xor(r, 8, 16);
+    if (li == 0 && i < T && r == want) tok = i;   // ranks are a permutation: exactly one writer
+  }
+  __syncthreads();
+  const int t = tok;
+  float best;
+  int bi;
+  row_argmax_masked(maps + ((size_t)b * T + t) * h * w, h, w, nullptr, nullptr, 0, 0.0f, best, bi, sv, si);
+  if (threadIdx.x == 0) {
+    const size_t o = (size_t)b * C + want;
+    cand[o] = t;
+    pos[2 * o] = (float)(bi / w) + 0.5f;
+    pos[2 * o + 1] = (float)(bi % w) + 0.5f;
+  }
+}
+
 // Furthest-point sampling over candidate positions (ptp_utils.py:115-159), one wave.
 __global__ __launch_bounds__(64) void fps_kernel(const float* __restrict__ cpos, const long long* __restrict__ cand,
                                                  int C, int h, int top_k, long long* __restrict__ out,
@@ -970,6 +1020,28 @@ extern "C" int skp_fps_batch(const float* maps, int nb, int T, int h, int w, con
   float* cpos = reinterpret_cast<float*>(workspace);
   hipLaunchKernelGGL(argmax_kernel, dim3(nb * n_cand), dim3(kRowThreads), 0, st, maps, T, h, w, cand, n_cand, cpos,
                      (long long*)nullptr);
+  SKP_LAUNCH_CHECK();
+  const size_t lds = (size_t)n_cand * 8 + (size_t)n_cand * 8 + (size_t)top_k * 8 + (size_t)top_k * 8;
+  SKP_CHECK_ARG(lds <= 64 * 1024, "fps LDS budget exceeded");
+  hipLaunchKernelGGL(fps_kernel, dim3(nb), dim3(64), lds, st, cpos, cand, n_cand, h, top_k, out, n_out);
+  SKP_LAUNCH_CHECK();
+  return SKP_OK;
+}
+
+extern "C" int skp_fps_keys_batch(const double* keys, const float* maps, int nb, int T, int h, int w, int n_cand,
+                                  int top_k, long long* cand, long long* out, int* n_out, void* workspace,
+                                  void* stream) {
+  SKP_CHECK_ARG(keys && maps && cand && out && workspace, "null pointer");
+  SKP_CHECK_ARG(nb > 0 && T > 0 && h > 0 && w > 0, "non-positive shape");
+  SKP_CHECK_ARG(T <= 8192, "T > 8192 tokens is not supported by the selection ranking");
+  SKP_CHECK_ARG(n_cand >= 2 && n_cand <= T, "n_cand must be in [2, T]");
+  SKP_CHECK_ARG(n_cand <= 4096, "n_cand > 4096");
+  SKP_CHECK_ARG(top_k >= 2 && top_k <= 1024, "top_k out of range [2, 1024]");
+  SKP_CHECK_ARG(nb <= 65535 && n_cand <= 65535, "grid too large");
+  hipStream_t st = as_stream(stream);
+  float* cpos = reinterpret_cast<float*>(workspace);
+  hipLaunchKernelGGL(rank_argmax_kernel, dim3(n_cand, nb), dim3(kRowThreads), (size_t)T * sizeof(double), st, keys, T,
+                     n_cand, maps, h, w, cand, cpos);
   SKP_LAUNCH_CHECK();
   const size_t lds = (size_t)n_cand * 8 + (size_t)n_cand * 8 + (size_t)top_k * 8 + (size_t)top_k * 8;
   SKP_CHECK_ARG(lds <= 64 * 1024, "fps LDS budget exceeded");

@@ -133,19 +133,18 @@ def _select_batched(strategy, top_k, n_cand):
 
 def _select_stack(stack, top_k, n_cand, strategy, sigma, num_subjects):
     """The reference's per-image candidates + furthest-point sampling (keypoint_regressor.py:95-112)
-    for every image of a (B, N, S, S) stack: one skp_topk_gaussian_batch + skp_topk_keys (the entropy
-    strategy: the entropy kernel over all rows + skp_topk_keys; consistent: an arange) and one
-    skp_fps_batch launch.  Returns the device tensors ((B, top_k) picks, (B,)
+    for every image of a (B, N, S, S) stack: the keys of every row in one launch (the Gaussian KL, or
+    the entropies for the entropy strategy), the ranking + the candidates' argmax in one, FPS in one
+    (consistent: an arange and skp_fps_batch).  Returns the device tensors ((B, top_k) picks, (B,)
     counts): image b's picks are the first counts[b] (fewer when its FPS ran out of candidates, as
     the reference's list, ptp_utils.py:156-157)."""
     from . import ops
     B, N = stack.shape[:2]
-    if strategy == "gaussian":
-        cand = ops.find_top_k_gaussian_batch(stack, n_cand, sigma=sigma, num_subjects=num_subjects)
-    elif strategy == "entropy":   # keypoint_regressor.py:104-105, every image in two launches
-        cand = ops.entropy_sort_batch(stack, n_cand)
-    else:
-        cand = torch.arange(n_cand, device=stack.device).expand(B, n_cand)
+    if strategy == "gaussian":    # KL keys → ranking + the candidates' argmax → FPS: 3 launches
+        return ops.gaussian_fps_batch(stack, stack, n_cand, top_k, sigma=sigma, num_subjects=num_subjects)[:2]
+    if strategy == "entropy":     # keypoint_regressor.py:104-105: entropy keys → ranking + argmax → FPS
+        return ops.fps_from_keys_batch(ops.entropy_keys_batch(stack), stack, n_cand, top_k)[:2]
+    cand = torch.arange(n_cand, device=stack.device).expand(B, n_cand)
     return ops.furthest_point_sampling_batch(stack, top_k, cand)
 
 

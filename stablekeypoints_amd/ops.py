@@ -727,6 +727,61 @@ def furthest_point_sampling_batch(maps, top_k, candidates):
     return out, n_out
 
 
+def fps_from_keys_batch(keys, maps, n_cand, top_k):
+    """Per image b: the n_cand tokens of smallest keys[b] (torch.argsort order: NaN last, ties by
+    index), then furthest_point_sampling(maps[b], top_k, those candidates) — skp_fps_keys_batch:
+    the ranking and the candidates' argmax in one launch, then FPS.  keys (nb, T) float64, maps
+    (nb, T, h, w).  Returns ((nb, top_k) int64, (nb,) int32 counts, (nb, n_cand) candidates)."""
+    _lib.require_device(maps)
+    maps = _c(maps)
+    nb, T, h, w = maps.shape
+    keys = keys.to(device=maps.device, dtype=torch.float64).contiguous()
+    if tuple(keys.shape) != (nb, T):
+        raise ValueError(f"keys {tuple(keys.shape)} for maps {tuple(maps.shape)}")
+    n_cand = min(int(n_cand), T)
+    dev = maps.device
+    cand = torch.empty(nb, n_cand, device=dev, dtype=torch.int64)
+    out = torch.empty(nb, top_k, device=dev, dtype=torch.int64)
+    n_out = torch.empty(nb, device=dev, dtype=torch.int32)
+    ws = torch.empty(2 * nb * n_cand + 2, device=dev, dtype=F32)
+    call("skp_fps_keys_batch", ptr(keys), ptr(maps), nb, T, h, w, n_cand, int(top_k), ptr(cand), ptr(out), ptr(n_out),
+         ptr(ws), stream(dev))
+    return out, n_out, cand
+
+
+def gaussian_fps_batch(maps, maps_t, n_cand, top_k, sigma=3, epsilon=1e-5, num_subjects=1):
+    """The training pass's selection for every image of a stack (optimize.py:403-410 per replica):
+    candidates = find_top_k_gaussian(maps[b], n_cand), then
+    furthest_point_sampling(maps_t[b], top_k, candidates) — maps (nb, T, h, w) the images' maps,
+    maps_t the maps the FPS reads (the warps').  Three launches: the KL keys
+    (skp_topk_gaussian_batch, top_k 0), the ranking + the candidates' argmax on maps_t, FPS.
+    Returns what fps_from_keys_batch returns: identical to find_top_k_gaussian_batch +
+    furthest_point_sampling_batch."""
+    _lib.require_device(maps)
+    maps = _c(maps)
+    nb, T, h, w = maps.shape
+    if tuple(maps_t.shape) != (nb, T, h, w):
+        raise ValueError(f"maps_t {tuple(maps_t.shape)} for maps {tuple(maps.shape)}")
+    kl = torch.empty(nb, T, device=maps.device, dtype=torch.float64)
+    # one timed scope for the pass's whole selection chain (bench: `selection`)
+    with _timed("skp_selection", maps.numel() * 4 + nb * T * 8 + nb * min(int(n_cand), T) * h * w * 4):
+        with _timed("skp_topk_gaussian_batch", maps.numel() * 4 + nb * T * 8):
+            call("skp_topk_gaussian_batch", ptr(maps), nb, T, h, w, 0, float(sigma), float(epsilon),
+                 int(num_subjects), ptr(kl), ptr(kl), ptr(kl), stream(maps.device))
+        return fps_from_keys_batch(kl, maps_t, n_cand, top_k)
+
+
+def entropy_keys_batch(maps):
+    """The softmax entropies of every row of a (nb, T, h, w) stack (ptp_utils.py:179-182) in one
+    launch: (nb, T) float64, the keys entropy_sort ranks ascending."""
+    _lib.require_device(maps)
+    maps = _c(maps)
+    nb, T, h, w = maps.shape
+    ent = torch.empty(nb, T, device=maps.device, dtype=torch.float64)
+    call("skp_entropy_sort", ptr(maps), nb * T, h, w, 0, ptr(ent), ptr(ent), ptr(ent), stream(maps.device))
+    return ent
+
+
 def entropy_sort_batch(maps, top_k):
     """entropy_sort of every image of a (nb, T, h, w) stack: the entropies of all nb·T rows in one
     launch (skp_entropy_sort's kernel, no ranking), then the per-image ascending top_k of them in

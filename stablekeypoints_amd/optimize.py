@@ -403,17 +403,18 @@ class TokenOptimizer:
 
     def _select_batch(self, maps, maps_t):
         """_select for k images at once: maps / maps_t (k, N, R, R) = the images' and their warps'
-        maps.  The Gaussian top-k ranking and the furthest-point sampling run as one launch each
-        over the k images (skp_topk_gaussian_batch / skp_fps_batch); each image's selection is the
-        reference's for that image (optimize.py:403-424 per replica).  Falls back to per-image
+        maps.  The Gaussian KL keys, the candidates' ranking + argmax, and the furthest-point
+        sampling run as one launch each over the k images (ops.gaussian_fps_batch); each image's
+        selection is the reference's for that image (optimize.py:403-424 per replica).  Falls back to per-image
         _select where the batched form does not apply (other strategies, fewer candidates than
         top_k)."""
         k, N = maps.shape[0], maps.shape[1]
         n_cand = min(int(self.fps_n), N)
         if not (SEL_BATCH and k > 1 and self.top_k_strategy == "gaussian" and 2 <= self.top_k <= n_cand):
             return [self._select(maps[i], maps_t[i]) for i in range(k)]
-        cand = ops.find_top_k_gaussian_batch(maps, n_cand, sigma=self.sigma, num_subjects=self.num_subjects)
-        sel, _ = ops.furthest_point_sampling_batch(maps_t, self.top_k, cand)
+        # KL keys → (ranking + the candidates' argmax on the warps' maps) → FPS: three launches
+        sel, _, _ = ops.gaussian_fps_batch(maps, maps_t, n_cand, self.top_k, sigma=self.sigma,
+                                           num_subjects=self.num_subjects)
         return list(sel.unbind(0))
 
     def _select(self, attn_map, attention_map_transformed):

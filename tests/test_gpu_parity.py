@@ -248,6 +248,34 @@ def test_topk_keys_rank_kernel_vs_stable_argsort(nb, Tn, top_k):
     assert np.array_equal(N(out), ref)
 
 
+@pytest.mark.parametrize("nb,Tn,R,n_cand,top_k", [(4, 500, 128, 25, 10), (3, 129, 32, 25, 10), (2, 37, 64, 37, 5),
+                                                  (1, 500, 256, 25, 10)])
+def test_fps_keys_batch_equals_rank_then_fps(nb, Tn, R, n_cand, top_k):
+    """r06 selection chain: ops.gaussian_fps_batch — KL keys, then the ranking and
+    the candidates' argmax in ONE launch (skp_fps_keys_batch), then FPS — selects exactly what the
+    r05 chain (find_top_k_gaussian_batch's KL + rank launches, furthest_point_sampling_batch's argmax +
+    FPS launches) selects: picks, counts and candidates, with FPS on different maps than the ranking
+    (the warps', optimize.py:403-410), duplicated rows (equal keys: ties by index), a NaN row (last)
+    and a flat row (argmax ties); and the entropy strategy's keys through the same launch."""
+    from stablekeypoints_amd import ops
+    maps = np.stack([recipes.attention_like_maps(400 + i, Tn, R) for i in range(nb)]).astype(np.float32)
+    maps_t = np.stack([recipes.attention_like_maps(500 + i, Tn, R) for i in range(nb)]).astype(np.float32)
+    maps[:, 3] = maps[:, 1]
+    maps[:, min(10, Tn - 1)] = np.nan
+    maps_t[:, 2] = 0.5
+    m, mt = T(maps), T(maps_t)
+    sel, n, cand = ops.gaussian_fps_batch(m, mt, n_cand, top_k, sigma=2.0)
+    cand0 = ops.find_top_k_gaussian_batch(m, n_cand, sigma=2.0)
+    sel0, n0 = ops.furthest_point_sampling_batch(mt, top_k, cand0)
+    assert torch.equal(cand, cand0) and torch.equal(sel, sel0) and torch.equal(n, n0)
+    ent = np.abs(maps_t) * 50.0   # finite rows for the entropies
+    e = T(ent)
+    sel_e, n_e, cand_e = ops.fps_from_keys_batch(ops.entropy_keys_batch(e), e, n_cand, top_k)
+    cand_e0 = ops.entropy_sort_batch(e, n_cand)
+    sel_e0, n_e0 = ops.furthest_point_sampling_batch(e, top_k, cand_e0)
+    assert torch.equal(cand_e, cand_e0) and torch.equal(sel_e, sel_e0) and torch.equal(n_e, n_e0)
+
+
 def test_entropy_sort_batch_equals_per_image():
     """ops.entropy_sort_batch (the entropies of all images' rows in one launch, the per-image
     top-k in one skp_topk_keys launch: the batched `entropy` strategy of find_best_indices,
