@@ -109,7 +109,12 @@ __device__ __forceinline__ void adj_range(int j, int S, int R, int& lo, int& hi)
 // sel_dot with the horizontal half of the sparse part's bicubicᵀ fused in (r05): the row's e_k stay
 // in LDS and leave as Hs[l][bh][k][y][j] = Σ_x A[j][x]·e_k[y][x] (R·s floats per (bh, k) instead
 // of E's R², so E's write + re-read — 2 × 168 MB at the bench shape — is gone; sel_adjv does the
-// vertical half).  One block per (layer, bh, y), R threads (R ≤ 256).
+// vertical half).  One block per (layer, bh, y), R threads (R ≤ 256).  The kernel is a chain of
+// short phases (staging → pixels → columns) over 32 K blocks at the bench shape, so its time is
+// set by how many blocks a CU holds and by each block's exposed load latency: r06 issues every
+// global load of the block (the staging's selected logits, the pixel's stats and its K gradient
+// values) before the first barrier, keeps the LDS at ≈ 9 KB (pads of 3.5·RATIO, no column buffer)
+// and writes the Hs values straight from the column phase (2 barriers instead of 3).
 // At R = RATIO·s (RATIO a power of two) virtual column c takes its taps from the 4·RATIO pixels
 // x = RATIO·(c − 2) + RATIO/2 + t, t ∈ [0, 4·RATIO), with weight W[t] = w_{3 − t/RATIO} of pixel
 // phase (RATIO/2 + t) mod RATIO: one fixed filter for every column, so column c is a 4·RATIO-tap dot
@@ -117,49 +122,69 @@ __device__ __forceinline__ void adj_range(int j, int S, int R, int& lo, int& hi)
 // virtual columns −2, −1, 0 / S − 1, S, S + 1 in that order.  Per column the terms run x ascending
 // from 0 — the summation order of a rolling window over the row (r04's sel_adjw, which took E
 // through HBM; r05 measured Hs and es bit-identical to it before it was removed in r06).
-constexpr int DOTH_PAD = 64;   // zero floats each side of a row's e (≥ 3.5·RATIO at RATIO ≤ 16)
+template <int RMAX>
+constexpr int doth_pad() { return 4 * RMAX; }   // zero floats each side of a row's e (≥ 3.5·RATIO)
 
-// virtual columns c = cv − 2, cv ∈ [0, S + 4): Vc[cv][k] = Σ_t W[t]·e_k[RATIO·(c − 2) + RATIO/2 + t]
-// (one fixed-length dot product per lane, lanes over k first: rows k sit 4 banks apart)
-template <int RATIO>
-__device__ __forceinline__ void doth_columns(const float* __restrict__ W, const float* __restrict__ Ep, int EP, int K,
-                                             int S, float* __restrict__ Vc) {
+// virtual column c = cv − 2 of e row k: Σ_t W[t]·e_k[RATIO·(c − 2) + RATIO/2 + t]
+template <int RATIO, int PAD>
+__device__ __forceinline__ float doth_column(const float* __restrict__ W, const float* __restrict__ Ek, int cv) {
   constexpr int NT = 4 * RATIO;
-  float w[NT];
+  const float* src = Ek + PAD + RATIO / 2 - 4 * RATIO + RATIO * cv;
+  float a = 0.0f;
+  if constexpr (RATIO >= 8) {   // 16-B aligned runs (EP, PAD and RATIO/2 multiples of 4)
+    const float4* s4 = reinterpret_cast<const float4*>(src);
+    const float4* w4 = reinterpret_cast<const float4*>(W);
 #pragma unroll
-  for (int q = 0; q < NT; ++q) w[q] = W[q];
-  for (int e = threadIdx.x; e < K * (S + 4); e += blockDim.x) {
-    const int k = e % K, cv = e / K;
-    const float* src = Ep + k * EP + DOTH_PAD + RATIO / 2 - 4 * RATIO + RATIO * cv;
-    float a = 0.0f;
-    if constexpr (RATIO >= 8) {   // 16-B aligned runs (EP, DOTH_PAD and RATIO/2 multiples of 4)
-      const float4* s4 = reinterpret_cast<const float4*>(src);
-#pragma unroll
-      for (int q = 0; q < NT / 4; ++q) {
-        const float4 v = s4[q];
-        a = fmaf(w[4 * q], v.x, a);
-        a = fmaf(w[4 * q + 1], v.y, a);
-        a = fmaf(w[4 * q + 2], v.z, a);
-        a = fmaf(w[4 * q + 3], v.w, a);
-      }
-    } else {                      // 8-B aligned at RATIO = 4
-      const float2* s2 = reinterpret_cast<const float2*>(src);
-#pragma unroll
-      for (int q = 0; q < NT / 2; ++q) {
-        const float2 v = s2[q];
-        a = fmaf(w[2 * q], v.x, a);
-        a = fmaf(w[2 * q + 1], v.y, a);
-      }
+    for (int q = 0; q < NT / 4; ++q) {
+      const float4 v = s4[q], w = w4[q];
+      a = fmaf(w.x, v.x, a);
+      a = fmaf(w.y, v.y, a);
+      a = fmaf(w.z, v.z, a);
+      a = fmaf(w.w, v.w, a);
     }
-    Vc[e] = a;
+  } else {                      // 8-B aligned at RATIO = 4
+    const float2* s2 = reinterpret_cast<const float2*>(src);
+    const float2* w2 = reinterpret_cast<const float2*>(W);
+#pragma unroll
+    for (int q = 0; q < NT / 2; ++q) {
+      const float2 v = s2[q], w = w2[q];
+      a = fmaf(w.x, v.x, a);
+      a = fmaf(w.y, v.y, a);
+    }
+  }
+  return a;
+}
+
+// Hs[j][k] of the row (lanes over k first: rows k sit 4 banks apart), the clamped edge columns as
+// their virtual columns in order (−2, −1, 0 / S − 1, S, S + 1)
+template <int RATIO, int PAD>
+__device__ __forceinline__ void doth_hs(const float* __restrict__ W, const float* __restrict__ Ep, int EP, int K, int S,
+                                        int R, int smax, float* __restrict__ hb) {
+  for (int e = threadIdx.x; e < K * S; e += blockDim.x) {
+    const int k = e % K, j = e / K;
+    const float* Ek = Ep + k * EP;
+    const bool edge = j == 0 || j == S - 1;
+    const int c0 = j == 0 ? 0 : (j == S - 1 ? S + 1 : j + 2);
+    float s = doth_column<RATIO, PAD>(W, Ek, c0);
+    if (edge) {
+      s += doth_column<RATIO, PAD>(W, Ek, c0 + 1);
+      s += doth_column<RATIO, PAD>(W, Ek, c0 + 2);
+    }
+    hb[(size_t)k * R * smax + j] = s;   // Hs[l][bh][k][y][j]
   }
 }
 
 template <int RMAX>
+constexpr size_t doth_lds_floats(int smax, int K, int R) {
+  return 64 + (size_t)((smax * K + 3) & ~3) + (size_t)K * (R + 2 * doth_pad<RMAX>() + 4);
+}
+
+template <int RMAX, int KMAX>
 __global__ __launch_bounds__(256) void sel_doth_kernel(SelSmall t, const float* __restrict__ zsel, int BH, int R,
                                                        int H, int K, const long long* __restrict__ tok,
                                                        const float* __restrict__ gsel, float gscale, int smax,
                                                        float* __restrict__ Hs, float2* __restrict__ pix) {
+  constexpr int PAD = doth_pad<RMAX>();
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int l = blockIdx.x / (BH * R);
   const int rem = blockIdx.x - l * (BH * R);
@@ -167,109 +192,111 @@ __global__ __launch_bounds__(256) void sel_doth_kernel(SelSmall t, const float* 
   const int b = bh / H;
   const int S = t.s[l];
   const int ratio = R / S;
-  const int EP = R + 2 * DOTH_PAD + 4;   // a multiple of 4 floats: 16-B aligned row runs
+  const int EP = R + 2 * PAD + 4;       // a multiple of 4 floats: 16-B aligned row runs
   float* W = sm;                        // [64] the column filter
-  float* Vs = W + 64;                   // S × K
-  float* Ep = Vs + ((S * K + 3) & ~3);  // K × EP, the row's e at [DOTH_PAD, DOTH_PAD + R)
+  float* Vs = W + 64;                   // S × K: the row's vertical pass of the selected logits
+  float* Ep = Vs + ((smax * K + 3) & ~3);   // K × EP, the row's e at [PAD, PAD + R)
   const size_t RR = (size_t)R * R;
-  pix += (size_t)l * BH * RR;
-  const float2* stats = t.stats[l];
-  const Taps4 ty = bicubic_taps(y, S, R);
-  const float* zb = zsel + t.zoff[l] + (size_t)bh * S * S * K;
-  for (int e = threadIdx.x; e < S * K; e += blockDim.x) {
-    const int j = e / K, k = e - j * K;
-    float v = ty.w[0] * zb[((size_t)ty.i[0] * S + j) * K + k];
-    v = fmaf(ty.w[1], zb[((size_t)ty.i[1] * S + j) * K + k], v);
-    v = fmaf(ty.w[2], zb[((size_t)ty.i[2] * S + j) * K + k], v);
-    v = fmaf(ty.w[3], zb[((size_t)ty.i[3] * S + j) * K + k], v);
-    Vs[e] = v;
+  const int x = threadIdx.x;            // blockDim.x == R
+  const size_t p = (size_t)y * R + x;
+  // every global load of the block first: the pixel's stats and gradient values, then the staging
+  const float2 st = t.stats[l][(size_t)bh * RR + p];
+  const float* gp = gsel + (size_t)b * K * RR + p;
+  float gv[KMAX];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k)
+    if (k < K) gv[k] = gp[(size_t)k * RR];
+  unsigned selmask = 0;                 // bit k: token k selected (tok ≥ 0)
+  for (int k = 0; k < K; ++k) selmask |= (tok[(size_t)b * K + k] >= 0 ? 1u : 0u) << k;
+  {
+    const Taps4 ty = bicubic_taps(y, S, R);
+    const float* zb = zsel + t.zoff[l] + (size_t)bh * S * S * K;
+    for (int e = x; e < S * K; e += blockDim.x) {
+      const int j = e / K, k = e - j * K;
+      float v = ty.w[0] * zb[((size_t)ty.i[0] * S + j) * K + k];
+      v = fmaf(ty.w[1], zb[((size_t)ty.i[1] * S + j) * K + k], v);
+      v = fmaf(ty.w[2], zb[((size_t)ty.i[2] * S + j) * K + k], v);
+      v = fmaf(ty.w[3], zb[((size_t)ty.i[3] * S + j) * K + k], v);
+      Vs[e] = v;
+    }
   }
-  for (int e = threadIdx.x; e < K * 2 * DOTH_PAD; e += blockDim.x) {   // the zero pads
-    const int k = e / (2 * DOTH_PAD), q = e - k * (2 * DOTH_PAD);
-    Ep[k * EP + (q < DOTH_PAD ? q : R + q)] = 0.0f;
+  for (int e = x; e < K * 2 * PAD; e += blockDim.x) {   // the zero pads
+    const int k = e / (2 * PAD), q = e - k * (2 * PAD);
+    Ep[k * EP + (q < PAD ? q : R + q)] = 0.0f;
   }
-  const int x = threadIdx.x;   // blockDim.x == R
   const Taps4 tx = bicubic_taps(x, S, R);
   if (x < ratio) {   // phase x's weights into the filter
 #pragma unroll
     for (int m = 0; m < 4; ++m) W[ratio * (3 - m) + (x + ratio / 2) % ratio] = tx.w[m];
   }
   __syncthreads();
-  const size_t p = (size_t)y * R + x;
-  const float2 st = stats[(size_t)bh * RR + p];
   const float mb = __builtin_amdgcn_logf(st.y) - st.x * L2E;   // v_log_f32 = log2
   float dot = 0.0f;
-  for (int k = 0; k < K; ++k) {
-    float e = 0.0f;
-    if (tok[(size_t)b * K + k] >= 0) {
-      float z = tx.w[0] * Vs[tx.i[0] * K + k];
-      z = fmaf(tx.w[1], Vs[tx.i[1] * K + k], z);
-      z = fmaf(tx.w[2], Vs[tx.i[2] * K + k], z);
-      z = fmaf(tx.w[3], Vs[tx.i[3] * K + k], z);
-      const float a = __builtin_amdgcn_exp2f(fmaf(z, L2E, mb));
-      e = a * (gsel[((size_t)b * K + k) * RR + p] * gscale);
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    if (k < K) {
+      float e = 0.0f;
+      if ((selmask >> k) & 1u) {
+        float z = tx.w[0] * Vs[tx.i[0] * K + k];
+        z = fmaf(tx.w[1], Vs[tx.i[1] * K + k], z);
+        z = fmaf(tx.w[2], Vs[tx.i[2] * K + k], z);
+        z = fmaf(tx.w[3], Vs[tx.i[3] * K + k], z);
+        const float a = __builtin_amdgcn_exp2f(fmaf(z, L2E, mb));
+        e = a * (gv[k] * gscale);
+      }
+      dot += e;
+      Ep[k * EP + PAD + x] = e;
     }
-    dot += e;
-    Ep[k * EP + DOTH_PAD + x] = e;
   }
-  pix[(size_t)bh * RR + p] = sel_pix(mb, dot);
+  pix[(size_t)l * BH * RR + (size_t)bh * RR + p] = sel_pix(mb, dot);
   __syncthreads();
   float* hb = Hs + ((size_t)l * BH + bh) * K * R * smax + (size_t)y * smax;
-  float* Vc = Ep + K * EP;   // [S + 4][K]
-  if (RMAX >= 16 && ratio == 16) doth_columns<(RMAX >= 16 ? 16 : 8)>(W, Ep, EP, K, S, Vc);
-  else if (ratio == 8) doth_columns<8>(W, Ep, EP, K, S, Vc);
-  else doth_columns<4>(W, Ep, EP, K, S, Vc);
-  __syncthreads();
-  // clamped edge columns: their virtual columns in order (−2, −1, 0 / S − 1, S, S + 1)
-  for (int e = threadIdx.x; e < K * S; e += blockDim.x) {
-    const int j = e % S, k = e / S;   // lanes over j: each k's row of s columns leaves contiguous
-    float s;
-    if (j == 0) {
-      s = Vc[k];
-      s += Vc[K + k];
-      s += Vc[2 * K + k];
-    } else if (j == S - 1) {
-      s = Vc[(S + 1) * K + k];
-      s += Vc[(S + 2) * K + k];
-      s += Vc[(S + 3) * K + k];
-    } else {
-      s = Vc[(j + 2) * K + k];
-    }
-    hb[(size_t)k * R * smax + j] = s;   // Hs[l][bh][k][y][j]
-  }
+  if (RMAX >= 16 && ratio == 16) doth_hs<(RMAX >= 16 ? 16 : 8), PAD>(W, Ep, EP, K, S, R, smax, hb);
+  else if (ratio == 8) doth_hs<8, PAD>(W, Ep, EP, K, S, R, smax, hb);
+  else doth_hs<4, PAD>(W, Ep, EP, K, S, R, smax, hb);
 }
 
 // The vertical half of the sparse part's bicubicᵀ after sel_doth: es[i][j] = Σ_y A[i][y]·Hs[y][j]
-// (y ascending) on the R × s rows sel_doth left in HBM.  Block = (layer,
-// bh, k), 256 threads; LDS: the adjoint matrix A[S][R + 1] and the block's Hs rows [R][S].
+// (y ascending) on the R × s rows sel_doth left in HBM.  Block = (layer, bh, k), 256 threads; LDS:
+// the block's Hs rows [R][S] and the adjoint matrix as its band, Ab[i][y − y0(i)] for y in
+// adj_range(i) (≤ 4·R/S + 4 entries per row; r05 held A dense, S × (R + 1), which limited the
+// blocks per CU at s = 32).  Entry (i, y) belongs to output row y's thread: it zeroes its entries and
+// adds its taps in order, so A is built without a barrier.
 __global__ __launch_bounds__(256) void sel_adjv_kernel(SelSmall t, const float* __restrict__ Hsg, int BH, int BHK,
                                                        int smax, int R, float* __restrict__ es) {
   extern __shared__ float sh[];
-  const int RP = R + 1;
   const int l = blockIdx.x / BHK;
   const int S = t.s[l];
-  float* A = sh;               // S × (R + 1)
-  float* Hs = A + S * RP;      // R × S
+  const int BW = 4 * (R / S) + 6;   // band width ≥ adj_range's hi − lo + 1
+  float* Hs = sh;                   // R × S
+  float* Ab = Hs + R * S;           // S × BW
   const size_t bk = blockIdx.x - (size_t)l * BHK;  // bh·K + k
   const float* hb = Hsg + ((size_t)l * BHK + bk) * (size_t)R * smax;   // [y][j] rows of sel_doth
   es += (size_t)l * BHK * smax * smax;
-  for (int e = threadIdx.x; e < S * RP; e += blockDim.x) A[e] = 0.0f;
   for (int e = threadIdx.x; e < R * S; e += blockDim.x) {
     const int yy = e / S, j = e - yy * S;
     Hs[e] = hb[(size_t)yy * smax + j];
   }
-  __syncthreads();
   for (int y = threadIdx.x; y < R; y += blockDim.x) {
+    for (int i = 0; i < S; ++i) {
+      int y0, y1;
+      adj_range(i, S, R, y0, y1);
+      if (y >= y0 && y <= y1) Ab[i * BW + (y - y0)] = 0.0f;
+    }
     const Taps4 ty = bicubic_taps(y, S, R);
 #pragma unroll
-    for (int m = 0; m < 4; ++m) A[ty.i[m] * RP + y] += ty.w[m];
+    for (int m = 0; m < 4; ++m) {
+      int y0, y1;
+      adj_range(ty.i[m], S, R, y0, y1);
+      if (y >= y0 && y <= y1) Ab[ty.i[m] * BW + (y - y0)] += ty.w[m];
+    }
   }
   __syncthreads();
   for (int e = threadIdx.x; e < S * S; e += blockDim.x) {
     const int i = e / S, j = e - i * S;
     int y0, y1;
     adj_range(i, S, R, y0, y1);
-    const float* Ai = A + i * RP;
+    const float* Ai = Ab + i * BW - y0;
     float acc = 0.0f;
     for (int yy = y0; yy <= y1; ++yy) acc = fmaf(Ai[yy], Hs[yy * S + j], acc);
     es[bk * (size_t)S * S + e] = acc;
@@ -636,6 +663,18 @@ __global__ void sel_scatter_kernel(const long long* __restrict__ tok, const floa
   }
 }
 
+template <int RMAX>
+void launch_doth(const SelSmall& t, int L, int BH, int R, int H, int K, int smax, const long long* tok,
+                 const float* gsel, float gscale, const float* zsel, float* hs, float2* pix, hipStream_t st) {
+  const size_t lds = doth_lds_floats<RMAX>(smax, K, R) * sizeof(float);
+  if (K <= 16)   // the pixel's gradient values are held in registers: 16 or SEL_MAXK of them
+    hipLaunchKernelGGL((sel_doth_kernel<RMAX, 16>), dim3((unsigned)(L * BH * R)), dim3(R), lds, st, t, zsel, BH, R, H, K,
+                       tok, gsel, gscale, smax, hs, pix);
+  else
+    hipLaunchKernelGGL((sel_doth_kernel<RMAX, SEL_MAXK>), dim3((unsigned)(L * BH * R)), dim3(R), lds, st, t, zsel, BH, R,
+                       H, K, tok, gsel, gscale, smax, hs, pix);
+}
+
 struct SelWs {   // workspace carve-up (floats)
   size_t zsel, hs, pix, es, total;
 };
@@ -763,18 +802,13 @@ extern "C" int skp_capture_maps_bwd_sel(const float* const* z_low, const int* si
   if (tev) (void)hipEventRecord(tev[1], st);
   // sel_doth: per (layer, bh, row) a_k, e_k = a_k·g_k and dot, with the horizontal half of the
   // sparse part's bicubicᵀ applied in LDS (Hs rows; the R² e rows never reach HBM)
-  const size_t lds = (size_t)(64 + ((smax * K + 3) & ~3) + K * (R + 2 * DOTH_PAD + 4) + K * (R / 4 + 4)) * sizeof(float);
-  if (rmax <= 8)
-    hipLaunchKernelGGL(sel_doth_kernel<8>, dim3((unsigned)(L * BH * R)), dim3(R), lds, st, t, zsel, BH, R, H, K, sel_tok,
-                       gsel, gscale, smax, hs, pix);
-  else
-    hipLaunchKernelGGL(sel_doth_kernel<16>, dim3((unsigned)(L * BH * R)), dim3(R), lds, st, t, zsel, BH, R, H, K,
-                       sel_tok, gsel, gscale, smax, hs, pix);
+  if (rmax <= 8) launch_doth<8>(t, L, BH, R, H, K, smax, sel_tok, gsel, gscale, zsel, hs, pix, st);
+  else launch_doth<16>(t, L, BH, R, H, K, smax, sel_tok, gsel, gscale, zsel, hs, pix, st);
   SKP_LAUNCH_CHECK();
   if (tev) (void)hipEventRecord(tev[2], st);
   // sel_adjv: the vertical half → es[l][bh][k] (s × s per selected row)
   hipLaunchKernelGGL(sel_adjv_kernel, dim3((unsigned)(L * BH * K)), dim3(256),
-                     (size_t)(smax * (R + 1) + R * smax) * sizeof(float), st, t, hs, BH, BH * K, smax, R, es);
+                     (size_t)(R * smax + 4 * R + 6 * smax) * sizeof(float), st, t, hs, BH, BH * K, smax, R, es);
   SKP_LAUNCH_CHECK();
   if (tev) (void)hipEventRecord(tev[3], st);
   // the dense part: layers of equal s share a class (up to 4 per launch); two classes that have
