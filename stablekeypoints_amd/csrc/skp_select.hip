@@ -661,50 +661,67 @@ __global__ __launch_bounds__(256) void rank_topk_kernel(const double* __restrict
 }
 
 // r06: the ranking of the KL keys and the candidates' argmax in ONE launch (skp_fps_keys_batch): block
-// (b, i) finds the token of rank i among image b's T keys — rank_topk_kernel's strict order (NaN
-// last, ties by index), 16 lanes per key — and then takes the argmax of that token's row of the
-// FPS maps (argmax_kernel's torch order and position convention), so the selection chain of a
-// pass is KL → (rank + argmax) → FPS.  Every block ranks its image's keys again (T ≤ 8192 doubles
-// from L2); that redundant work replaces a dependent launch.
-__global__ __launch_bounds__(kRowThreads) void rank_argmax_kernel(const double* __restrict__ keys, int T, int C,
-                                                               const float* __restrict__ maps, int h, int w,
-                                                               long long* __restrict__ cand,
-                                                               float* __restrict__ pos) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  double* k = reinterpret_cast<double*>(smem);
-  __shared__ float sv[kRowThreads / 64];
-  __shared__ int si[kRowThreads / 64];
-  __shared__ int tok;
-  const int b = blockIdx.y, want = blockIdx.x;   // image, rank
+// (i, b) ranks token i among image b's T keys — rank_topk_kernel's strict order (NaN last, ties by
+// index), the block's threads over the other keys — and, if the rank r is below C, takes the argmax
+// of token i's row of the FPS maps (argmax_kernel's torch order and position convention) and writes
+// candidate r.  Ranks are a permutation, so exactly one block writes each candidate; the C blocks
+// with an argmax to do are the only ones that read a map row.  The selection chain of a pass is
+// KL → (rank + argmax) → FPS.
+#ifndef SKP_RANKARG_THREADS
+#define SKP_RANKARG_THREADS 512   // threads per rank_argmax block (256: 15.2 us, 1024: 15.8, 512: 13.3)
+#endif
+constexpr int kRankArgThreads = SKP_RANKARG_THREADS;
+__global__ __launch_bounds__(kRankArgThreads) void rank_argmax_kernel(const double* __restrict__ keys, int T, int C,
+                                                                   const float* __restrict__ maps, int h, int w,
+                                                                   long long* __restrict__ cand,
+                                                                   float* __restrict__ pos) {
+  __shared__ float sv[kRankArgThreads / 64];
+  __shared__ int si[kRankArgThreads / 64];
+  __shared__ double sd[kRankArgThreads / 64];
+  const int i = blockIdx.x, b = blockIdx.y;
   keys += (size_t)b * T;
-  for (int i = threadIdx.x; i < T; i += blockDim.x) k[i] = keys[i];
-  if (threadIdx.x == 0) tok = -1;
-  __syncthreads();
-  const int li = threadIdx.x & 15;
-  for (int i0 = 0; i0 < T; i0 += kRowThreads / 16) {
-    const int i = i0 + (threadIdx.x >> 4);
-    const int ii = min(i, T - 1);
-    const double ki = k[ii];
-    const bool ni = isnan(ki);
-    int r = 0;
-    for (int j = li; j < T; j += 16) {
-      const double kj = k[j];   // NaN kj compares false: never before a number
-      r += ni ? ((!isnan(kj) || j < ii) ? 1 : 0) : ((kj < ki || (kj == ki && j < ii)) ? 1 : 0);
-    }
-    r += __shfl_xor(r, 1, 16);
-    r += __shfl_xor(r, 2, 16);
-    r += __shfl_xor(r, 4, 16);
-    r += __shfl_xor(r, 8, 16);
-    if (li == 0 && i < T && r == want) tok = i;   // ranks are a permutation: exactly one writer
+  const double ki = keys[i];
+  const bool ni = isnan(ki);
+  double r = 0.0;   // a count: exact in any order
+  for (int j = threadIdx.x; j < T; j += blockDim.x) {
+    const double kj = keys[j];   // NaN kj compares false: never before a number
+    r += ni ? ((!isnan(kj) || j < i) ? 1.0 : 0.0) : ((kj < ki || (kj == ki && j < i)) ? 1.0 : 0.0);
   }
-  __syncthreads();
-  const int t = tok;
-  float best;
-  int bi;
-  row_argmax_masked(maps + ((size_t)b * T + t) * h * w, h, w, nullptr, nullptr, 0, 0.0f, best, bi, sv, si);
+  const int rank = (int)block_sum(r, sd);
+  if (rank >= C) return;   // uniform
+  // the row's argmax with 4 16-B loads in flight per thread (argmax_better is a total order, so
+  // the visiting order does not matter)
+  const float* m = maps + ((size_t)b * T + i) * h * w;
+  const int HW = h * w;
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+  if ((HW & 3) == 0 && (reinterpret_cast<uintptr_t>(m) & 15) == 0) {
+    const float4* m4 = reinterpret_cast<const float4*>(m);
+    const int n4 = HW >> 2, step = blockDim.x;
+    for (int q0 = threadIdx.x; q0 < n4; q0 += 4 * step) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (q0 + u * step < n4) v[u] = m4[q0 + u * step];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int q = q0 + u * step;
+        if (q < n4) {
+          if (argmax_better(v[u].x, 4 * q, best, bi)) { best = v[u].x; bi = 4 * q; }
+          if (argmax_better(v[u].y, 4 * q + 1, best, bi)) { best = v[u].y; bi = 4 * q + 1; }
+          if (argmax_better(v[u].z, 4 * q + 2, best, bi)) { best = v[u].z; bi = 4 * q + 2; }
+          if (argmax_better(v[u].w, 4 * q + 3, best, bi)) { best = v[u].w; bi = 4 * q + 3; }
+        }
+      }
+    }
+  } else {
+    for (int e = threadIdx.x; e < HW; e += blockDim.x)
+      if (argmax_better(m[e], e, best, bi)) { best = m[e]; bi = e; }
+  }
+  block_argmax(best, bi, sv, si);
   if (threadIdx.x == 0) {
-    const size_t o = (size_t)b * C + want;
-    cand[o] = t;
+    const size_t o = (size_t)b * C + rank;
+    cand[o] = i;
     pos[2 * o] = (float)(bi / w) + 0.5f;
     pos[2 * o + 1] = (float)(bi % w) + 0.5f;
   }
@@ -789,6 +806,119 @@ __global__ __launch_bounds__(64) void fps_kernel(const float* __restrict__ cpos,
   }
   for (int q = lane; q < top_k; q += 64) out[q] = q < nsel ? sel[q] : -1;
   if (lane == 0 && n_out) *n_out = nsel;
+}
+
+// The same FPS with one candidate per lane (C ≤ 64, top_k ≤ 64; r06): the candidates' positions and
+// tokens stay in registers and every lane keeps its candidate's running minimum distance to the
+// selected set, updated with the newest pick only — fminf over the same distances in another order
+// is the same minimum, and the NaN flag is an OR — so a round is one distance and one wave
+// reduction instead of nsel distances read back from LDS.  Selections are identical to fps_kernel's.
+__device__ __forceinline__ float lane_f(float v, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+__device__ __forceinline__ long long lane_ll(long long v, int l) {
+  const unsigned long long u = (unsigned long long)v;
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
+  return (long long)(((unsigned long long)hi << 32) | lo);
+}
+// (v, i) with the larger v, ties to the smaller i (FPS's strict '>' in index order; v is never NaN
+// here), over the wave: DPP within each 16-lane row (quad perms, half-row and row mirrors — no LDS
+// round trip as __shfl_xor's ds_bpermute takes), then the 4 row results read into SGPRs: the result
+// is wave-uniform
+__device__ __forceinline__ void fps_pick(float& v, int& i, float ov, int oi) {
+  if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }
+}
+template <int CTRL>
+__device__ __forceinline__ void fps_dpp_step(float& v, int& i) {
+  const float ov = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v),
+                                                                         __builtin_bit_cast(int, v), CTRL, 0xF, 0xF,
+                                                                         false));
+  const int oi = __builtin_amdgcn_update_dpp(i, i, CTRL, 0xF, 0xF, false);
+  fps_pick(v, i, ov, oi);
+}
+__device__ __forceinline__ void fps_wave_best(float& v, int& i) {
+  fps_dpp_step<0xB1>(v, i);    // quad_perm [1, 0, 3, 2]
+  fps_dpp_step<0x4E>(v, i);    // quad_perm [2, 3, 0, 1]
+  fps_dpp_step<0x141>(v, i);   // row_half_mirror
+  fps_dpp_step<0x140>(v, i);   // row_mirror
+  float bv = lane_f(v, 0);
+  int bi = __builtin_amdgcn_readlane(i, 0);
+#pragma unroll
+  for (int r = 1; r < 4; ++r) fps_pick(bv, bi, lane_f(v, 16 * r), __builtin_amdgcn_readlane(i, 16 * r));
+  v = bv;
+  i = bi;
+}
+
+__global__ __launch_bounds__(64) void fps_wave_kernel(const float* __restrict__ cpos, const long long* __restrict__ cand,
+                                                      int C, int h, int top_k, long long* __restrict__ out,
+                                                      int* __restrict__ n_out) {
+  const int lane = threadIdx.x;
+  cpos += (size_t)blockIdx.x * 2 * C;   // blockIdx.x = image of a batched launch
+  cand += (size_t)blockIdx.x * C;
+  out += (size_t)blockIdx.x * top_k;
+  if (n_out) n_out += blockIdx.x;
+  const bool act = lane < C;
+  const float pr = act ? cpos[2 * lane] / (float)h : 0.0f;
+  const float pc = act ? cpos[2 * lane + 1] / (float)h : 0.0f;
+  const long long tk = act ? cand[lane] : 0;
+  auto dist = [&](float qr, float qc) {
+    const float dr = pr - qr, dc = pc - qc;
+    return sqrt_rn(dr * dr + dc * dc);
+  };
+  // 1) furthest pair: the pairs (lane, j > lane) in j order with strict '>' (first wins)
+  float best = -1.0f;
+  int brank = 0x7fffffff;
+  for (int j = 1; j < C; ++j) {
+    const float qr = lane_f(pr, j), qc = lane_f(pc, j);
+    if (act && j > lane) {
+      const float d = dist(qr, qc);
+      if (d > best) { best = d; brank = lane * C + j; }
+    }
+  }
+  fps_wave_best(best, brank);
+  long long mine = -1;   // lane q: the q-th selected token
+  int nsel = 0;
+  float dm = INFINITY;
+  bool nan_seen = false, taken = false;
+  auto add = [&](int s) {   // candidate s joins the selected set
+    const long long ts = lane_ll(tk, s);
+    const float qr = lane_f(pr, s), qc = lane_f(pc, s);
+    if (lane == nsel) mine = ts;
+    ++nsel;
+    taken |= tk == ts;
+    const float d = dist(qr, qc);
+    nan_seen |= isnan(d);
+    dm = fminf(dm, d);
+  };
+  if (brank != 0x7fffffff) {
+    add(brank / C);
+    add(brank % C);
+  }
+  // 2) greedy max-min additions (top_k − 2 rounds), candidates skipped if their token is selected
+  for (int round = 0; round < top_k - 2 && nsel >= 2; ++round) {
+    float bd = -1.0f;
+    int bi = 0x7fffffff;
+    if (act && !taken) {
+      const float v = nan_seen ? NAN : dm;   // torch.min propagates NaN
+      if (v > bd) { bd = v; bi = lane; }
+    }
+    fps_wave_best(bd, bi);
+    if (bi == 0x7fffffff) break;   // nothing left: the later rounds find nothing either
+    add(bi);
+  }
+  if (lane < top_k) out[lane] = mine;
+  if (lane == 0 && n_out) *n_out = nsel;
+}
+
+void launch_fps(const float* cpos, const long long* cand, int nb, int n_cand, int h, int top_k, long long* out,
+                int* n_out, hipStream_t st) {
+  if (n_cand <= 64 && top_k <= 64) {
+    hipLaunchKernelGGL(fps_wave_kernel, dim3(nb), dim3(64), 0, st, cpos, cand, n_cand, h, top_k, out, n_out);
+  } else {
+    const size_t lds = (size_t)n_cand * 8 + (size_t)n_cand * 8 + (size_t)top_k * 8 + (size_t)top_k * 8;
+    hipLaunchKernelGGL(fps_kernel, dim3(nb), dim3(64), lds, st, cpos, cand, n_cand, h, top_k, out, n_out);
+  }
 }
 
 // ------------------------------------------------------------------------------------ losses
@@ -1021,9 +1151,8 @@ extern "C" int skp_fps_batch(const float* maps, int nb, int T, int h, int w, con
   hipLaunchKernelGGL(argmax_kernel, dim3(nb * n_cand), dim3(kRowThreads), 0, st, maps, T, h, w, cand, n_cand, cpos,
                      (long long*)nullptr);
   SKP_LAUNCH_CHECK();
-  const size_t lds = (size_t)n_cand * 8 + (size_t)n_cand * 8 + (size_t)top_k * 8 + (size_t)top_k * 8;
-  SKP_CHECK_ARG(lds <= 64 * 1024, "fps LDS budget exceeded");
-  hipLaunchKernelGGL(fps_kernel, dim3(nb), dim3(64), lds, st, cpos, cand, n_cand, h, top_k, out, n_out);
+  SKP_CHECK_ARG((size_t)n_cand * 16 + (size_t)top_k * 16 <= 64 * 1024, "fps LDS budget exceeded");
+  launch_fps(cpos, cand, nb, n_cand, h, top_k, out, n_out, st);
   SKP_LAUNCH_CHECK();
   return SKP_OK;
 }
@@ -1040,12 +1169,10 @@ extern "C" int skp_fps_keys_batch(const double* keys, const float* maps, int nb,
   SKP_CHECK_ARG(nb <= 65535 && n_cand <= 65535, "grid too large");
   hipStream_t st = as_stream(stream);
   float* cpos = reinterpret_cast<float*>(workspace);
-  hipLaunchKernelGGL(rank_argmax_kernel, dim3(n_cand, nb), dim3(kRowThreads), (size_t)T * sizeof(double), st, keys, T,
-                     n_cand, maps, h, w, cand, cpos);
+  hipLaunchKernelGGL(rank_argmax_kernel, dim3(T, nb), dim3(kRankArgThreads), 0, st, keys, T, n_cand, maps, h, w, cand, cpos);
   SKP_LAUNCH_CHECK();
-  const size_t lds = (size_t)n_cand * 8 + (size_t)n_cand * 8 + (size_t)top_k * 8 + (size_t)top_k * 8;
-  SKP_CHECK_ARG(lds <= 64 * 1024, "fps LDS budget exceeded");
-  hipLaunchKernelGGL(fps_kernel, dim3(nb), dim3(64), lds, st, cpos, cand, n_cand, h, top_k, out, n_out);
+  SKP_CHECK_ARG((size_t)n_cand * 16 + (size_t)top_k * 16 <= 64 * 1024, "fps LDS budget exceeded");
+  launch_fps(cpos, cand, nb, n_cand, h, top_k, out, n_out, st);
   SKP_LAUNCH_CHECK();
   return SKP_OK;
 }

@@ -276,6 +276,27 @@ def test_fps_keys_batch_equals_rank_then_fps(nb, Tn, R, n_cand, top_k):
     assert torch.equal(cand_e, cand_e0) and torch.equal(sel_e, sel_e0) and torch.equal(n_e, n_e0)
 
 
+@pytest.mark.parametrize("n_cand,top_k", [(25, 10), (64, 64), (80, 70), (2, 2)])
+def test_fps_both_kernels_vs_oracle(n_cand, top_k):
+    """skp_fps: the one-lane-per-candidate kernel (r06, C ≤ 64 and top_k ≤ 64: running minima in
+    registers) and the LDS kernel it falls back to (C = 80) against the oracle's FPS
+    (ptp_utils.py:115-159): candidates with duplicated tokens, maps with tied argmax positions, all
+    rounds run (top_k = C − duplicates) — bit-exact picks and counts."""
+    from stablekeypoints_amd import ops
+    rng = np.random.default_rng(n_cand * 100 + top_k)
+    maps = rng.random((120, 24, 24), dtype=np.float32)
+    maps[7] = maps[9]                       # tied positions
+    maps[11, 3, 3] = maps[11].max() + 1.0   # edge-ish positions
+    cand = rng.choice(120, size=n_cand, replace=False).astype(np.int64)
+    if n_cand > 4:
+        cand[3] = cand[1]                   # a duplicated token: skipped once selected
+    sel, n = ops.furthest_point_sampling(T(maps), top_k, torch.from_numpy(cand).to(DEV))
+    ref = O.furthest_point_sampling(maps, top_k, cand)
+    k = int(n.item())
+    assert k == len(ref) and np.array_equal(N(sel)[:k], ref)
+    assert (N(sel)[k:] == -1).all()
+
+
 def test_entropy_sort_batch_equals_per_image():
     """ops.entropy_sort_batch (the entropies of all images' rows in one launch, the per-image
     top-k in one skp_topk_keys launch: the batched `entropy` strategy of find_best_indices,

@@ -141,6 +141,15 @@ def main():
             res[name] = timed(lambda: ops.find_top_k_gaussian_batch(m4, 25, sigma=2.0, num_subjects=ns), args.iters)
             res[name + "_GBs"] = m4.numel() * 4 / (res[name] * 1e-3) / 1e9 / 1e3
             del m4
+        elif name in ("sel4", "sel4_r05"):   # a pass's selection chain: 4 images' KL keys, 25 candidates, FPS 10
+            m4 = torch.rand(4, N, R, R, device=dev, generator=g) ** 8
+            mt4 = torch.rand(4, N, R, R, device=dev, generator=g) ** 8
+            if name == "sel4":   # r06: KL → rank + argmax → FPS
+                fn = lambda: ops.gaussian_fps_batch(m4, mt4, 25, 10, sigma=2.0)
+            else:                # r05: KL → rank → argmax → FPS
+                fn = lambda: ops.furthest_point_sampling_batch(mt4, 10, ops.find_top_k_gaussian_batch(m4, 25, sigma=2.0))
+            res[name] = timed(fn, args.iters)
+            del m4, mt4
         elif name == "bwd16_dense":
             res[name] = timed(lambda: ops.capture_bwd(zs[16], 16, R, attn[16]), args.iters)
     agg_bytes = (4 * H * R * R * N + N * R * R) * 4
