@@ -278,7 +278,10 @@ __global__ __launch_bounds__(256) void sel_adjv_kernel(SelSmall t, const float* 
     Hs[e] = hb[(size_t)yy * smax + j];
   }
   for (int y = threadIdx.x; y < R; y += blockDim.x) {
-    for (int i = 0; i < S; ++i) {
+    // the rows i whose range holds y lie within [lo(y) − 2, lo(y) + 3] (lo: the first tap, before
+    // clamping); the scan covers one more each side
+    const int lo = bicubic_taps(y, S, R).lo;
+    for (int i = max(0, lo - 3); i <= min(S - 1, lo + 4); ++i) {
       int y0, y1;
       adj_range(i, S, R, y0, y1);
       if (y >= y0 && y <= y1) Ab[i * BW + (y - y0)] = 0.0f;
@@ -298,6 +301,7 @@ __global__ __launch_bounds__(256) void sel_adjv_kernel(SelSmall t, const float* 
     adj_range(i, S, R, y0, y1);
     const float* Ai = Ab + i * BW - y0;
     float acc = 0.0f;
+#pragma unroll 4
     for (int yy = y0; yy <= y1; ++yy) acc = fmaf(Ai[yy], Hs[yy * S + j], acc);
     es[bk * (size_t)S * S + e] = acc;
   }
