@@ -566,6 +566,12 @@ constexpr int maps_pxw(int qpl) { return (32 / qpl) < 4 ? 4 : ((32 / qpl) > 16 ?
 #ifndef SKP_MAPS_PRIO
 #define SKP_MAPS_PRIO 1   // s_setprio level of the staging phase (0: off; 1, 2, 3 measured 972, 983, 982 vs 1003 us)
 #endif
+#ifndef SKP_MAPS_PROBE
+// timing probes (A/B builds via tools/build_variant.sh only; r06: staging alone 417 µs, pixels
+// alone 605 µs, both 900 µs at the bench shape, profiles/r06s_maps_fwd_probes.txt): 1 = the
+// staging without its z_low loads, 2 = no pixel work
+#define SKP_MAPS_PROBE 0
+#endif
 #ifndef SKP_MAPS_NT
 // 1: the maps and stats leave with non-temporal stores, so the 296 MB write stream does not evict
 // the z_low rows the XCD's other workgroups are about to read: 975 vs 994 µs, FETCH_SIZE 823 vs
@@ -684,7 +690,7 @@ void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nc
             f4 a[VPT][4];
   #pragma unroll
             for (int k = 0; k < VPT; ++k) {
-              if (e0 + k * kMapThreads < tot && q < nq) {
+              if (e0 + k * kMapThreads < tot && q < nq && SKP_MAPS_PROBE != 1) {   // timing probe 1: no z_low loads
                 const unsigned o = ob + k * obs;
                 a[k][0] = *reinterpret_cast<gcf4*>(reinterpret_cast<gcc*>(r0) + o);
                 a[k][1] = *reinterpret_cast<gcf4*>(reinterpret_cast<gcc*>(r1) + o);
@@ -697,7 +703,9 @@ void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nc
               const int e = e0 + k * kMapThreads;
               if (e < tot) {
                 f4 v = (f4)kPadLogit;
-                if (q < nq) {
+                if (SKP_MAPS_PROBE == 1) {
+                  v = (f4)wy[0];
+                } else if (q < nq) {
                   v = a[k][0] * wy[0];
                   v = __builtin_elementwise_fma(a[k][1], (f4)wy[1], v);
                   v = __builtin_elementwise_fma(a[k][2], (f4)wy[2], v);
@@ -730,7 +738,7 @@ void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nc
         // this (head, row, chunk)'s stats run: a uniform base, lane offsets xl
         auto* st = cl.stats[l] ? uniform_ptr(reinterpret_cast<f2v*>(cl.stats[l]) + ((size_t)bh * R + y) * R + x0) : nullptr;
   #pragma unroll
-        for (int g = 0; g < G; ++g) {
+        for (int g = 0; g < (SKP_MAPS_PROBE == 2 ? 0 : G); ++g) {   // timing probe 2: no pixel work
           const int xl = wid * PXW + 4 * g + row;              // pixel of this 16-lane row
           const int xr = min(xl, np - 1);                        // past-the-edge rows redo a valid one
           const float4 w = tw[xr];
