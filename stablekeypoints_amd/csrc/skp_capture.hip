@@ -659,6 +659,11 @@ void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nc
       for (int h = 0; h < H; ++h) {
         const int it = l * H + h;
         const int bh = b * H + h;
+        // the lane-derived offsets are recomputed per slab from an opaque copy of the thread index
+        // (hoisted out of the head loop they held VGPRs across it: 898–901 vs 909–911 µs, r06s)
+        int tl = tid;
+        asm volatile("" : "+v"(tl));
+        const int lanel = tl & 63, widl = tl >> 6, rowl = lanel >> 4, lil = lanel & 15;
   #if SKP_MAPS_PRIO
         __builtin_amdgcn_s_setprio(SKP_MAPS_PRIO);   // the staging's loads ahead of the other workgroup's pixels
   #endif
@@ -667,8 +672,8 @@ void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nc
         float* Vb = V + (it & 1) * vstride;
         const float* zb = cl.z[l] + (size_t)bh * s * s * N;
         if (vec) {
-          // V[jj][n] = Σ_k wy_k · z[iy_k][c0 + jj][n]: thread element e = tid + k·threads, lane
-          // offset o = jj·nq + q (a 32-bit offset from each uniform row base)
+          // V[jj][n] = Σ_k wy_k · z[iy_k][c0 + jj][n]: thread element e = tl + k·threads, lane
+          // offset o = jj·nq + q (a 32-bit offset from each uniform rowl base)
           const auto* r0 = uniform_ptr(reinterpret_cast<const f4*>(zb + ro[0]));
           const auto* r1 = uniform_ptr(reinterpret_cast<const f4*>(zb + ro[1]));
           const auto* r2 = uniform_ptr(reinterpret_cast<const f4*>(zb + ro[2]));
@@ -676,8 +681,8 @@ void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nc
           f4* V4 = reinterpret_cast<f4*>(Vb);
           constexpr unsigned JS = kMapThreads / Npq;   // columns per thread step (4 at 8 waves, QPL 8)
           static_assert(kMapThreads % Npq == 0, "thread step must cover whole columns");
-          const unsigned q = (unsigned)tid % Npq;
-          unsigned ob = (((unsigned)tid / Npq) * nq + q) * 16u;   // byte offset (saddr + 32-bit voffset loads)
+          const unsigned q = (unsigned)tl % Npq;
+          unsigned ob = (((unsigned)tl / Npq) * nq + q) * 16u;   // byte offset (saddr + 32-bit voffset loads)
           const unsigned obs = JS * nq * 16u;
           using gcf4 = const __attribute__((address_space(1))) f4;
           using gcc = const __attribute__((address_space(1))) char;
@@ -686,7 +691,7 @@ void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nc
 #endif
           constexpr int VPT = SKP_MAPS_VPT;
   #pragma unroll 1
-          for (int e0 = tid; e0 < tot; e0 += VPT * kMapThreads, ob += VPT * obs) {
+          for (int e0 = tl; e0 < tot; e0 += VPT * kMapThreads, ob += VPT * obs) {
             f4 a[VPT][4];
   #pragma unroll
             for (int k = 0; k < VPT; ++k) {
@@ -717,7 +722,7 @@ void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nc
           }
         } else {
   #pragma unroll 1
-          for (int e = tid; e < nc * Np; e += kMapThreads) {
+          for (int e = tl; e < nc * Np; e += kMapThreads) {
             const int jj = e / Np, n = e - jj * Np;
             float v = kPadLogit;
             if (n < N) {
@@ -734,12 +739,12 @@ void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nc
         __builtin_amdgcn_s_setprio(0);
   #endif
         __syncthreads();
-        const f4* V4 = reinterpret_cast<const f4*>(Vb) + li;
-        // this (head, row, chunk)'s stats run: a uniform base, lane offsets xl
+        const f4* V4 = reinterpret_cast<const f4*>(Vb) + lil;
+        // this (head, rowl, chunk)'s stats run: a uniform base, lane offsets xl
         auto* st = cl.stats[l] ? uniform_ptr(reinterpret_cast<f2v*>(cl.stats[l]) + ((size_t)bh * R + y) * R + x0) : nullptr;
   #pragma unroll
         for (int g = 0; g < (SKP_MAPS_PROBE == 2 ? 0 : G); ++g) {   // timing probe 2: no pixel work
-          const int xl = wid * PXW + 4 * g + row;              // pixel of this 16-lane row
+          const int xl = widl * PXW + 4 * g + rowl;              // pixel of this 16-lane rowl
           const int xr = min(xl, np - 1);                        // past-the-edge rows redo a valid one
           const float4 w = tw[xr];
           const int4 ti = tiw[xr];
@@ -775,7 +780,7 @@ void capture_maps_kernel(CapLayers cl, int L, int B, int H, int N, int R, int nc
           const float inv = __builtin_amdgcn_rcpf(row16_sum((sv.x + sv.y) + (sv.z + sv.w)));
   #pragma unroll
           for (int c = 0; c < QPL; ++c) acc[g][c] = __builtin_elementwise_fma(zc[c], (f4)inv, acc[g][c]);
-          if (st && li == 0 && xl < np) {
+          if (st && lil == 0 && xl < np) {
             const f2v mi = {m, inv};
             SKP_MAPS_ST(st[(unsigned)xl], mi);
           }
